@@ -1,0 +1,65 @@
+// gc_engine.h -- the gc_graph handle (internal; the ABI only sees an opaque pointer).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <string>
+#include <vector>
+
+#include "gcolor.h"
+#include "gc_launch.h"
+
+struct gc_graph {
+    int device = 0;
+    long long n = 0, nnz = 0, maxdeg = 0;
+    uint32_t flags = 0;
+    // graph (HBM-resident)
+    long long* rp = nullptr;
+    int* col = nullptr;
+    int* deg = nullptr;
+    long long* trp = nullptr;  // in-neighbour CSR; == rp/col when symmetric
+    int* tcol = nullptr;
+    // run state
+    int* color = nullptr;
+    int* cround = nullptr;
+    ull* key = nullptr;
+    unsigned char* jp = nullptr;
+    unsigned* inF = nullptr;
+    int* F[2] = {nullptr, nullptr};
+    int* heavy = nullptr;
+    int* wide = nullptr;
+    int* und[2] = {nullptr, nullptr};
+    int* seeds[2] = {nullptr, nullptr};
+    int* ulist = nullptr;
+    int* parent = nullptr;
+    ull* best = nullptr;
+    int* vcolors = nullptr;
+    DevCtl* ctl = nullptr;
+    DevCtl* hctl = nullptr;  // pinned host mirror
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> evpool;
+    bool has_run_state = false;
+};
+
+void gc_set_error(const char* fmt, ...);
+
+#define GC_HIP(call)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            gc_set_error("%s failed at %s:%d: %s", #call, __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return GC_EHIP;                                                                   \
+        }                                                                                     \
+    } while (0)
+
+int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
+int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
+void gc_free_all(gc_graph* g);
+GcDevView gc_view(const gc_graph* g);
+static inline int gc_grid_for_waves(long long items, int cap = 2048) {
+    long long chunks = (items + GC_WAVE - 1) / GC_WAVE;
+    long long blocks = (chunks + GC_WAVES_PER_BLOCK - 1) / GC_WAVES_PER_BLOCK;
+    if (blocks < 1) blocks = 1;
+    if (blocks > cap) blocks = cap;
+    return (int)blocks;
+}

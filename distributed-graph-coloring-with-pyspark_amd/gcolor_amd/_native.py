@@ -1,0 +1,98 @@
+"""ctypes binding of libgcolor.so (the C-ABI declared in include/gcolor.h).
+
+The library is built in-tree (``make -C distributed-graph-coloring-with-pyspark_amd/csrc``
+or ``__graft_entry__.build()``) and loaded from ``gcolor_amd/lib/libgcolor.so``.  There is
+no fallback: if the library is missing or no GPU is present the calls fail loudly.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libgcolor.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+GC_OK, GC_FAILED, GC_STALLED = 0, 1, 2
+GC_EINVAL, GC_EHIP, GC_ENOMEM, GC_ERCCL, GC_EROUNDS = -1, -2, -3, -4, -5
+GC_GRAPH_SYMMETRIC = 1
+GC_VARIANT_A, GC_VARIANT_B = 0, 1
+GC_NKERNELS = 8
+KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "validate", "other"]
+
+# Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
+EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
+           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_color", "gc_validate",
+           "gc_gen_uniform", "gc_last_error", "gc_device_count", "gc_set_device"]
+
+
+class GcOptions(ctypes.Structure):
+    _fields_ = [("variant", ctypes.c_int32), ("e1", ctypes.c_int32), ("num_colors", ctypes.c_int64),
+                ("kernel_timing", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+_I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+class GcStats(ctypes.Structure):
+    _fields_ = [("rounds", ctypes.c_int64), ("fail_round", ctypes.c_int64), ("fail_count", ctypes.c_int64),
+                ("reseeds", ctypes.c_int64), ("max_color", ctypes.c_int64), ("jp_sweeps", ctypes.c_int64),
+                ("device_ms", ctypes.c_double),
+                ("k_launches", ctypes.c_int64 * GC_NKERNELS), ("k_ms", ctypes.c_double * GC_NKERNELS),
+                ("k_bytes", ctypes.c_double * GC_NKERNELS),
+                ("round_cap", ctypes.c_int64), ("round_U", _I64P), ("round_F", _I64P),
+                ("round_maxmex", _I64P), ("round_accepted", _I64P), ("round_seeds", _I64P)]
+
+
+class GcolorError(RuntimeError):
+    def __init__(self, fn, status, msg):
+        super().__init__(f"{fn} failed (status {status}): {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def build(jobs=8):
+    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"], check=True)
+
+
+def load():
+    """Load libgcolor.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P, I32, I64, U32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "gc_graph_create": ([P, P, I64, I64, U32, PP], ctypes.c_int),
+        "gc_graph_create_device": ([P, P, I64, I64, U32, PP], ctypes.c_int),
+        "gc_graph_create_rmat": ([I32, I32, ctypes.c_double, ctypes.c_double, ctypes.c_double, U64, PP], ctypes.c_int),
+        "gc_graph_create_mesh": ([I64, I64, I64, PP], ctypes.c_int),
+        "gc_graph_destroy": ([P], None),
+        "gc_graph_info": ([P, _I64P, _I64P, _I64P, ctypes.POINTER(U32)], ctypes.c_int),
+        "gc_graph_export": ([P, P, P], ctypes.c_int),
+        "gc_color": ([P, ctypes.POINTER(GcOptions), P, P, ctypes.POINTER(GcStats)], ctypes.c_int),
+        "gc_validate": ([P, P, _I64P, _I64P], ctypes.c_int),
+        "gc_gen_uniform": ([I64, I32, U64, P, P, I64, _I64P], ctypes.c_int),
+        "gc_last_error": ([], ctypes.c_char_p),
+        "gc_device_count": ([ctypes.POINTER(I32)], ctypes.c_int),
+        "gc_set_device": ([I32], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(fn_name, status, ok=(GC_OK,)):
+    if status in ok:
+        return status
+    msg = _lib.gc_last_error().decode(errors="replace") if _lib is not None else ""
+    raise GcolorError(fn_name, status, msg)

@@ -1,0 +1,198 @@
+"""Device-resident graphs and the colouring / validation entry points (C-ABI wrappers).
+
+``DeviceGraph`` replaces the reference's persisted RDD of ``Node`` objects
+(coloring.py:201-209) with an HBM-resident CSR; ``DeviceGraph.color`` replaces
+``graph_coloring(graph_rdd, numOfColors, sc)`` (coloring.py:73, variant B
+coloring_optimized.py:70) and ``DeviceGraph.validate`` replaces
+``validate_graph_coloring`` (coloring.py:149-162).  All compute runs in libgcolor.so.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as nat
+
+ROUND_CAP = 1 << 17
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def is_symmetric(rp, col):
+    """True iff (v,u) listed <=> (u,v) listed (as sets); host-side, small graphs."""
+    n = len(rp) - 1
+    if n == 0:
+        return True
+    src = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+    dst = col.astype(np.int64)
+    a = np.unique(src * n + dst)
+    b = np.unique(dst * n + src)
+    return a.shape == b.shape and bool(np.array_equal(a, b))
+
+
+@dataclass
+class ColorResult:
+    status: int
+    colors: np.ndarray
+    colored_round: np.ndarray
+    rounds: int
+    round_U: np.ndarray
+    round_F: np.ndarray
+    round_maxmex: np.ndarray
+    round_accepted: np.ndarray
+    round_seeds: np.ndarray
+    fail_round: int
+    fail_count: int
+    reseeds: int
+    max_color: int
+    jp_sweeps: int
+    device_ms: float
+    kernels: dict = field(default_factory=dict)
+
+    @property
+    def ok(self):
+        return self.status == nat.GC_OK
+
+    @property
+    def num_colors(self):
+        return self.max_color + 1
+
+    @property
+    def balg_bytes(self):
+        """SURVEY.md §8d algorithmic bytes of the colouring (validate pass excluded)."""
+        return sum(k["bytes"] for k in self.kernels.values())
+
+
+class DeviceGraph:
+    """An HBM-resident CSR graph (file positions; adjacency exactly as listed)."""
+
+    def __init__(self, handle):
+        self._lib = nat.load()
+        self._h = handle
+        n, nnz, md = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        fl = ctypes.c_uint32()
+        nat.check("gc_graph_info", self._lib.gc_graph_info(self._h, ctypes.byref(n), ctypes.byref(nnz),
+                                                            ctypes.byref(md), ctypes.byref(fl)))
+        self.n, self.nnz, self.max_degree, self.flags = n.value, nnz.value, md.value, fl.value
+
+    # ---- construction -------------------------------------------------------------------
+    @classmethod
+    def from_csr(cls, rp, col, symmetric=None):
+        lib = nat.load()
+        rp = np.ascontiguousarray(rp, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        n = rp.shape[0] - 1
+        if symmetric is None:
+            symmetric = is_symmetric(rp, col) if col.shape[0] <= 20_000_000 else False
+        h = ctypes.c_void_p()
+        nat.check("gc_graph_create", lib.gc_graph_create(_ptr(rp), _ptr(col), n, col.shape[0],
+                                                         nat.GC_GRAPH_SYMMETRIC if symmetric else 0,
+                                                         ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def rmat(cls, scale, edge_factor=16, a=0.57, b=0.19, c=0.19, seed=1):
+        lib = nat.load()
+        h = ctypes.c_void_p()
+        nat.check("gc_graph_create_rmat", lib.gc_graph_create_rmat(scale, edge_factor, a, b, c, seed, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def mesh(cls, nx, ny, nz):
+        lib = nat.load()
+        h = ctypes.c_void_p()
+        nat.check("gc_graph_create_mesh", lib.gc_graph_create_mesh(nx, ny, nz, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def uniform(cls, n, max_degree, seed=42):
+        rp, col = uniform_csr(n, max_degree, seed)
+        return cls.from_csr(rp, col, symmetric=True)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gc_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def symmetric(self):
+        return bool(self.flags & nat.GC_GRAPH_SYMMETRIC)
+
+    def export(self):
+        rp = np.empty(self.n + 1, np.int64)
+        col = np.empty(max(self.nnz, 1), np.int32)
+        nat.check("gc_graph_export", self._lib.gc_graph_export(self._h, _ptr(rp), _ptr(col)))
+        return rp, col[: self.nnz]
+
+    # ---- hot path -------------------------------------------------------------------------
+    def color(self, variant="A", num_colors=None, e1=True, kernel_timing=False, want_rounds=True,
+              want_colors=True):
+        """graph_coloring(graph, numOfColors): returns ColorResult.  ``num_colors=None``
+        is unbounded; on a bounded failure ``colors`` is the round-start snapshot."""
+        opt = nat.GcOptions(variant=nat.GC_VARIANT_A if variant == "A" else nat.GC_VARIANT_B,
+                            e1=1 if e1 else 0, num_colors=-1 if num_colors is None else int(num_colors),
+                            kernel_timing=1 if kernel_timing else 0, reserved=0)
+        st = nat.GcStats()
+        cap = ROUND_CAP if want_rounds else 0
+        rb = {k: np.zeros(max(cap, 1), np.int64) for k in ("U", "F", "maxmex", "accepted", "seeds")}
+        if want_rounds:
+            st.round_cap = cap
+            for k, arr in rb.items():
+                setattr(st, "round_" + k, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+        colors = np.empty(self.n, np.int32) if want_colors else None
+        cround = np.empty(self.n, np.int32) if want_colors else None
+        status = self._lib.gc_color(self._h, ctypes.byref(opt), _ptr(colors), _ptr(cround), ctypes.byref(st))
+        nat.check("gc_color", status, ok=(nat.GC_OK, nat.GC_FAILED, nat.GC_STALLED))
+        r = st.rounds
+        kernels = {}
+        for i, name in enumerate(nat.KERNEL_CLASSES):
+            kernels[name] = {"launches": int(st.k_launches[i]), "ms": float(st.k_ms[i]), "bytes": float(st.k_bytes[i])}
+        return ColorResult(status=status, colors=colors, colored_round=cround, rounds=r,
+                           round_U=rb["U"][:r].copy() if want_rounds else None,
+                           round_F=rb["F"][:r].copy() if want_rounds else None,
+                           round_maxmex=rb["maxmex"][:r].copy() if want_rounds else None,
+                           round_accepted=rb["accepted"][:r].copy() if want_rounds else None,
+                           round_seeds=rb["seeds"][:r].copy() if want_rounds else None,
+                           fail_round=st.fail_round, fail_count=st.fail_count, reseeds=st.reseeds,
+                           max_color=st.max_color, jp_sweeps=st.jp_sweeps, device_ms=st.device_ms,
+                           kernels=kernels)
+
+    def validate(self, colors=None):
+        """validate_graph_coloring counts on the device: (#uncoloured, #conflicting listed pairs).
+        ``colors=None`` validates the last colouring still resident on the device."""
+        u, c = ctypes.c_int64(), ctypes.c_int64()
+        arr = None if colors is None else np.ascontiguousarray(colors, dtype=np.int32)
+        nat.check("gc_validate", self._lib.gc_validate(self._h, _ptr(arr), ctypes.byref(u), ctypes.byref(c)))
+        return u.value, c.value
+
+
+def uniform_csr(n, max_degree, seed=42):
+    """Native graph.py:30-43 process (splitmix64 stream) on the host, as CSR."""
+    lib = nat.load()
+    rp = np.empty(n + 1, np.int64)
+    col = np.empty(max(n * max_degree, 1), np.int32)
+    nnz = ctypes.c_int64()
+    nat.check("gc_gen_uniform", lib.gc_gen_uniform(n, max_degree, seed, _ptr(rp), _ptr(col), col.shape[0],
+                                                   ctypes.byref(nnz)))
+    return rp, col[: nnz.value].copy()
+
+
+def device_count():
+    lib = nat.load()
+    c = ctypes.c_int32()
+    nat.check("gc_device_count", lib.gc_device_count(ctypes.byref(c)))
+    return c.value

@@ -1,0 +1,138 @@
+/*
+ * gcolor.h -- C-ABI of the MI355X-native graph-colouring engine (libgcolor.so).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference exposes no
+ * FFI; its in-process surface is two Python functions that this ABI replaces:
+ *
+ *   graph_coloring(graph_rdd, numOfColors, sc) -> (bool, rdd)   /root/reference/coloring.py:73
+ *        (variant B: /root/reference/coloring_optimized.py:70)     -> gc_color()
+ *   validate_graph_coloring(graph_rdd) -> bool                     /root/reference/coloring.py:149
+ *                                                                   -> gc_validate()
+ *   the Spark data model (Node objects in an RDD, node.py:1-18,     -> gc_graph (device CSR)
+ *        graph.py:15-28, coloring.py:201-209)
+ *   Graph(node_count, max_degree) generator, graph.py:30-43        -> gc_gen_uniform()
+ *
+ * Conventions: every function is extern "C", never throws, returns an int status
+ * (GC_OK == 0) unless it returns void/const char*; host arrays are caller-owned;
+ * device memory is owned by the gc_graph handle.  One handle per calling thread.
+ * Vertices are FILE POSITIONS 0..n-1 (the caller maps JSON ids); adjacency lists are
+ * kept exactly as listed (duplicates, self-loops and asymmetric lists are legal and
+ * keep the reference's directed semantics).
+ */
+#ifndef GCOLOR_H
+#define GCOLOR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define GC_OK 0
+#define GC_FAILED 1    /* bounded attempt: a proposer's mex >= num_colors (coloring.py:104-108) */
+#define GC_STALLED 2   /* zero proposers, uncoloured vertices left, E1 off (coloring.py:93-95)  */
+#define GC_EINVAL (-1)
+#define GC_EHIP (-2)
+#define GC_ENOMEM (-3)
+#define GC_ERCCL (-4)
+#define GC_EROUNDS (-5)
+
+/* ---- graph -------------------------------------------------------------------------- */
+typedef struct gc_graph gc_graph;
+
+#define GC_GRAPH_SYMMETRIC 1u /* caller asserts (v,u) listed <=> (u,v) listed: no transpose kept */
+
+/* Copy a host CSR (row_ptr int64[n+1], col int32[nnz] of positions) to the device.
+   Replaces: sc.parallelize(graph.nodes)...persist(), coloring.py:201-209.           */
+int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t nnz,
+                    uint32_t flags, gc_graph** out);
+/* Same, from device pointers already resident in HBM (copied device-to-device).      */
+int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
+                           uint32_t flags, gc_graph** out);
+/* Device-side synthetic generators (no host round trip):
+   R-MAT (a,b,c; d = 1-a-b-c), 2^scale vertices, edge_factor*2^scale generated edges,
+   self-loops dropped, symmetrised, de-duplicated, rows sorted, no vertex permutation. */
+int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a, double b, double c,
+                         uint64_t seed, gc_graph** out);
+/* 3-D 7-point mesh, id = x + nx*(y + ny*z), neighbours in order -x,+x,-y,+y,-z,+z.   */
+int gc_graph_create_mesh(int64_t nx, int64_t ny, int64_t nz, gc_graph** out);
+void gc_graph_destroy(gc_graph* g);
+int gc_graph_info(const gc_graph* g, int64_t* n, int64_t* nnz, int64_t* max_degree, uint32_t* flags);
+/* Copy the device CSR back (row_ptr int64[n+1], col int32[nnz]); either may be NULL.  */
+int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col);
+
+/* ---- colouring ---------------------------------------------------------------------- */
+#define GC_VARIANT_A 0 /* coloring.py (default)           */
+#define GC_VARIANT_B 1 /* coloring_optimized.py           */
+
+typedef struct gc_options {
+    int32_t variant;       /* GC_VARIANT_A / GC_VARIANT_B                                  */
+    int32_t e1;            /* 1: re-seed on a zero-proposer round (extension E1)           */
+    int64_t num_colors;    /* k of graph_coloring(graph, k); < 0 = unbounded               */
+    int32_t kernel_timing; /* 1: bracket every launch with HIP events (per-kernel stats)   */
+    int32_t reserved;
+} gc_options;
+
+/* kernel classes reported in gc_stats.k_* */
+#define GC_K_INIT 0
+#define GC_K_PROPOSE 1
+#define GC_K_RESOLVE 2
+#define GC_K_SWEEP 3
+#define GC_K_COMMIT 4
+#define GC_K_RESEED 5
+#define GC_K_VALIDATE 6
+#define GC_K_OTHER 7
+#define GC_NKERNELS 8
+
+typedef struct gc_stats {
+    /* outputs */
+    int64_t rounds;        /* entries written to the per-round arrays                     */
+    int64_t fail_round;    /* bounded attempt: round that failed, else -1                 */
+    int64_t fail_count;    /* #proposers with mex >= k in that round                      */
+    int64_t reseeds;       /* E1 seeds planted                                            */
+    int64_t max_color;     /* max colour of the final state (-1: none)                    */
+    int64_t jp_sweeps;     /* Jones-Plassmann sweeps beyond the first, summed over rounds */
+    double device_ms;      /* HIP-event time of the whole colouring (resident CSR in)     */
+    int64_t k_launches[GC_NKERNELS];
+    double k_ms[GC_NKERNELS];    /* valid when kernel_timing = 1                           */
+    double k_bytes[GC_NKERNELS]; /* algorithmic bytes per kernel class     */
+    /* optional caller buffers (may be NULL), capacity round_cap */
+    int64_t round_cap;
+    int64_t* round_U;      /* uncoloured at round start (coloring.py:89 transcript)        */
+    int64_t* round_F;      /* proposers                                                   */
+    int64_t* round_maxmex; /* max candidate colour proposed (-1 if none)                  */
+    int64_t* round_accepted;
+    int64_t* round_seeds;  /* E1 seeds planted in the round                               */
+} gc_stats;
+
+/* Colour the graph.  colors_out (host int32[n], may be NULL): final state, -1 =
+   uncoloured; on GC_FAILED it is the state at the START of the failing round, exactly
+   what graph_coloring returns with False.  colored_round_out (host int32[n], may be
+   NULL): round at whose start each vertex was coloured (0 = init/seed, -1 = never). */
+int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* colored_round_out,
+             gc_stats* stats);
+
+/* validate_graph_coloring counts: #uncoloured and the directed count of listed pairs
+   (v, u in N(v)) with colour[u] == colour[v] (self-loops and duplicates count, as in
+   coloring.py:157-158).  colors == NULL validates the device result of the last
+   gc_color on this handle without a host round trip.                                 */
+int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts);
+
+/* ---- host-side generator ------------------------------------------------------------ */
+/* The graph.py:30-43 process (per node: target = U{0..D}; draw random partners, keep
+   those that are not self, not yet adjacent and below D) with a splitmix64 stream
+   instead of Python's MT19937.  row_ptr int64[n+1]; col capacity col_cap (n*D is
+   always enough); *nnz_out receives the entry count.                                 */
+int gc_gen_uniform(int64_t n, int32_t max_degree, uint64_t seed, int64_t* row_ptr, int32_t* col,
+                   int64_t col_cap, int64_t* nnz_out);
+
+/* ---- misc ----------------------------------------------------------------------------- */
+const char* gc_last_error(void);
+int gc_device_count(int32_t* count);
+int gc_set_device(int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCOLOR_H */

@@ -1,0 +1,59 @@
+"""Shared test helpers.
+
+`-m "not gpu"` tests run in the build container (no GPU); `-m gpu` tests run on an
+MI355X through gpurun and always exercise the HIP path through the C-ABI.
+"""
+import glob
+import gzip
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(REPO, "distributed-graph-coloring-with-pyspark_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden", "cases")
+for p in (REPO, PKG_DIR):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through gpurun)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def golden_names():
+    return sorted(os.path.basename(p)[: -len(".json.gz")] for p in glob.glob(os.path.join(GOLDEN, "*.json.gz")))
+
+
+_cache = {}
+
+
+def load_golden(name):
+    if name not in _cache:
+        with gzip.open(os.path.join(GOLDEN, name + ".json.gz"), "rt") as f:
+            _cache[name] = json.load(f)
+    return _cache[name]
+
+
+def fixture_csr(rec):
+    """(ids, adjacency-by-position, rp, col) exactly as graph.py:15-28 links them
+    (a neighbour id resolves to the LAST node carrying that id)."""
+    graph = rec["graph"]
+    ids = [g[0] for g in graph]
+    pos = {}
+    for i, vid in enumerate(ids):
+        pos[vid] = i
+    adj = [[pos[u] for u in g[1]] for g in graph]
+    rp = np.zeros(len(adj) + 1, np.int64)
+    rp[1:] = np.cumsum([len(a) for a in adj])
+    col = np.array([u for a in adj for u in a], dtype=np.int32)
+    return ids, adj, rp, col
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden

@@ -1,0 +1,228 @@
+"""GPU parity: libgcolor.so (through the C-ABI) against the CPU oracle and the golden set.
+
+Bit-exact for everything (integer work): final colours, per-round uncoloured /
+proposer / accepted counts, max proposal per round, the round each vertex was coloured,
+bounded-attempt failure round / count / snapshot, validation counts.
+"""
+import hashlib
+import io
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import fixture_csr, golden_names, load_golden
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _dg():
+    from gcolor_amd.engine import DeviceGraph
+    return DeviceGraph
+
+
+def assert_same_run(g, o, check_rounds=True):
+    assert g.status == o["status"]
+    assert np.array_equal(g.colors, o["colors"])
+    if check_rounds:
+        assert list(g.round_U) == list(o["round_U"])
+        assert list(g.round_F) == list(o["round_F"])
+        assert list(g.round_maxmex) == list(o["round_maxmex"])
+        assert list(g.round_accepted) == list(o["round_accepted"])
+        assert list(g.round_seeds) == list(o["round_seeds"])
+        assert np.array_equal(g.colored_round, o["colored_round"])
+    assert g.reseeds == o["reseeds"]
+    if g.status == oracle.FAILED:
+        assert (g.fail_round, g.fail_count) == (o["fail_round"], o["fail_count"])
+
+
+GOLD_A = [n for n in golden_names() if "load_error" not in load_golden(n)["variants"]["A"]["run"]]
+
+
+@pytest.mark.parametrize("name", GOLD_A)
+def test_golden_graphs_unbounded_and_bounded(name):
+    rec = load_golden(name)
+    ids, adj, rp, col = fixture_csr(rec)
+    with _dg().from_csr(rp, col) as dg:
+        o = oracle.c_color(rp, col, "A")
+        g = dg.color("A")
+        assert_same_run(g, o)
+        run = rec["variants"]["A"]["run"]
+        if run.get("colors") is not None:  # reference terminated: direct golden check too
+            assert list(g.colors) == run["colors"]
+            assert list(g.round_U) == run["rounds_U"]
+        for k in range(0, int(o["max_color"]) + 2):
+            assert_same_run(dg.color("A", num_colors=k), oracle.c_color(rp, col, "A", k=k))
+        assert dg.validate(g.colors) == oracle.c_validate(rp, col, o["colors"])
+        assert dg.validate() == oracle.c_validate(rp, col, o["colors"])  # device-resident result
+        s = oracle.c_color(rp, col, "A", e1=False)
+        gs = dg.color("A", e1=False)
+        assert gs.status == s["status"] and np.array_equal(gs.colors, s["colors"])
+
+
+CLI_CASES = [n for n in golden_names() if not load_golden(n)["variants"]["A"]["cli"]["hang"]
+             and not load_golden(n)["variants"]["A"]["cli"].get("exception")]
+
+
+@pytest.mark.parametrize("name", CLI_CASES)
+def test_cli_end_to_end_matches_reference(name, tmp_path):
+    from gcolor_amd import cli
+    rec = load_golden(name)
+    cli_rec = rec["variants"]["A"]["cli"]
+    gpath = tmp_path / "g.json"
+    with open(gpath, "w") as f:
+        json.dump([{"id": i, "neighbors": nb, "color": -1} for i, nb in rec["graph"]], f, indent=4)
+    argv = [a for a in cli_rec["argv"]]
+    if "--input" in argv:
+        argv[argv.index("--input") + 1] = str(gpath)
+    else:  # generation mode: seed the global RNG like make_golden did
+        argv += ["--seed", str(rec["params"]["seed"])]
+        argv[argv.index("--output-graph") + 1] = str(tmp_path / "gen.json")
+    out_c = tmp_path / "c.json"
+    argv[argv.index("--output-coloring") + 1] = str(out_c)
+    buf = io.StringIO()
+    code = 0
+    try:
+        cli.main(argv + ["--compat-output"], out=buf)
+    except SystemExit as e:
+        code = e.code
+    assert (code or 0) == cli_rec["exit"]
+    lines = buf.getvalue().splitlines()
+    norm = [("Iteration time: <t> seconds" if ln.startswith("Iteration time") else
+             "Total execution time: <t> seconds" if ln.startswith("Total execution time") else ln) for ln in lines]
+    assert norm == cli_rec["stdout"]
+    if "output_sha256" in cli_rec:
+        assert hashlib.sha256(out_c.read_bytes()).hexdigest() == cli_rec["output_sha256"]
+        # default mode writes the valid colouring instead
+        out_v = tmp_path / "v.json"
+        argv[argv.index("--output-coloring") + 1] = str(out_v)
+        cli.main(argv, out=io.StringIO())
+        data = json.loads(out_v.read_text())
+        assert [d["color"] for d in data] == rec["variants"]["A"]["run"]["colors"]
+
+
+def _random_directed(n, m, seed, selfloops=True):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    if not selfloops:
+        keep = src != dst
+        src, dst = src[keep], dst[keep]
+    order = np.argsort(src, kind="stable")
+    src, dst = src[order], dst[order]
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    return np.cumsum(rp), dst.astype(np.int32)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_directed_multigraphs_with_selfloops(seed):
+    """Asymmetric lists, duplicates and self-loops keep the reference's directed semantics."""
+    rp, col = _random_directed(3000, 9000, seed)
+    with _dg().from_csr(rp, col) as dg:
+        assert not dg.symmetric
+        assert_same_run(dg.color("A"), oracle.c_color(rp, col, "A"))
+        o = oracle.c_color(rp, col, "A")
+        for k in (1, 2, int(o["max_color"])):
+            assert_same_run(dg.color("A", num_colors=k), oracle.c_color(rp, col, "A", k=k))
+
+
+@pytest.mark.parametrize("n,d,seed", [(200_000, 16, 1), (100_000, 8, 2), (50_000, 40, 3)])
+def test_uniform_native_generator_graphs(n, d, seed):
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(n, d, seed)
+    with _dg().from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("A")
+        o = oracle.c_color(rp, col, "A")
+        assert_same_run(g, o)
+        assert dg.validate() == (0, 0)
+
+
+@pytest.mark.parametrize("scale", [8, 10, 12, 14])
+def test_rmat_graphs(scale):
+    """Power-law: hubs (workgroup path), mex >= 64 (wide path), many small components (E1)."""
+    DG = _dg()
+    with DG.rmat(scale, 16, seed=scale) as dg:
+        rp, col = dg.export()
+        assert oracle_is_symmetric_simple(rp, col)
+        g = dg.color("A")
+        o = oracle.c_color(rp, col, "A")
+        assert_same_run(g, o)
+        assert dg.validate() == (0, 0)
+
+
+def oracle_is_symmetric_simple(rp, col):
+    n = len(rp) - 1
+    src = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+    a = src * n + col
+    b = col.astype(np.int64) * n + src
+    return (not np.any(src == col)) and np.array_equal(np.sort(a), np.sort(b)) and np.unique(a).size == a.size
+
+
+@pytest.mark.parametrize("dims", [(8, 8, 8), (16, 8, 4), (24, 24, 24)])
+def test_mesh_graphs(dims):
+    DG = _dg()
+    with DG.mesh(*dims) as dg:
+        rp, col = dg.export()
+        g = dg.color("A")
+        o = oracle.c_color(rp, col, "A")
+        assert_same_run(g, o)
+        assert g.max_color + 1 == 2   # wavefront 2-colours the bipartite mesh
+
+
+def test_heavy_vertices_and_wide_mex():
+    """A clique of 150 (mex up to 149) joined to a hub of degree 6000 (> GC_HEAVY_T)."""
+    n = 150 + 6000
+    adj = [[] for _ in range(n)]
+    for i in range(150):
+        for j in range(150):
+            if i != j:
+                adj[i].append(j)
+    for leaf in range(150, n):
+        adj[0].append(leaf)
+        adj[leaf].append(0)
+    for leaf in range(151, n, 7):  # some leaf-leaf edges
+        adj[leaf].append(leaf - 1)
+        adj[leaf - 1].append(leaf)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    with _dg().from_csr(rp, col) as dg:
+        g = dg.color("A")
+        o = oracle.c_color(rp, col, "A")
+        assert_same_run(g, o)
+        assert o["max_color"] >= 100
+
+
+def test_empty_and_edgeless():
+    DG = _dg()
+    rp = np.zeros(4, np.int64)
+    col = np.zeros(0, np.int32)
+    with DG.from_csr(rp, col) as dg:
+        g = dg.color("A")
+        assert g.ok and list(g.colors) == [0, 0, 0] and list(g.round_U) == [0]
+
+
+def test_reference_generator_10000_seeds():
+    """random.seed(s); Graph(10000, 8) for s = 0..5 (golden) -- E1 seeds 1,2,3,5."""
+    from gcolor_amd.generators import reference_csr
+    for s in range(6):
+        rp, col = reference_csr(10000, 8, random.Random(s))
+        with _dg().from_csr(rp, col, symmetric=True) as dg:
+            assert_same_run(dg.color("A"), oracle.c_color(rp, col, "A"))
+
+
+def test_repeat_runs_are_identical():
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(300_000, 16, 9)
+    with _dg().from_csr(rp, col, symmetric=True) as dg:
+        a = dg.color("A")
+        for _ in range(3):
+            b = dg.color("A", kernel_timing=True)
+            assert np.array_equal(a.colors, b.colors) and list(a.round_U) == list(b.round_U)
+        assert b.kernels["propose"]["ms"] > 0
