@@ -220,7 +220,7 @@ struct Run {
         GC_HIP(hipEventRecord(g->ev0, s));
         // init + seed (coloring.py:74-76)
         kt.begin(GC_K_INIT);
-        gcl_init(d, gc_grid_for_waves(g->n), s);
+        gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), s);
         kt.end();
         kt.begin(GC_K_INIT);
         gcl_seed_prep(d, g->seeds[0], g->seeds[1], s);
@@ -228,7 +228,7 @@ struct Run {
         int cur = 0;
         if ((rc = commit_seeds(cur, 0))) return rc;
         if ((rc = sync_ctl())) return rc;
-        long long U = (long long)h.uncolored - (long long)h.accepted;
+        long long U = (long long)h.uncolored - (h.seedkey ? 1 : 0);
         long long F = (long long)h.fcnt[cur];
         long long status = GC_OK;
         if (st) { st->fail_round = -1; st->fail_count = 0; }

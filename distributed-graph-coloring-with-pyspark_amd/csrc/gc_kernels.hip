@@ -40,7 +40,9 @@ struct GDev {
 // ------------------------------------------------------------------------------------
 // init: coloring.py:12-17 (+ argmax seed key for coloring.py:19-35)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g) {
+// Isolated vertices are coloured at init; when some OTHER vertex lists one of them
+// (asymmetric input) it must push like a committed vertex, so it joins the seed list.
+__global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     ull best = 0, unc = 0;
@@ -60,6 +62,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g) {
                 best = k > best ? k : best;
             }
         }
+        const bool push0 = iso && g.trp[v + 1] > g.trp[v];
+        if (push0) {
+            g.key[v] = gc_make_key(0, 0);
+            g.jp[v] = GC_JP_IN;
+        }
+        gc_wave_append(push0, (int)v, seed_light, &g.ctl->seed_cnt[0]);
         // claim bitmap: isolated vertices are coloured (never enter a frontier)
         const ull m = __ballot(iso || !valid);
         if (lane == 0) {
@@ -608,8 +616,8 @@ static inline GDev to_dev(const GcDevView& d) {
     return g;
 }
 
-void gcl_init(const GcDevView& d, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d));
+void gcl_init(const GcDevView& d, int* seed_light, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), seed_light);
 }
 void gcl_seed_prep(const GcDevView& d, int* sl, int* sh, hipStream_t s) {
     hipLaunchKernelGGL(k_seed_prep, dim3(1), dim3(64), 0, s, to_dev(d), sl, sh);

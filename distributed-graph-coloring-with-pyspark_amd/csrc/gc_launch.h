@@ -19,7 +19,7 @@ struct GcDevView {
     DevCtl* ctl;
 };
 
-void gcl_init(const GcDevView& d, int grid, hipStream_t s);
+void gcl_init(const GcDevView& d, int* seed_light, int grid, hipStream_t s);
 void gcl_seed_prep(const GcDevView& d, int* sl, int* sh, hipStream_t s);
 void gcl_propose_light(const GcDevView& d, const int* list, const ull* cnt, int* heavy, int* wide, long long k,
                        int grid, hipStream_t s);
