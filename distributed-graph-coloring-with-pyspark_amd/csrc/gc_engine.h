@@ -21,20 +21,27 @@ struct gc_graph {
     // run state
     int* color = nullptr;
     int* cround = nullptr;
-    ull* key = nullptr;
-    unsigned char* jp = nullptr;
+    int* cand = nullptr;
+    unsigned char* c8 = nullptr;
+    unsigned* c4 = nullptr;
+    unsigned short* kw = nullptr;
     unsigned* inF = nullptr;
     int* F[2] = {nullptr, nullptr};
     int* heavy = nullptr;
     int* wide = nullptr;
-    int* und[2] = {nullptr, nullptr};
+    int* undL[3] = {nullptr, nullptr, nullptr};
+    int* undH[3] = {nullptr, nullptr, nullptr};
     int* seeds[2] = {nullptr, nullptr};
     int* ulist = nullptr;
     int* parent = nullptr;
     ull* best = nullptr;
     int* vcolors = nullptr;
+    RoundRec* rec = nullptr;   // device round records
+    long long rcap = 0;
     DevCtl* ctl = nullptr;
-    DevCtl* hctl = nullptr;  // pinned host mirror
+    DevCtl* hctl = nullptr;    // pinned host mirror
+    DevCtl* hsnap = nullptr;   // pinned per-batch snapshots (2, pipelined)
+    hipEvent_t evsnap[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> evpool;
@@ -55,7 +62,8 @@ void gc_set_error(const char* fmt, ...);
 int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
 void gc_free_all(gc_graph* g);
-GcDevView gc_view(const gc_graph* g);
+GDev gc_view(const gc_graph* g);
+GLists gc_lists(const gc_graph* g);
 static inline int gc_grid_for_waves(long long items, int cap = 2048) {
     long long chunks = (items + GC_WAVE - 1) / GC_WAVE;
     long long blocks = (chunks + GC_WAVES_PER_BLOCK - 1) / GC_WAVES_PER_BLOCK;

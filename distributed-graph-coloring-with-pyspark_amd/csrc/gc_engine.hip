@@ -1,9 +1,14 @@
 // gc_engine.hip -- host engine: the round loop of graph_coloring (coloring.py:73-132) on
 // one MI355X, plus validate_graph_coloring (coloring.py:149-162), behind the C-ABI.
 //
-// Every round is a fixed kernel schedule on one stream: propose -> resolve (JP sweeps
-// until no vertex is undecided) -> commit+push.  The host only reads a 200-byte
-// counter block back (pinned) at the few points where control flow depends on it.
+// The host never waits on a round.  It enqueues batches of rounds -- propose,
+// propose_block, resolve, S sweeps, commit per round -- and each kernel takes its counts
+// from the device control block; the last workgroup of every commit closes the round on
+// the device (record, counter reset, termination).  The host reads the control block
+// back once per batch (batches grow 2 -> 64 rounds) and only steps in for the rare
+// events the device cannot finish alone: an E1 re-seed (zero proposers, uncoloured
+// vertices left), a round whose Jones-Plassmann depth exceeded the S sweeps enqueued
+// (more sweeps, then the commit again), a full round-record buffer.
 #include <stdio.h>
 #include <string.h>
 
@@ -36,8 +41,8 @@ extern "C" int gc_set_device(int32_t device) {
     return GC_OK;
 }
 
-GcDevView gc_view(const gc_graph* g) {
-    GcDevView d;
+GDev gc_view(const gc_graph* g) {
+    GDev d;
     d.n = (int)g->n;
     d.nnz = g->nnz;
     d.rp = g->rp;
@@ -47,11 +52,29 @@ GcDevView gc_view(const gc_graph* g) {
     d.tcol = g->tcol;
     d.color = g->color;
     d.cround = g->cround;
-    d.key = g->key;
-    d.jp = g->jp;
+    d.cand = g->cand;
+    d.c8 = g->c8;
+    d.c4 = g->c4;
+    d.kw = g->kw;
     d.inF = g->inF;
     d.ctl = g->ctl;
     return d;
+}
+
+GLists gc_lists(const gc_graph* g) {
+    GLists L;
+    L.F[0] = g->F[0];
+    L.F[1] = g->F[1];
+    L.heavy = g->heavy;
+    L.wide = g->wide;
+    for (int k = 0; k < 3; ++k) {
+        L.undL[k] = g->undL[k];
+        L.undH[k] = g->undH[k];
+    }
+    L.seeds[0] = g->seeds[0];
+    L.seeds[1] = g->seeds[1];
+    L.rec = g->rec;
+    return L;
 }
 
 template <typename T>
@@ -65,6 +88,8 @@ static int dalloc(T** p, size_t count) {
     return GC_OK;
 }
 
+static const long long kRoundCap = 4096;
+
 int gc_alloc_run_state(gc_graph* g) {
     if (g->has_run_state) return GC_OK;
     const size_t n = (size_t)g->n;
@@ -72,21 +97,30 @@ int gc_alloc_run_state(gc_graph* g) {
 #define A(p, c) if ((st = dalloc(&(p), (c))) != GC_OK) return st
     A(g->color, n);
     A(g->cround, n);
-    A(g->key, n);
-    A(g->jp, n);
+    A(g->cand, n);
+    A(g->c8, n);
+    A(g->c4, n / 8 + 2);
+    A(g->kw, n);
     A(g->inF, (n + 63) / 32 + 2);
     A(g->F[0], n);
     A(g->F[1], n);
     A(g->heavy, n);
     A(g->wide, n);
-    A(g->und[0], n);
-    A(g->und[1], n);
+    for (int k = 0; k < 3; ++k) {
+        A(g->undL[k], n);
+        A(g->undH[k], n);
+    }
     A(g->seeds[0], n);
     A(g->seeds[1], n);
     A(g->ulist, n);
     A(g->parent, n);
     A(g->best, n);
+    A(g->rec, (size_t)kRoundCap);
 #undef A
+    GC_HIP(hipHostMalloc((void**)&g->hsnap, 2 * sizeof(DevCtl), hipHostMallocDefault));
+    GC_HIP(hipEventCreateWithFlags(&g->evsnap[0], hipEventDisableTiming));
+    GC_HIP(hipEventCreateWithFlags(&g->evsnap[1], hipEventDisableTiming));
+    g->rcap = kRoundCap;
     g->has_run_state = true;
     return GC_OK;
 }
@@ -133,90 +167,124 @@ struct Run {
     const gc_options* opt;
     gc_stats* st;
     KTimer kt;
-    GcDevView d;
+    GDev d;
+    GLists L;
     hipStream_t s;
-    long long kbound;
-    long long rounds = 0;
+    std::vector<RoundRec> recs;  // drained round records
+    long long drained = 0;       // absolute index of the first record not yet drained
 
     int sync_ctl() {
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipStreamSynchronize(s));
         return GC_OK;
     }
-    template <typename T>
-    int zero(T* dev_field) {
-        GC_HIP(hipMemsetAsync(dev_field, 0, sizeof(T), s));
+    int clear_halt() {
+        GC_HIP(hipMemsetAsync(&g->ctl->halt, 0, sizeof(int), s));
         return GC_OK;
     }
-    int set_i64(long long* dev_field, long long v) {
-        // small values only: -1 via memset 0xFF
-        if (v == -1) { GC_HIP(hipMemsetAsync(dev_field, 0xFF, sizeof(long long), s)); }
-        else if (v == 0) { GC_HIP(hipMemsetAsync(dev_field, 0, sizeof(long long), s)); }
-        else return GC_EINVAL;
-        return GC_OK;
-    }
-    void record_round(long long U, long long F, long long maxmex, long long acc, long long seeds) {
-        if (st && st->round_cap > rounds) {
-            if (st->round_U) st->round_U[rounds] = U;
-            if (st->round_F) st->round_F[rounds] = F;
-            if (st->round_maxmex) st->round_maxmex[rounds] = maxmex;
-            if (st->round_accepted) st->round_accepted[rounds] = acc;
-            if (st->round_seeds) st->round_seeds[rounds] = seeds;
+    // copy the device records [drained, round) out and restart the device buffer
+    int drain_records() {
+        const long long r = g->hctl->round;
+        const long long cnt = r - drained;
+        if (cnt > 0) {
+            const size_t off = recs.size();
+            recs.resize(off + (size_t)cnt);
+            GC_HIP(hipMemcpyAsync(recs.data() + off, g->rec, sizeof(RoundRec) * (size_t)cnt, hipMemcpyDeviceToHost,
+                                  s));
         }
-        rounds++;
-    }
-
-    // commit the prepared seed lists (key/jp/inF already set) into frontier slot `dst`
-    int commit_seeds(int dst, int round) {
-        DevCtl& h = *g->hctl;
-        int rc;
-        if ((rc = sync_ctl())) return rc;
-        const long long nl = (long long)h.seed_cnt[0], nh = (long long)h.seed_cnt[1];
-        if (nl) {
-            kt.begin(GC_K_COMMIT);
-            gcl_commit_light(d, g->seeds[0], &g->ctl->seed_cnt[0], 0, g->F[dst], &g->ctl->fcnt[dst], round,
-                             gc_grid_for_waves(nl), s);
-            kt.end();
-        }
-        if (nh) {
-            kt.begin(GC_K_COMMIT);
-            gcl_commit_block(d, g->seeds[1], &g->ctl->seed_cnt[1], g->F[dst], &g->ctl->fcnt[dst], round,
-                             (int)std::min<long long>(nh, 1024), s);
-            kt.end();
-        }
+        drained = r;
+        GC_HIP(hipMemcpyAsync(&g->ctl->rbase, &g->hctl->round, sizeof(long long), hipMemcpyHostToDevice, s));
+        GC_HIP(hipStreamSynchronize(s));
         return GC_OK;
     }
 
-    int e1_reseed(int dst, int round, long long* nseeds) {
+    void launch_commit(int mode, int nsweeps) {
+        kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
+        gcl_commit(d, L, mode, nsweeps, s);
+        kt.end();
+    }
+    void launch_sweeps(int from, int to) {  // sweeps from..to inclusive
+        for (int i = from; i <= to; ++i) {
+            kt.begin(GC_K_SWEEP);
+            gcl_sweep(d, L, i, s);
+            kt.end();
+        }
+    }
+    void enqueue_round(int S) {
+        kt.begin(GC_K_OTHER);
+        gcl_pack_c4(d, s);
+        kt.end();
+        kt.begin(GC_K_PROPOSE);
+        gcl_propose(d, L, s);
+        kt.end();
+        kt.begin(GC_K_PROPOSE);
+        gcl_propose_block(d, L, s);
+        kt.end();
+        kt.begin(GC_K_RESOLVE);
+        gcl_resolve(d, L, s);
+        kt.end();
+        launch_sweeps(1, S);
+        launch_commit(GC_CM_ROUND, S);
+    }
+    // a batch of rounds followed by an async snapshot of the control block
+    int enqueue_batch(int B, int S, int slot) {
+        for (int b = 0; b < B; ++b) enqueue_round(S);
+        GC_HIP(hipMemcpyAsync(&g->hsnap[slot], g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
+        GC_HIP(hipEventRecord(g->evsnap[slot], s));
+        return GC_OK;
+    }
+    // sweeps to enqueue per round from the depths seen so far: none while every round
+    // was decided by the first sweep (meshes), else twice the last round's depth
+    static int pick_sweeps(const DevCtl& h) {
+        if (h.maxdepth <= 1) return 0;
+        return (int)std::min<long long>(64, h.lastdepth + 2);
+    }
+    // rounds per batch: small while the frontier is tiny or the colouring is nearly done
+    static int pick_batch(const DevCtl& h, long long n, int prev) {
+        if (h.U * 64 < n) return 1;
+        return std::min(prev * 2, 4);
+    }
+
+    // E1: every component of the uncoloured-induced subgraph gets its
+    // argmax-(deg, pos) vertex as a colour-0 seed; committed like a round's winners.
+    int e1_reseed() {
         int rc;
-        if ((rc = zero(&g->ctl->list_cnt)) || (rc = zero(&g->ctl->seed_cnt[0])) || (rc = zero(&g->ctl->seed_cnt[1])))
-            return rc;
+        GC_HIP(hipMemsetAsync(&g->ctl->list_cnt, 0, sizeof(ull), s));
+        GC_HIP(hipMemsetAsync(&g->ctl->seed_cnt[0], 0, 2 * sizeof(ull), s));
         const int gridn = gc_grid_for_waves(g->n);
         kt.begin(GC_K_RESEED);
         gcl_unc_compact(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gridn, s);
         kt.end();
         if ((rc = sync_ctl())) return rc;
-        const long long L = (long long)g->hctl->list_cnt;
+        const long long Lc = (long long)g->hctl->list_cnt;
         kt.begin(GC_K_RESEED);
-        gcl_cc_hook(d, g->ulist, &g->ctl->list_cnt, g->parent, gc_grid_for_waves(L), s);
+        gcl_cc_hook(d, g->ulist, &g->ctl->list_cnt, g->parent, gc_grid_for_waves(Lc), s);
         kt.end();
         kt.begin(GC_K_RESEED);
-        gcl_cc_best(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gc_grid_for_waves(L, 4096), s);
+        gcl_cc_best(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gc_grid_for_waves(Lc, 4096), s);
         kt.end();
         kt.begin(GC_K_RESEED);
         gcl_cc_seeds(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, g->seeds[0], g->seeds[1],
-                     gc_grid_for_waves(L, 4096), s);
+                     gc_grid_for_waves(Lc, 4096), s);
         kt.end();
-        if ((rc = commit_seeds(dst, round))) return rc;
-        *nseeds = (long long)(g->hctl->seed_cnt[0] + g->hctl->seed_cnt[1]);
+        kt.begin(GC_K_RESEED);
+        gcl_commit(d, L, GC_CM_RESEED, 0, s);
+        kt.end();
         return GC_OK;
     }
 
     int go(int32_t* colors_out, int32_t* cround_out) {
         int rc;
         DevCtl& h = *g->hctl;
-        GC_HIP(hipMemsetAsync(g->ctl, 0, sizeof(DevCtl), s));
-        if ((rc = set_i64(&g->ctl->maxcolor, -1))) return rc;
+        memset(&h, 0, sizeof(DevCtl));
+        h.kbound = opt->num_colors;
+        h.e1 = opt->e1 ? 1 : 0;
+        h.rcap = g->rcap;
+        h.maxmex = -1;
+        h.maxcolor = -1;
+        h.fail_round = -1;
+        h.want_cround = cround_out != nullptr;
+        GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, s));
         GC_HIP(hipEventRecord(g->ev0, s));
         // init + seed (coloring.py:74-76)
         kt.begin(GC_K_INIT);
@@ -225,116 +293,93 @@ struct Run {
         kt.begin(GC_K_INIT);
         gcl_seed_prep(d, g->seeds[0], g->seeds[1], s);
         kt.end();
-        int cur = 0;
-        if ((rc = commit_seeds(cur, 0))) return rc;
-        if ((rc = sync_ctl())) return rc;
-        long long U = (long long)h.uncolored - (h.seedkey ? 1 : 0);
-        long long F = (long long)h.fcnt[cur];
-        long long status = GC_OK;
-        if (st) { st->fail_round = -1; st->fail_count = 0; }
+        launch_commit(GC_CM_INIT, 0);
         const long long max_rounds = 4ll * g->n + 16;
-        for (long long r = 0;; ++r) {
-            if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
-            if (U == 0) { record_round(0, 0, -1, 0, 0); break; }
-            const int nxt = cur ^ 1;
-            if (F == 0) {  // zero proposers: reference spins here (coloring.py:93-95)
-                if (!opt->e1) { record_round(U, 0, -1, 0, 0); status = GC_STALLED; break; }
-                if ((rc = zero(&g->ctl->fcnt[cur])) || (rc = zero(&g->ctl->accepted))) return rc;
-                long long ns = 0;
-                if ((rc = e1_reseed(cur, (int)r + 1, &ns))) return rc;
+        // Pipelined: batch k+1 is enqueued before the host waits on batch k's snapshot, so
+        // the device never idles on the host.  Any halt drains the stream and is handled on
+        // the synchronous path below, then the pipeline restarts.
+        int batch = 1, S = 1;
+        for (;;) {
+            int slot = 0;
+            if ((rc = enqueue_batch(batch, S, slot))) return rc;
+            for (;;) {
+                if ((rc = enqueue_batch(batch, S, slot ^ 1))) return rc;
+                GC_HIP(hipEventSynchronize(g->evsnap[slot]));
+                const DevCtl& sn = g->hsnap[slot];
+                if (sn.halt != GC_RUN) break;
+                if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
+                S = pick_sweeps(sn);
+                batch = pick_batch(sn, g->n, batch);
+                slot ^= 1;
+            }
+            if ((rc = sync_ctl())) return rc;
+            if (h.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
+            int halt = h.halt;
+            // a round deeper than the sweeps enqueued: finish its sweeps, then its commit
+            while (halt == GC_H_SWEEPS) {
+                const int done = (int)h.sweeps_enq;
+                if (done > g->n + 64) { gc_set_error("Jones-Plassmann sweeps do not converge"); return GC_EROUNDS; }
+                const int more = std::max(4, done);
+                if ((rc = clear_halt())) return rc;
+                launch_sweeps(done + 1, done + more);
+                launch_commit(GC_CM_ROUND, done + more);
                 if ((rc = sync_ctl())) return rc;
-                record_round(U, 0, -1, 0, ns);
-                if (st) st->reseeds += ns;
-                U -= ns;
-                F = (long long)h.fcnt[cur];
+                halt = h.halt;
+            }
+            S = pick_sweeps(h);
+            batch = pick_batch(h, g->n, 1);
+            if (halt == GC_RUN) continue;
+            if (halt == GC_H_DONE || halt == GC_H_FAILED || halt == GC_H_STALLED) break;
+            if (halt == GC_H_ROUNDCAP) {
+                if ((rc = drain_records()) || (rc = clear_halt())) return rc;
                 continue;
             }
-            // ---- propose ----
-            if ((rc = zero(&g->ctl->heavy_cnt)) || (rc = zero(&g->ctl->wide_cnt)) || (rc = zero(&g->ctl->failcnt)) ||
-                (rc = set_i64(&g->ctl->maxmex, -1)))
-                return rc;
-            kt.begin(GC_K_PROPOSE);
-            gcl_propose_light(d, g->F[cur], &g->ctl->fcnt[cur], g->heavy, g->wide, kbound, gc_grid_for_waves(F), s);
-            kt.end();
-            if ((rc = sync_ctl())) return rc;
-            const long long nh = (long long)h.heavy_cnt, nw = (long long)h.wide_cnt;
-            if (nh + nw > 0) {
-                long long words = (h.maxcolor + 2 + 31) / 32;
-                words = std::max<long long>(1, std::min<long long>(words, 16384));
-                kt.begin(GC_K_PROPOSE);
-                gcl_propose_block(d, g->heavy, &g->ctl->heavy_cnt, g->wide, &g->ctl->wide_cnt, kbound, (int)words,
-                                  (int)std::min<long long>(nh + nw, 4096), s);
-                kt.end();
-                if ((rc = sync_ctl())) return rc;
+            if (halt == GC_H_RESEED) {
+                if ((rc = drain_records())) return rc;
+                if ((rc = clear_halt()) || (rc = e1_reseed()) || (rc = sync_ctl())) return rc;
+                if (h.halt == GC_H_DONE) break;
+                if (h.halt == GC_H_RESEED || h.halt == GC_H_ROUNDCAP || h.halt == GC_H_STALLED) {
+                    // handled by the synchronous path of the next pass (no rounds run first)
+                    continue;
+                }
+                batch = 1;
+                continue;
             }
-            const long long maxmex = h.maxmex;
-            if (kbound >= 0 && h.failcnt > 0) {  // coloring.py:104-108: state at round start
-                record_round(U, F, maxmex, 0, 0);
-                status = GC_FAILED;
-                if (st) { st->fail_round = r; st->fail_count = (long long)h.failcnt; }
-                break;
-            }
-            // ---- resolve: JP sweeps ----
-            if ((rc = zero(&g->ctl->und_cnt[0]))) return rc;
-            kt.begin(GC_K_RESOLVE);
-            gcl_resolve_light(d, g->F[cur], &g->ctl->fcnt[cur], 1, g->und[0], &g->ctl->und_cnt[0], GC_K_RESOLVE,
-                              gc_grid_for_waves(F), s);
-            kt.end();
-            if (nh) {
-                kt.begin(GC_K_RESOLVE);
-                gcl_resolve_block(d, g->heavy, &g->ctl->heavy_cnt, g->und[0], &g->ctl->und_cnt[0],
-                                  (int)std::min<long long>(nh, 4096), s);
-                kt.end();
-            }
-            if ((rc = sync_ctl())) return rc;
-            int a = 0;
-            while (h.und_cnt[a] > 0) {
-                const long long nu = (long long)h.und_cnt[a];
-                if ((rc = zero(&g->ctl->und_cnt[a ^ 1]))) return rc;
-                kt.begin(GC_K_SWEEP);
-                gcl_resolve_light(d, g->und[a], &g->ctl->und_cnt[a], 0, g->und[a ^ 1], &g->ctl->und_cnt[a ^ 1],
-                                  GC_K_SWEEP, gc_grid_for_waves(nu), s);
-                kt.end();
-                if (st) st->jp_sweeps++;
-                if ((rc = sync_ctl())) return rc;
-                a ^= 1;
-            }
-            // ---- commit + frontier push ----
-            if ((rc = zero(&g->ctl->fcnt[nxt])) || (rc = zero(&g->ctl->accepted))) return rc;
-            kt.begin(GC_K_COMMIT);
-            gcl_commit_light(d, g->F[cur], &g->ctl->fcnt[cur], 1, g->F[nxt], &g->ctl->fcnt[nxt], (int)r + 1,
-                             gc_grid_for_waves(F), s);
-            kt.end();
-            if (nh) {
-                kt.begin(GC_K_COMMIT);
-                gcl_commit_block(d, g->heavy, &g->ctl->heavy_cnt, g->F[nxt], &g->ctl->fcnt[nxt], (int)r + 1,
-                                 (int)std::min<long long>(nh, 1024), s);
-                kt.end();
-            }
-            if ((rc = sync_ctl())) return rc;
-            const long long acc = (long long)h.accepted;
-            record_round(U, F, maxmex, acc, 0);
-            U -= acc;
-            cur = nxt;
-            F = (long long)h.fcnt[cur];
+            gc_set_error("unexpected device halt code %d", halt);
+            return GC_EHIP;
         }
         GC_HIP(hipEventRecord(g->ev1, s));
         if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
         if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
         if ((rc = sync_ctl())) return rc;
+        if ((rc = drain_records())) return rc;
+        GC_HIP(hipGetLastError());
+        const int status = h.halt == GC_H_FAILED ? GC_FAILED : (h.halt == GC_H_STALLED ? GC_STALLED : GC_OK);
         if (st) {
             float ms = 0.f;
             GC_HIP(hipEventElapsedTime(&ms, g->ev0, g->ev1));
             st->device_ms = ms;
-            st->rounds = rounds;
+            st->rounds = (long long)recs.size();
             st->max_color = h.maxcolor;
+            st->jp_sweeps = h.sweep_total;
+            st->fail_round = h.halt == GC_H_FAILED ? h.fail_round : -1;
+            st->fail_count = h.halt == GC_H_FAILED ? h.fail_count : 0;
+            for (const RoundRec& r : recs) st->reseeds += r.seeds;
+            for (long long i = 0; i < (long long)recs.size() && i < st->round_cap; ++i) {
+                const RoundRec& r = recs[(size_t)i];
+                if (st->round_U) st->round_U[i] = r.U;
+                if (st->round_F) st->round_F[i] = r.F;
+                if (st->round_maxmex) st->round_maxmex[i] = r.maxmex;
+                if (st->round_accepted) st->round_accepted[i] = r.accepted;
+                if (st->round_seeds) st->round_seeds[i] = r.seeds;
+            }
             // SURVEY.md §8d algorithmic bytes per kernel class
-            st->k_bytes[GC_K_PROPOSE] = 24.0 * (double)h.nvert[1] + 8.0 * (double)h.sumdeg[1];
-            st->k_bytes[GC_K_RESOLVE] = 24.0 * (double)h.nvert[2] + 12.0 * (double)h.sumdeg[2];
-            st->k_bytes[GC_K_COMMIT] = 16.0 * (double)h.nvert[4] + 8.0 * (double)h.sumdeg[4];
+            st->k_bytes[GC_K_PROPOSE] = 24.0 * (double)h.nvert[GC_K_PROPOSE] + 8.0 * (double)h.sumdeg[GC_K_PROPOSE];
+            st->k_bytes[GC_K_RESOLVE] = 24.0 * (double)h.nvert[GC_K_RESOLVE] + 12.0 * (double)h.sumdeg[GC_K_RESOLVE];
+            st->k_bytes[GC_K_COMMIT] = 16.0 * (double)h.nvert[GC_K_COMMIT] + 8.0 * (double)h.sumdeg[GC_K_COMMIT];
             kt.collect();
         }
-        return (int)status;
+        return status;
     }
 };
 
@@ -362,12 +407,12 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         stats->round_seeds = keep.round_seeds;
         stats->max_color = -1;
     }
-    Run run{g, opt, stats, KTimer{g, opt->kernel_timing != 0, stats, {}, 0}, gc_view(g), g->stream,
-            opt->num_colors, 0};
+    Run run{g, opt, stats, KTimer{g, opt->kernel_timing != 0, stats, {}, 0}, gc_view(g), gc_lists(g), g->stream,
+            {}, 0};
     rc = run.go(colors_out, cround_out);
     if (rc < 0) return rc;
-    if (stats && stats->round_cap < run.rounds && (stats->round_U || stats->round_F)) {
-        gc_set_error("round buffers too small: %lld rounds", run.rounds);
+    if (stats && stats->round_cap < (long long)run.recs.size() && (stats->round_U || stats->round_F)) {
+        gc_set_error("round buffers too small: %zu rounds", run.recs.size());
         return GC_EROUNDS;
     }
     return rc;

@@ -144,12 +144,15 @@ void gc_free_all(gc_graph* g) {
     hipSetDevice(g->device);
     if (g->trp && g->trp != g->rp) hipFree(g->trp);
     if (g->tcol && g->tcol != g->col) hipFree(g->tcol);
-    void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->key, g->jp, g->inF, g->F[0], g->F[1],
-                    g->heavy, g->wide, g->und[0], g->und[1], g->seeds[0], g->seeds[1], g->ulist, g->parent,
-                    g->best, g->vcolors, g->ctl};
+    void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->cand, g->c8, g->c4, g->kw, g->inF, g->F[0],
+                    g->F[1], g->heavy, g->wide, g->undL[0], g->undL[1], g->undL[2], g->undH[0], g->undH[1],
+                    g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->rec, g->ctl};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (g->hctl) hipHostFree(g->hctl);
+    if (g->hsnap) hipHostFree(g->hsnap);
+    for (auto e : g->evsnap)
+        if (e) hipEventDestroy(e);
     for (auto e : g->evpool) hipEventDestroy(e);
     if (g->ev0) hipEventDestroy(g->ev0);
     if (g->ev1) hipEventDestroy(g->ev1);

@@ -3,12 +3,21 @@
 // Layout in HBM (per gc_graph, all resident for the handle's lifetime):
 //   rp    int64[n+1]   CSR row offsets (file positions, lists as listed)
 //   col   int32[nnz]   neighbour positions
-//   deg   int32[n]     rp[v+1]-rp[v] (hot: rank compares, binning)
+//   deg   int32[n]     rp[v+1]-rp[v] (rank compares, binning)
 //   trp/tcol           in-neighbour CSR for the frontier push (aliases rp/col when symmetric)
 // Run state (reused across gc_color calls):
-//   color int32[n], cround int32[n], key u64[n] = (cand<<32 | deg), jp u8[n] (JP state),
-//   inF   u32[n/32]    bit = coloured or already in the frontier (claim bitmap)
-//   lists int32[n]     frontier (cur/next), heavy, wide, undecided x2, seed lists
+//   color int32[n]  cround int32[n] (written only when the caller asks for it)
+//   cand  int32[n]  candidate of the current round, only for candidates >= 254
+//   c8    u8[n]     colour mirror gathered by propose: colour, GC_C8_NONE (uncoloured) or
+//                   GC_C8_BIG (colour >= 254; light propose ignores colours >= 64 anyway)
+//   c4    u32[n/8]  nibble mirror of c8, rebuilt for big rounds while colours < 14
+//   kw    u16[n]    packed proposal word gathered by resolve: cand8 << 8 | state << 6 |
+//                   min(deg, 63); cand8 = GC_C8_NONE for non-proposers, GC_C8_BIG for
+//                   candidates >= 254 (then cand[] holds it)
+//   inF   u32[n/32] bit = coloured or already in the frontier (claim bitmap)
+//   lists int32[n]  frontier (x2), heavy, wide, undecided (x3 light, x3 heavy), seeds, E1
+// The narrow mirrors shrink the footprint of the per-edge random gathers against the
+// 4 MB L2 per XCD (C2: 5-10 MB for propose, 20 MB for resolve instead of 40-80 MB).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,18 +31,56 @@ typedef unsigned long long ull;
 #define GC_HEAVY_T 2048
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512
+// fixed grid of the device-predicated round kernels (grid-stride over device counts)
+#define GC_ROUND_GRID 2048
+#define GC_BLOCK_GRID 1024
+// dynamic LDS words of the workgroup-per-vertex mex bitmap (128 Ki colours per window)
+#define GC_MEX_WORDS 4096
 
-#define GC_KEY_INVALID 0xFFFFFFFF00000000ull
+#define GC_C8_NONE 0xFFu
+#define GC_C8_BIG 0xFEu
 #define GC_JP_UND 0
 #define GC_JP_IN 1
 #define GC_JP_OUT 2
 
-// Device-resident counters.  Zeroed / read by the host engine around each launch group.
+// halt codes of the device round pipeline (DevCtl.halt)
+#define GC_RUN 0
+#define GC_H_DONE 1
+#define GC_H_FAILED 2
+#define GC_H_STALLED 3
+#define GC_H_RESEED 4   // zero proposers with uncoloured vertices left: host runs E1
+#define GC_H_SWEEPS 5   // JP not finished after the enqueued sweeps: host adds sweeps
+#define GC_H_ROUNDCAP 6 // per-round record buffer full
+
+// commit modes (bookkeeping done by the last workgroup)
+#define GC_CM_ROUND 0
+#define GC_CM_INIT 1
+#define GC_CM_RESEED 2
+
+// per-round record (device), copied to gc_stats at the end
+struct RoundRec {
+    long long U, F, maxmex, accepted, seeds, sweeps;
+};
+
+// Device-resident control block.  Counters are updated with device-scope atomics; the
+// round state (cur, round, U, halt) is advanced by the last workgroup of each commit.
 struct DevCtl {
-    ull fcnt[2];       // frontier sizes (ping-pong: current / next)
+    int halt;          // GC_RUN or a GC_H_* code; every round kernel returns at once if set
+    int cur;           // frontier slot of the current round
+    long long round;   // index of the current round (records written so far)
+    long long U;       // uncoloured at the start of the current round
+    long long kbound;  // k of graph_coloring(graph, k); < 0 unbounded
+    int e1;            // E1 re-seed enabled
+    int pad0;
+    long long rcap;    // capacity of the round record buffer
+    long long rbase;   // absolute round index of record slot 0 (host drains full buffers)
+    long long fail_round;
+    long long fail_count;
+    ull fcnt[2];      // frontier sizes (ping-pong: current / next)
     ull heavy_cnt;     // heavy proposers (this round)
     ull wide_cnt;      // light proposers whose mex >= 64
-    ull und_cnt[2];    // undecided lists (ping-pong)
+    ull und_cnt[3];    // undecided light lists (rotating)
+    ull undh_cnt[3];   // undecided heavy lists (rotating)
     ull seed_cnt[2];   // seed lists: [0] light, [1] heavy
     ull accepted;      // committed this round
     ull failcnt;       // proposers with mex >= k
@@ -43,7 +90,14 @@ struct DevCtl {
     ull uncolored;     // init: #uncoloured; validate: #uncoloured
     ull conflicts;     // validate
     ull list_cnt;      // E1: compacted uncoloured list
-    ull nseeds;        // E1 seeds planted
+    ull ticket;        // last-workgroup detection in commit
+    long long sweeps;  // JP sweeps that found work in the current round (first included)
+    long long sweep_total;  // sum over rounds of sweeps beyond the first
+    long long maxdepth;     // max JP passes of a round (first sweep included)
+    long long lastdepth;    // JP passes of the last closed round
+    long long sweeps_enq;   // GC_H_SWEEPS: sweeps enqueued for the halted round
+    int use_c4;             // this round's propose gathers the nibble mirror
+    int want_cround;        // commit records the round each vertex was coloured in
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };
@@ -96,6 +150,16 @@ __device__ __forceinline__ int gc_owner(int excl, int e) {
     return o;
 }
 
+// Vertices per wave chunk for a list of cnt entries spread over `waves` waves: 64 for
+// big lists (bandwidth), down to 1 for short ones (one vertex per wave, its edges over
+// the lanes: a tail sweep costs one dependent gather instead of ceil(64*deg/64)).
+__device__ __forceinline__ int gc_vpw(long long cnt, long long waves) {
+    long long per = (cnt + waves - 1) / waves;
+    int v = 1;
+    while (v < 64 && v < per) v <<= 1;
+    return v;
+}
+
 // Per-wave append staging in LDS: one global atomic per GC_STAGE_CAP entries instead of
 // one per wave-instruction (a single counter saturates at ~88 returning atomics/us).
 struct GcStage {
@@ -109,6 +173,7 @@ __device__ __forceinline__ void gc_stage_flush(GcStage& s, int* out, ull* out_cn
     ull base = 0;
     if (gc_lane() == 0) base = atomicAdd(out_cnt, (ull)s.cnt);
     base = __shfl(base, 0, GC_WAVE);
+#pragma unroll 1
     for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
     gc_wave_sync();
     s.cnt = 0;
@@ -157,16 +222,23 @@ __device__ __forceinline__ void gc_block_max(long long* dst, long long v, long l
     if (threadIdx.x == 0) {
         long long t = lds_scratch[0];
         for (int i = 1; i < (int)(blockDim.x / GC_WAVE); ++i) t = lds_scratch[i] > t ? lds_scratch[i] : t;
-        atomicMax(dst, t);
+        if (t >= 0) atomicMax(dst, t);
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t gc_key_cand(ull k) { return (uint32_t)(k >> 32); }
-__device__ __forceinline__ uint32_t gc_key_deg(ull k) { return (uint32_t)k; }
-__device__ __forceinline__ ull gc_make_key(uint32_t cand, uint32_t deg) { return ((ull)cand << 32) | deg; }
+__device__ __forceinline__ unsigned char gc_c8_of(long long c) {
+    return c < 0 ? (unsigned char)GC_C8_NONE : (c >= 254 ? (unsigned char)GC_C8_BIG : (unsigned char)c);
+}
+
+__device__ __forceinline__ unsigned short gc_kw(unsigned cand8, unsigned st, int deg) {
+    return (unsigned short)((cand8 << 8) | (st << 6) | (unsigned)(deg < 63 ? deg : 63));
+}
+__device__ __forceinline__ unsigned gc_kw_cand8(unsigned w) { return w >> 8; }
+__device__ __forceinline__ unsigned gc_kw_state(unsigned w) { return (w >> 6) & 3u; }
+__device__ __forceinline__ unsigned gc_kw_deg6(unsigned w) { return w & 63u; }
 
 // rank order of coloring.py:64 (stable sort by deg of a file-ordered group): (deg, pos) asc
-__device__ __forceinline__ bool gc_rank_lt(uint32_t du, int u, uint32_t dv, int v) {
+__device__ __forceinline__ bool gc_rank_lt(int du, int u, int dv, int v) {
     return du < dv || (du == dv && u < v);
 }

@@ -1,41 +1,62 @@
 // gc_kernels.hip -- gfx950 kernels of the colouring round (variant A, coloring.py:73-132).
 //
-// Per round r (host engine in gc_engine.hip drives the order):
-//   propose  : k_propose_light (edge-balanced wave chunks) + k_propose_block (hubs / wide mex)
-//              mex of coloured neighbours' colours, colours as at the round start
-//              (coloring.py:44-54, 82-83, 98-102)
-//   resolve  : k_resolve_light / k_resolve_block, then k_resolve_light over the undecided
-//              list until empty -- Jones-Plassmann sweeps computing, per candidate colour,
-//              the lexicographically-first maximal independent set under rank
-//              (deg asc, pos asc) == coloring.py:56-70's stable-sorted greedy pass
-//   commit   : k_commit_light / k_commit_block -- scatter accepted colours
-//              (coloring.py:37-41, 114-127) and push the next frontier from the newly
-//              coloured vertices through the in-neighbour lists (claim bitmap + LDS-staged
-//              appends), so the next round touches only vertices that can propose.
+// The round is a fixed sequence of launches that the host enqueues WITHOUT reading
+// anything back: every kernel takes its work counts from the device control block
+// (DevCtl), runs a fixed grid that grid-strides over them, and returns at once when a
+// previous kernel raised DevCtl.halt.  Per round r:
+//   k_propose       mex of coloured neighbours' colours, colours as at the round start
+//                   (coloring.py:44-54, 82-83, 98-102); gathers the 1-byte colour mirror
+//   k_propose_block hubs (deg > GC_HEAVY_T) and light vertices whose mex >= 64
+//   k_resolve       first Jones-Plassmann sweep of the per-candidate-colour conflict
+//                   resolution: the lexicographically-first maximal independent set under
+//                   rank (deg asc, pos asc) == coloring.py:56-70's stable-sorted greedy
+//                   pass; raises GC_H_FAILED for a bounded attempt (coloring.py:104-108)
+//   k_sweep x S     further JP sweeps over the undecided lists (rotating slots)
+//   k_commit        scatter accepted colours (coloring.py:37-41, 114-127), push the next
+//                   frontier through the in-neighbour lists (claim bitmap + LDS-staged
+//                   appends); its last workgroup closes the round: per-round record,
+//                   counter reset, termination / E1 / "more sweeps" decisions.
 // E1 re-seed (k_unc_compact, k_cc_hook, k_cc_best, k_cc_seeds) and the validator
 // (k_validate, coloring.py:149-162) live here too.
 //
-// Edge-balanced wave chunks: a wave takes 64 list entries, prefix-sums their degrees and
-// walks the concatenated edge range 64 slots at a time, so consecutive lanes read
-// consecutive col[] entries and no lane idles on a short row (HBM-bound gather work; no
-// MFMA involved).
+// Edge-balanced wave chunks: a wave takes `vpw` list entries (64 for big lists, fewer for
+// short ones), prefix-sums their degrees and walks the concatenated edge range 64 slots
+// at a time (two slots in flight per lane), so consecutive lanes read consecutive col[]
+// entries and no lane idles on a short row.  All of it is HBM/L2-bound gather work; no
+// MFMA involved.
+#include "gcolor.h"
 #include "gc_internal.h"
+#include "gc_launch.h"
 
-struct GDev {
-    int n;
-    long long nnz;
-    const long long* rp;
-    const int* col;
-    const int* deg;
-    const long long* trp;  // in-neighbour CSR (== rp/col when symmetric)
-    const int* tcol;
-    int* color;
-    int* cround;
-    ull* key;
-    unsigned char* jp;
-    unsigned int* inF;
-    DevCtl* ctl;
-};
+// ------------------------------------------------------------------------------------
+// chunk geometry shared by the light kernels
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ long long gc_nchunks(long long cnt, int vpw) { return (cnt + vpw - 1) / vpw; }
+
+// Iterate the edge slots [0, total) of a wave chunk, two 64-slot groups per step so each
+// lane has two independent col[] -> gather chains in flight.  load(u) returns the
+// gathered value; apply(o, u, val) consumes it for owner lane o.
+template <typename Load, typename Apply>
+__device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, const long long* s_start, int excl,
+                                               int total, Load load, Apply apply) {
+    const int lane = gc_lane();
+    for (int base = 0; base < total; base += 2 * GC_WAVE) {
+        const int e0 = base + lane, e1 = e0 + GC_WAVE;
+        const int o0 = gc_owner(excl, e0);
+        const int o1 = gc_owner(excl, e1);
+        const int x0 = __shfl(excl, o0, GC_WAVE);
+        const int x1 = __shfl(excl, o1, GC_WAVE);
+        const bool v0 = e0 < total, v1 = e1 < total;
+        int u0 = 0, u1 = 0;
+        if (v0) u0 = col[s_start[o0] + (e0 - x0)];
+        if (v1) u1 = col[s_start[o1] + (e1 - x1)];
+        decltype(load(0)) g0{}, g1{};
+        if (v0) g0 = load(u0);
+        if (v1) g1 = load(u1);
+        if (v0) apply(o0, u0, g0);
+        if (v1) apply(o1, u1, g1);
+    }
+}
 
 // ------------------------------------------------------------------------------------
 // init: coloring.py:12-17 (+ argmax seed key for coloring.py:19-35)
@@ -51,21 +72,17 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
         const bool valid = v < g.n;
         const int d = valid ? g.deg[v] : 0;
         const bool iso = valid && d == 0;
+        const bool push0 = iso && g.trp[v + 1] > g.trp[v];
         if (valid) {
             g.color[v] = iso ? 0 : -1;
             g.cround[v] = iso ? 0 : -1;
-            g.key[v] = GC_KEY_INVALID;
-            g.jp[v] = GC_JP_UND;
+            g.c8[v] = iso ? 0 : (unsigned char)GC_C8_NONE;
+            g.kw[v] = push0 ? gc_kw(0u, GC_JP_IN, d) : gc_kw(GC_C8_NONE, GC_JP_UND, d);
             if (!iso) {
                 unc++;
                 const ull k = ((ull)d << 32) | (ull)v;
                 best = k > best ? k : best;
             }
-        }
-        const bool push0 = iso && g.trp[v + 1] > g.trp[v];
-        if (push0) {
-            g.key[v] = gc_make_key(0, 0);
-            g.jp[v] = GC_JP_IN;
         }
         gc_wave_append(push0, (int)v, seed_light, &g.ctl->seed_cnt[0]);
         // claim bitmap: isolated vertices are coloured (never enter a frontier)
@@ -97,34 +114,83 @@ __global__ void k_seed_prep(GDev g, int* seed_light, int* seed_heavy) {
     if (sk == 0) return;
     const int s = (int)(sk & 0xFFFFFFFFull);
     const int d = g.deg[s];
-    g.key[s] = gc_make_key(0, (unsigned)d);
-    g.jp[s] = GC_JP_IN;
+    g.kw[s] = gc_kw(0u, GC_JP_IN, d);
     atomicOr(&g.inF[s >> 5], 1u << (s & 31));
     if (d > GC_HEAVY_T) seed_heavy[atomicAdd(&g.ctl->seed_cnt[1], 1ull)] = s;
     else seed_light[atomicAdd(&g.ctl->seed_cnt[0], 1ull)] = s;
 }
 
 // ------------------------------------------------------------------------------------
+// nibble colour mirror for the big rounds of few-colour graphs: 8 vertices per word
+// (half the footprint of c8 against the 4 MB L2 per XCD).  Built when the frontier is
+// large (>= n/32) and every committed colour is < 14, else the round gathers c8.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(GC_BLOCK) k_pack_c4(GDev g) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    const long long words = ((long long)g.n + 7) >> 3;
+    const bool on = (long long)c->fcnt[c->cur] * 32 >= (long long)g.n && c->maxcolor < 14;
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->use_c4 = on ? 1 : 0;
+    if (!on) return;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+         i += (long long)gridDim.x * blockDim.x) {
+        unsigned lo = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
+        if (8 * i + 8 <= g.n) {
+            const uint2 b = *reinterpret_cast<const uint2*>(g.c8 + 8 * i);
+            lo = b.x;
+            hi = b.y;
+        } else {
+            unsigned char t[8];
+            for (int k = 0; k < 8; ++k) t[k] = 8 * i + k < g.n ? g.c8[8 * i + k] : 0xFF;
+            lo = t[0] | (t[1] << 8) | (t[2] << 16) | ((unsigned)t[3] << 24);
+            hi = t[4] | (t[5] << 8) | (t[6] << 16) | ((unsigned)t[7] << 24);
+        }
+        unsigned wv = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned a = (lo >> (8 * k)) & 0xFFu, b = (hi >> (8 * k)) & 0xFFu;
+            wv |= (a < 14u ? a : 15u) << (4 * k);
+            wv |= (b < 14u ? b : 15u) << (4 * (k + 4));
+        }
+        g.c4[i] = wv;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // propose (assign_color, coloring.py:44-54)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(GC_BLOCK) k_propose_light(GDev g, const int* __restrict__ list,
-                                                            const ull* list_cnt, int* heavy, int* wide,
-                                                            long long kbound) {
+__device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex, int d) {
+    const unsigned c8 = gc_c8_of(mex);
+    if (c8 == GC_C8_BIG) g.cand[v] = (int)mex;
+    g.kw[v] = gc_kw(c8, GC_JP_UND, d);
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
     __shared__ ull s_mask[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const long long cnt = (long long)*list_cnt;
+    const int cur = c->cur;
+    const int* __restrict__ list = L.F[cur];
+    const long long cnt = (long long)c->fcnt[cur];
+    const long long kbound = c->kbound;
+    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    const long long nch = gc_nchunks(cnt, vpw);
     long long lmax = -1;
     ull lfail = 0, lsum = 0, lnv = 0;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk * GC_WAVE < cnt;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long idx = chunk * GC_WAVE + lane;
-        const int v = idx < cnt ? list[idx] : -1;
+    const unsigned char* __restrict__ c8 = g.c8;
+    const unsigned* __restrict__ c4 = g.c4;
+    const bool use_c4 = c->use_c4 != 0;
+    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
+         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long idx = ch * vpw + lane;
+        const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool isheavy = d > GC_HEAVY_T;
-        gc_wave_append(isheavy, v, heavy, &g.ctl->heavy_cnt);
+        gc_wave_append(isheavy, v, L.heavy, &c->heavy_cnt);
         const int de = isheavy ? 0 : d;
         s_mask[w][lane] = 0;
         s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
@@ -132,15 +198,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_light(GDev g, const int* _
         const int excl = incl - de;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) {
-                const int u = g.col[s_start[w][o] + (e - eo)];
-                const int c = g.color[u];
-                if ((unsigned)c < 64u) atomicOr(&s_mask[w][o], 1ull << c);
-            }
+        if (use_c4) {  // nibble mirror: 0..13 colour, 14 never (maxcolor < 14), 15 uncoloured
+            gc_chunk_edges(
+                g.col, s_start[w], excl, total, [&](int u) { return (c4[u >> 3] >> ((u & 7) * 4)) & 15u; },
+                [&](int o, int, unsigned cc) {
+                    if (cc < 15u) atomicOr(&s_mask[w][o], 1ull << cc);
+                });
+        } else {
+            gc_chunk_edges(
+                g.col, s_start[w], excl, total, [&](int u) { return (unsigned)c8[u]; },
+                [&](int o, int, unsigned cc) {
+                    if (cc < 64u) atomicOr(&s_mask[w][o], 1ull << cc);
+                });
         }
         gc_wave_sync();
         bool iswide = false;
@@ -150,37 +219,41 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_light(GDev g, const int* _
                 iswide = true;
             } else {
                 const int mex = __builtin_ctzll(~m);
-                g.key[v] = gc_make_key((unsigned)mex, (unsigned)d);
-                g.jp[v] = GC_JP_UND;
+                gc_set_cand(g, v, mex, d);
                 lmax = mex > lmax ? mex : lmax;
                 if (kbound >= 0 && mex >= kbound) lfail++;
                 lsum += (ull)d;
                 lnv++;
             }
         }
-        gc_wave_append(iswide, v, wide, &g.ctl->wide_cnt);
+        gc_wave_append(iswide, v, L.wide, &c->wide_cnt);
     }
     __syncthreads();
-    gc_block_max(&g.ctl->maxmex, lmax, (long long*)scratch);
-    gc_block_add(&g.ctl->failcnt, lfail, scratch);
-    gc_block_add(&g.ctl->sumdeg[1], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[1], lnv, scratch);
+    gc_block_max(&c->maxmex, lmax, (long long*)scratch);
+    gc_block_add(&c->failcnt, lfail, scratch);
+    gc_block_add(&c->sumdeg[GC_K_PROPOSE], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_PROPOSE], lnv, scratch);
 }
 
 // One workgroup per vertex: hubs (deg > GC_HEAVY_T) and light vertices whose mex >= 64.
-// Forbidden-colour bitmap in LDS covering [base, base + 32*words); mex <= maxcolor + 1,
-// so one window suffices unless the colour count outgrows the LDS budget.
-__global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, const int* la, const ull* ca,
-                                                            const int* lb, const ull* cb, long long kbound,
-                                                            int words) {
+// Forbidden-colour bitmap in LDS covering [base, base + 32*GC_MEX_WORDS); mex <=
+// maxcolor + 1, so one window suffices unless the colour count outgrows it.
+__global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
     extern __shared__ __attribute__((aligned(16))) unsigned s_bits[];
     __shared__ int s_first;
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
-    const long long na = (long long)*ca, nb = (long long)*cb;
+    const long long na = (long long)c->heavy_cnt, nb = (long long)c->wide_cnt;
+    if (na + nb == 0) return;
+    const long long kbound = c->kbound;
+    const long long maxc = c->maxcolor;
+    long long words = (maxc + 2 + 31) / 32;
+    words = words < 1 ? 1 : (words > GC_MEX_WORDS ? GC_MEX_WORDS : words);
     long long lmax = -1;
     ull lfail = 0, lsum = 0, lnv = 0;
     for (long long i = blockIdx.x; i < na + nb; i += gridDim.x) {
-        const int v = i < na ? la[i] : lb[i - na];
+        const int v = i < na ? L.heavy[i] : L.wide[i - na];
         const int d = g.deg[v];
         const long long start = g.rp[v];
         long long mex = -1;
@@ -189,8 +262,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, const int* l
             if (threadIdx.x == 0) s_first = 0x7FFFFFFF;
             __syncthreads();
             for (long long e = threadIdx.x; e < d; e += blockDim.x) {
-                const long long c = g.color[g.col[start + e]] - base;
-                if (c >= 0 && c < 32ll * words) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
+                const long long cc = g.color[g.col[start + e]] - base;
+                if (cc >= 0 && cc < 32ll * words) atomicOr(&s_bits[cc >> 5], 1u << (cc & 31));
             }
             __syncthreads();
             for (int t = threadIdx.x; t < words; t += blockDim.x)
@@ -200,8 +273,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, const int* l
             __syncthreads();
         }
         if (threadIdx.x == 0) {
-            g.key[v] = gc_make_key((unsigned)mex, (unsigned)d);
-            g.jp[v] = GC_JP_UND;
+            gc_set_cand(g, v, mex, d);
             lmax = mex > lmax ? mex : lmax;
             if (kbound >= 0 && mex >= kbound) lfail++;
             lsum += (ull)d;
@@ -209,157 +281,356 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, const int* l
         }
     }
     __syncthreads();
-    gc_block_max(&g.ctl->maxmex, lmax, (long long*)scratch);
-    gc_block_add(&g.ctl->failcnt, lfail, scratch);
-    gc_block_add(&g.ctl->sumdeg[1], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[1], lnv, scratch);
+    gc_block_max(&c->maxmex, lmax, (long long*)scratch);
+    gc_block_add(&c->failcnt, lfail, scratch);
+    gc_block_add(&c->sumdeg[GC_K_PROPOSE], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_PROPOSE], lnv, scratch);
 }
 
 // ------------------------------------------------------------------------------------
 // resolve (resolve_collisions, coloring.py:56-70) as Jones-Plassmann sweeps.
 // v is IN iff every same-candidate listed neighbour u of lower rank is OUT, OUT as soon
 // as one is IN.  States only move UND -> IN/OUT, so reading a newer state than the
-// sweep started with is harmless (decisions are final).
+// sweep started with is harmless (decisions are final).  Per edge ONE 2-byte gather of
+// the packed word kw[u] = cand8 | state | deg6 decides almost every case; cand[] and
+// deg[] are read only for candidates >= 254 and degrees >= 63.
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(GC_BLOCK) k_resolve_light(GDev g, const int* __restrict__ list,
-                                                            const ull* list_cnt, int skip_heavy,
-                                                            int* und, ull* und_cnt, int kclass) {
+__device__ __forceinline__ unsigned gc_jp_flag(const GDev& g, int u, unsigned wu, int v, unsigned cv8, int cv,
+                                               int dv) {
+    if (u == v || gc_kw_cand8(wu) != cv8) return 0u;
+    if (cv8 == GC_C8_BIG && g.cand[u] != cv) return 0u;
+    const unsigned d6 = gc_kw_deg6(wu);
+    const int du = d6 < 63u ? (int)d6 : g.deg[u];
+    if (!gc_rank_lt(du, u, dv, v)) return 0u;
+    const unsigned st = gc_kw_state(wu);
+    return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
+}
+
+__device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned wv, unsigned st) {
+    g.kw[v] = (unsigned short)((wv & ~0xC0u) | (st << 6));
+}
+
+// One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
+// undecided vertices are appended to (uo, uo_cnt) / (ho, ho_cnt).
+__device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ list, long long cnt, int skip_heavy,
+                                            const int* hlist, long long hcnt, int* uo, ull* uo_cnt, int* ho,
+                                            ull* ho_cnt, ull& lsum, ull& lnv) {
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ unsigned s_cand[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ unsigned s_deg[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ unsigned s_c8[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_deg[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ unsigned s_f;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const long long cnt = (long long)*list_cnt;
-    ull lsum = 0, lnv = 0;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk * GC_WAVE < cnt;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long idx = chunk * GC_WAVE + lane;
-        const int v = idx < cnt ? list[idx] : -1;
-        const int d = v >= 0 ? g.deg[v] : 0;
-        const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
-        const int de = skip ? 0 : d;
-        s_flag[w][lane] = 0;
-        s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
-        s_v[w][lane] = v;
-        s_cand[w][lane] = skip ? 0xFFFFFFFFu : gc_key_cand(g.key[v]);
-        s_deg[w][lane] = (unsigned)d;
-        const int incl = gc_wave_incl_scan(de);
-        const int excl = incl - de;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) {
-                const int u = g.col[s_start[w][o] + (e - eo)];
-                const int vo = s_v[w][o];
-                if (u != vo) {
-                    const ull ku = g.key[u];
-                    if (gc_key_cand(ku) == s_cand[w][o] && gc_rank_lt(gc_key_deg(ku), u, s_deg[w][o], vo)) {
-                        const unsigned char st = g.jp[u];
-                        if (st == GC_JP_IN) atomicOr(&s_flag[w][o], 1u);
-                        else if (st == GC_JP_UND) atomicOr(&s_flag[w][o], 2u);
-                    }
-                }
-            }
-        }
-        gc_wave_sync();
-        bool pend = false;
-        if (!skip) {
-            const unsigned f = s_flag[w][lane];
-            if (f & 1u) g.jp[v] = GC_JP_OUT;
-            else if (f & 2u) pend = true;
-            else g.jp[v] = GC_JP_IN;
-            lsum += (ull)d;
-            lnv++;
-        }
-        gc_wave_append(pend, v, und, und_cnt);
-    }
-    __syncthreads();
-    gc_block_add(&g.ctl->sumdeg[kclass], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[kclass], lnv, scratch);
-}
-
-__global__ void __launch_bounds__(GC_BLOCK) k_resolve_block(GDev g, const int* list, const ull* list_cnt,
-                                                            int* und, ull* und_cnt) {
-    __shared__ unsigned s_f;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
-    const long long cnt = (long long)*list_cnt;
-    ull lsum = 0, lnv = 0;
-    for (long long i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const int v = list[i];
+    const unsigned short* __restrict__ kw = g.kw;
+    // hubs first: one workgroup per vertex
+    for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
+        const int v = hlist[i];
         const int d = g.deg[v];
         const long long start = g.rp[v];
-        const unsigned cv = gc_key_cand(g.key[v]);
+        const unsigned wv = kw[v];
+        const unsigned cv8 = gc_kw_cand8(wv);
+        const int cv = cv8 == GC_C8_BIG ? g.cand[v] : (int)cv8;
         if (threadIdx.x == 0) s_f = 0;
         __syncthreads();
         unsigned f = 0;
         for (long long e = threadIdx.x; e < d; e += blockDim.x) {
             const int u = g.col[start + e];
-            if (u == v) continue;
-            const ull ku = g.key[u];
-            if (gc_key_cand(ku) == cv && gc_rank_lt(gc_key_deg(ku), u, (unsigned)d, v)) {
-                const unsigned char st = g.jp[u];
-                f |= st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
-            }
+            f |= gc_jp_flag(g, u, kw[u], v, cv8, cv, d);
         }
         if (f) atomicOr(&s_f, f);
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned ff = s_f;
-            if (ff & 1u) g.jp[v] = GC_JP_OUT;
-            else if (ff & 2u) und[atomicAdd(und_cnt, 1ull)] = v;
-            else g.jp[v] = GC_JP_IN;
+            if (ff & 1u) gc_set_state(g, v, wv, GC_JP_OUT);
+            else if (ff & 2u) ho[atomicAdd(ho_cnt, 1ull)] = v;
+            else gc_set_state(g, v, wv, GC_JP_IN);
             lsum += (ull)d;
             lnv++;
         }
         __syncthreads();
     }
-    gc_block_add(&g.ctl->sumdeg[2], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[2], lnv, scratch);
+    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    const long long nch = gc_nchunks(cnt, vpw);
+    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
+         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long idx = ch * vpw + lane;
+        const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+        const int d = v >= 0 ? g.deg[v] : 0;
+        const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
+        const int de = skip ? 0 : d;
+        const unsigned wv = skip ? 0xFFFFu : (unsigned)kw[v];
+        const unsigned cv8 = skip ? 0x100u : gc_kw_cand8(wv);
+        s_flag[w][lane] = 0;
+        s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
+        s_v[w][lane] = v;
+        s_c8[w][lane] = cv8;
+        s_cv[w][lane] = cv8 == GC_C8_BIG ? g.cand[v] : (int)cv8;
+        s_deg[w][lane] = d;
+        const int incl = gc_wave_incl_scan(de);
+        const int excl = incl - de;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        gc_chunk_edges(
+            g.col, s_start[w], excl, total, [&](int u) { return (unsigned)kw[u]; },
+            [&](int o, int u, unsigned wu) {
+                const unsigned f = gc_jp_flag(g, u, wu, s_v[w][o], s_c8[w][o], s_cv[w][o], s_deg[w][o]);
+                if (f) atomicOr(&s_flag[w][o], f);
+            });
+        gc_wave_sync();
+        bool pend = false;
+        if (!skip) {
+            const unsigned f = s_flag[w][lane];
+            if (f & 1u) gc_set_state(g, v, wv, GC_JP_OUT);
+            else if (f & 2u) pend = true;
+            else gc_set_state(g, v, wv, GC_JP_IN);
+            lsum += (ull)d;
+            lnv++;
+        }
+        gc_wave_append(pend, v, uo, uo_cnt);
+    }
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    if (c->kbound >= 0 && c->failcnt > 0) {  // coloring.py:104-108: fail with the round-start state
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const long long r = c->round;
+            RoundRec* rec = L.rec + (r - c->rbase);
+            rec->U = c->U;
+            rec->F = (long long)c->fcnt[c->cur];
+            rec->maxmex = c->maxmex;
+            rec->accepted = 0;
+            rec->seeds = 0;
+            rec->sweeps = 0;
+            c->fail_round = r;
+            c->fail_count = (long long)c->failcnt;
+            c->round = r + 1;
+            c->halt = GC_H_FAILED;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->und_cnt[1] = 0;
+        c->undh_cnt[1] = 0;
+        c->sweeps = 1;
+    }
+    const int cur = c->cur;
+    ull lsum = 0, lnv = 0;
+    gc_jp_sweep(g, L.F[cur], (long long)c->fcnt[cur], 1, L.heavy, (long long)c->heavy_cnt, L.undL[0],
+                &c->und_cnt[0], L.undH[0], &c->undh_cnt[0], lsum, lnv);
+    __syncthreads();
+    gc_block_add(&c->sumdeg[GC_K_RESOLVE], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_RESOLVE], lnv, scratch);
+}
+
+// Sweep i >= 1 reads slot (i-1)%3, appends to slot i%3 and clears slot (i+1)%3, which
+// sweep i+1 appends to (its previous reader, sweep i-1, has finished).
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    const int in = (i - 1) % 3, out = i % 3, z = (i + 1) % 3;
+    const long long cl = (long long)c->und_cnt[in], ch = (long long)c->undh_cnt[in];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->und_cnt[z] = 0;
+        c->undh_cnt[z] = 0;
+        if (cl + ch > 0) c->sweeps += 1;
+    }
+    if (cl + ch == 0) return;
+    ull lsum = 0, lnv = 0;
+    gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
+                &c->undh_cnt[out], lsum, lnv);
+    __syncthreads();
+    gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
 }
 
 // ------------------------------------------------------------------------------------
-// commit (color_node + join, coloring.py:37-41, 114-127) fused with the frontier push.
+// commit (color_node + join, coloring.py:37-41, 114-127) fused with the frontier push,
+// and the end-of-round bookkeeping (last workgroup).
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ bool gc_claim(unsigned* inF, int w) {
-    const unsigned bit = 1u << (w & 31);
-    if (inF[w >> 5] & bit) return false;
-    return !(atomicOr(&inF[w >> 5], bit) & bit);
+__device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
+    const unsigned bit = 1u << (x & 31);
+    if (inF[x >> 5] & bit) return false;
+    return !(atomicOr(&inF[x >> 5], bit) & bit);
 }
 
-__global__ void __launch_bounds__(GC_BLOCK) k_commit_light(GDev g, const int* __restrict__ list,
-                                                           const ull* list_cnt, int skip_heavy, int* next,
-                                                           ull* next_cnt, int round) {
+__device__ __forceinline__ ull gc_aread(ull* p) { return atomicAdd(p, 0ull); }
+template <typename T>
+__device__ __forceinline__ void gc_st(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void gc_record(const GLists& L, DevCtl* c, long long U, long long F, long long maxmex,
+                                          long long acc, long long seeds, long long sweeps) {
+    RoundRec* rec = L.rec + (c->round - c->rbase);
+    rec->U = U;
+    rec->F = F;
+    rec->maxmex = maxmex;
+    rec->accepted = acc;
+    rec->seeds = seeds;
+    rec->sweeps = sweeps;
+    gc_st(&c->round, c->round + 1);
+}
+
+// Start-of-round checks (coloring.py:86-95 plus E1): U == 0 ends the colouring; no
+// proposer with uncoloured vertices left either stalls (E1 off: the reference spins
+// forever) or asks the host for an E1 re-seed.
+__device__ __forceinline__ void gc_precheck(const GLists& L, DevCtl* c, long long U, long long F) {
+    if (U == 0) {
+        gc_record(L, c, 0, 0, -1, 0, 0, 0);
+        gc_st(&c->halt, (int)GC_H_DONE);
+    } else if (F == 0) {
+        if (!c->e1) {
+            gc_record(L, c, U, 0, -1, 0, 0, 0);
+            gc_st(&c->halt, (int)GC_H_STALLED);
+        } else {
+            gc_st(&c->halt, (int)GC_H_RESEED);
+        }
+    } else if (c->round - c->rbase + 4 >= c->rcap) {
+        gc_st(&c->halt, (int)GC_H_ROUNDCAP);
+    }
+}
+
+// Run by ONE thread of the last workgroup of a commit, after every other workgroup's
+// counter atomics (counters are read back with atomic RMWs, written with agent-scope
+// stores; the next kernel reads them after the launch boundary).
+__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode) {
+    const long long acc = (long long)gc_aread(&c->accepted);
+    long long U = c->U;
+    int cur = c->cur;
+    if (mode == GC_CM_ROUND) {
+        const long long F = (long long)c->fcnt[cur];
+        const long long sw = c->sweeps;
+        gc_st(&c->sweep_total, c->sweep_total + (sw > 0 ? sw - 1 : 0));
+        if (sw > c->maxdepth) gc_st(&c->maxdepth, sw);
+        gc_st(&c->lastdepth, sw);
+        gc_record(L, c, U, F, c->maxmex, acc, 0, sw);
+        U -= acc;
+        gc_st(&c->fcnt[cur], 0ull);  // becomes the next round's output slot
+        cur ^= 1;
+        gc_st(&c->cur, cur);
+    } else if (mode == GC_CM_INIT) {
+        U = (long long)gc_aread(&c->uncolored) - (c->seedkey ? 1 : 0);
+    } else {  // GC_CM_RESEED: the E1 round record (no proposers, `acc` seeds planted)
+        gc_record(L, c, U, 0, -1, 0, acc, 0);
+        U -= acc;
+    }
+    gc_st(&c->U, U);
+    gc_st(&c->heavy_cnt, 0ull);
+    gc_st(&c->wide_cnt, 0ull);
+    gc_st(&c->failcnt, 0ull);
+    gc_st(&c->accepted, 0ull);
+    gc_st(&c->maxmex, -1ll);
+    gc_st(&c->sweeps, 0ll);
+    for (int k = 0; k < 3; ++k) {
+        gc_st(&c->und_cnt[k], 0ull);
+        gc_st(&c->undh_cnt[k], 0ull);
+    }
+    gc_st(&c->seed_cnt[0], 0ull);
+    gc_st(&c->seed_cnt[1], 0ull);
+    gc_st(&c->ticket, 0ull);
+    gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
+}
+
+// mode GC_CM_ROUND: light = F[cur] (hubs skipped), heavy = the heavy list, output F[cur^1];
+// GC_CM_INIT / GC_CM_RESEED: light = seeds[0], heavy = seeds[1], output F[cur].
+// nsweeps: sweeps enqueued for this round; undecided vertices left in the last sweep's
+// slot mean the host must enqueue more sweeps first (GC_H_SWEEPS, resume after nsweeps).
+__global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps) {
+    DevCtl* c = g.ctl;
+    if (mode == GC_CM_ROUND && c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ int s_acc;
+    __shared__ int s_last;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const long long cnt = (long long)*list_cnt;
+    const int last_slot = nsweeps % 3;
+    if (mode == GC_CM_ROUND && (c->und_cnt[last_slot] | c->undh_cnt[last_slot])) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            c->sweeps_enq = nsweeps;
+            c->halt = GC_H_SWEEPS;
+        }
+        return;
+    }
+    const int cur = c->cur;
+    const int round = mode == GC_CM_INIT ? 0 : (int)(c->round + 1);
+    const bool want_cround = c->want_cround != 0;
+    const int* __restrict__ list = mode == GC_CM_ROUND ? L.F[cur] : L.seeds[0];
+    const long long cnt = (long long)(mode == GC_CM_ROUND ? c->fcnt[cur] : c->seed_cnt[0]);
+    const int* hlist = mode == GC_CM_ROUND ? L.heavy : L.seeds[1];
+    const long long hcnt = (long long)(mode == GC_CM_ROUND ? c->heavy_cnt : c->seed_cnt[1]);
+    const int skip_heavy = mode == GC_CM_ROUND;
+    const int nxt = mode == GC_CM_ROUND ? cur ^ 1 : cur;
+    int* next = L.F[nxt];
+    ull* next_cnt = &c->fcnt[nxt];
     GcStage st{s_stage[w], 0};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk * GC_WAVE < cnt;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long idx = chunk * GC_WAVE + lane;
-        const int v = idx < cnt ? list[idx] : -1;
+    // hubs: one workgroup per vertex
+    for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
+        const int v = hlist[i];
+        if (threadIdx.x == 0) {
+            const unsigned wv = g.kw[v];
+            const unsigned js = gc_kw_state(wv);
+            s_acc = js == GC_JP_IN;
+            if (js == GC_JP_IN) {
+                const int cc = gc_kw_cand8(wv) == GC_C8_BIG ? g.cand[v] : (int)gc_kw_cand8(wv);
+                g.color[v] = cc;
+                g.c8[v] = gc_c8_of(cc);
+                if (want_cround) g.cround[v] = round;
+                g.kw[v] = (unsigned short)((GC_C8_NONE << 8) | (wv & 63u));
+                lmaxc = cc > lmaxc ? cc : lmaxc;
+                lacc++;
+                lsum += (ull)(g.trp[v + 1] - g.trp[v]);
+            } else if (js == GC_JP_OUT) {
+                next[atomicAdd(next_cnt, 1ull)] = v;
+            }
+        }
+        __syncthreads();
+        if (s_acc) {
+            const long long ts = g.trp[v], te = g.trp[v + 1];
+            for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
+                const long long e = e0 + threadIdx.x;
+                bool claim = false;
+                int x = 0;
+                if (e < te) {
+                    x = g.tcol[e];
+                    claim = gc_claim(g.inF, x);
+                }
+                gc_stage_push(st, claim, x, next, next_cnt);
+            }
+        }
+        __syncthreads();
+    }
+    // light vertices: wave chunks
+    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    const long long nch = gc_nchunks(cnt, vpw);
+    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
+         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long idx = ch * vpw + lane;
+        const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
-        const unsigned char js = skip ? GC_JP_UND : g.jp[v];
+        const unsigned wv = skip ? 0u : (unsigned)g.kw[v];
+        const unsigned js = skip ? (unsigned)GC_JP_UND : gc_kw_state(wv);
         const bool acc = js == GC_JP_IN;
         int din = 0;
         long long tstart = 0;
         if (acc) {
-            const int c = (int)gc_key_cand(g.key[v]);
-            g.color[v] = c;
-            g.cround[v] = round;
-            g.key[v] = GC_KEY_INVALID;
-            lmaxc = c > lmaxc ? c : lmaxc;
+            const int cc = gc_kw_cand8(wv) == GC_C8_BIG ? g.cand[v] : (int)gc_kw_cand8(wv);
+            g.color[v] = cc;
+            g.c8[v] = gc_c8_of(cc);
+            if (want_cround) g.cround[v] = round;
+            g.kw[v] = (unsigned short)((GC_C8_NONE << 8) | (wv & 63u));
+            lmaxc = cc > lmaxc ? cc : lmaxc;
             lacc++;
             tstart = g.trp[v];
             din = (int)(g.trp[v + 1] - tstart);
@@ -388,61 +659,23 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_light(GDev g, const int* __
     }
     gc_stage_flush(st, next, next_cnt);
     __syncthreads();
-    gc_block_max(&g.ctl->maxcolor, lmaxc, (long long*)scratch);
-    gc_block_add(&g.ctl->accepted, lacc, scratch);
-    gc_block_add(&g.ctl->sumdeg[4], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[4], lacc, scratch);
-}
-
-__global__ void __launch_bounds__(GC_BLOCK) k_commit_block(GDev g, const int* list, const ull* list_cnt,
-                                                           int* next, ull* next_cnt, int round) {
-    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
-    __shared__ int s_acc;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
-    const int w = threadIdx.x / GC_WAVE;
-    const long long cnt = (long long)*list_cnt;
-    GcStage st{s_stage[w], 0};
-    long long lmaxc = -1;
-    ull lacc = 0, lsum = 0;
-    for (long long i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const int v = list[i];
-        if (threadIdx.x == 0) {
-            const unsigned char js = g.jp[v];
-            s_acc = js == GC_JP_IN;
-            if (js == GC_JP_IN) {
-                const int c = (int)gc_key_cand(g.key[v]);
-                g.color[v] = c;
-                g.cround[v] = round;
-                g.key[v] = GC_KEY_INVALID;
-                lmaxc = c > lmaxc ? c : lmaxc;
-                lacc++;
-                lsum += (ull)(g.trp[v + 1] - g.trp[v]);
-            } else if (js == GC_JP_OUT) {
-                next[atomicAdd(next_cnt, 1ull)] = v;
-            }
-        }
-        __syncthreads();
-        if (s_acc) {
-            const long long ts = g.trp[v], te = g.trp[v + 1];
-            for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
-                const long long e = e0 + threadIdx.x;
-                bool claim = false;
-                int x = 0;
-                if (e < te) {
-                    x = g.tcol[e];
-                    claim = gc_claim(g.inF, x);
-                }
-                gc_stage_push(st, claim, x, next, next_cnt);
-            }
-        }
-        __syncthreads();
+    gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
+    gc_block_add(&c->accepted, lacc, scratch);
+    gc_block_add(&c->sumdeg[GC_K_COMMIT], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
+    // Last workgroup closes the round.  Everything it reads is a device-scope counter
+    // (read back with atomic RMWs); the block's counter atomics all come from lane 0 of
+    // wave 0 or are returning atomics, so lane 0 draining its own queue before the ticket
+    // orders them -- no agent fence per workgroup (measured ~125 us per commit with one).
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(&c->ticket, 1ull) == (ull)gridDim.x - 1;
     }
-    gc_stage_flush(st, next, next_cnt);
     __syncthreads();
-    gc_block_max(&g.ctl->maxcolor, lmaxc, (long long*)scratch);
-    gc_block_add(&g.ctl->accepted, lacc, scratch);
-    gc_block_add(&g.ctl->sumdeg[4], lsum, scratch);
-    gc_block_add(&g.ctl->nvert[4], lacc, scratch);
+    if (s_last && threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        gc_close_round(L, c, mode);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -541,8 +774,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_seeds(GDev g, const int* list, 
         if (root) {
             s = (int)(best[v] & 0xFFFFFFFFull);
             d = g.deg[s];
-            g.key[s] = gc_make_key(0, (unsigned)d);
-            g.jp[s] = GC_JP_IN;
+            g.kw[s] = gc_kw(0u, GC_JP_IN, d);
             atomicOr(&g.inF[s >> 5], 1u << (s & 31));
         }
         gc_wave_append(root && d > GC_HEAVY_T, s, seed_heavy, &g.ctl->seed_cnt[1]);
@@ -566,23 +798,19 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __rest
         const long long v = chunk * GC_WAVE + lane;
         const bool valid = v < g.n;
         const int d = valid ? g.deg[v] : 0;
-        const int c = valid ? colors[v] : 0;
-        if (valid && c == -1) unc++;
+        const int cv = valid ? colors[v] : 0;
+        if (valid && cv == -1) unc++;
         s_start[w][lane] = valid ? g.rp[v] : 0;
-        s_c[w][lane] = c;
+        s_c[w][lane] = cv;
         const int incl = gc_wave_incl_scan(d);
         const int excl = incl - d;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) {
-                const int u = g.col[s_start[w][o] + (e - eo)];
-                if (colors[u] == s_c[w][o]) conf++;
-            }
-        }
+        gc_chunk_edges(
+            g.col, s_start[w], excl, total, [&](int u) { return colors[u]; },
+            [&](int o, int, int cu) {
+                if (cu == s_c[w][o]) conf++;
+            });
         gc_wave_sync();
     }
     __syncthreads();
@@ -605,66 +833,47 @@ __global__ void k_degrees(const long long* rp, int n, int* deg, ull* maxdeg) {
 }
 
 // ------------------------------------------------------------------------------------
-// host-callable launch wrappers (extern "C++" linkage within the library)
+// host-callable launch wrappers
 // ------------------------------------------------------------------------------------
-#include "gc_launch.h"
-
-static inline GDev to_dev(const GcDevView& d) {
-    GDev g;
-    g.n = d.n; g.nnz = d.nnz; g.rp = d.rp; g.col = d.col; g.deg = d.deg; g.trp = d.trp; g.tcol = d.tcol;
-    g.color = d.color; g.cround = d.cround; g.key = d.key; g.jp = d.jp; g.inF = d.inF; g.ctl = d.ctl;
-    return g;
+void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, seed_light);
 }
-
-void gcl_init(const GcDevView& d, int* seed_light, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), seed_light);
+void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s) {
+    hipLaunchKernelGGL(k_seed_prep, dim3(1), dim3(64), 0, s, g, sl, sh);
 }
-void gcl_seed_prep(const GcDevView& d, int* sl, int* sh, hipStream_t s) {
-    hipLaunchKernelGGL(k_seed_prep, dim3(1), dim3(64), 0, s, to_dev(d), sl, sh);
+void gcl_pack_c4(const GDev& g, hipStream_t s) {
+    hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
 }
-void gcl_propose_light(const GcDevView& d, const int* list, const ull* cnt, int* heavy, int* wide, long long k,
-                       int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose_light, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, heavy, wide, k);
+void gcl_propose(const GDev& g, const GLists& L, hipStream_t s) {
+    hipLaunchKernelGGL(k_propose, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
 }
-void gcl_propose_block(const GcDevView& d, const int* la, const ull* ca, const int* lb, const ull* cb, long long k,
-                       int words, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose_block, dim3(grid), dim3(GC_BLOCK), (size_t)words * 4, s, to_dev(d), la, ca, lb, cb,
-                       k, words);
+void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
+    hipLaunchKernelGGL(k_propose_block, dim3(GC_BLOCK_GRID), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
-void gcl_resolve_light(const GcDevView& d, const int* list, const ull* cnt, int skip_heavy, int* und, ull* und_cnt,
-                       int kclass, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve_light, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, skip_heavy, und,
-                       und_cnt, kclass);
+void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
+    hipLaunchKernelGGL(k_resolve, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
 }
-void gcl_resolve_block(const GcDevView& d, const int* list, const ull* cnt, int* und, ull* und_cnt, int grid,
-                       hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve_block, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, und, und_cnt);
+void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, i);
 }
-void gcl_commit_light(const GcDevView& d, const int* list, const ull* cnt, int skip_heavy, int* next, ull* next_cnt,
-                      int round, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_commit_light, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, skip_heavy, next,
-                       next_cnt, round);
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s) {
+    hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps);
 }
-void gcl_commit_block(const GcDevView& d, const int* list, const ull* cnt, int* next, ull* next_cnt, int round,
-                      int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_commit_block, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, next, next_cnt, round);
+void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
 }
-void gcl_unc_compact(const GcDevView& d, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, parent, best);
+void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_cc_hook, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent);
 }
-void gcl_cc_hook(const GcDevView& d, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_hook, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, parent);
+void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_cc_best, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
 }
-void gcl_cc_best(const GcDevView& d, const int* list, const ull* cnt, int* parent, ull* best, int grid,
-                 hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_best, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, parent, best);
+void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, const ull* best, int* sl, int* sh,
+                  int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best, sl, sh);
 }
-void gcl_cc_seeds(const GcDevView& d, const int* list, const ull* cnt, int* parent, const ull* best, int* sl,
-                  int* sh, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), list, cnt, parent, best, sl, sh);
-}
-void gcl_validate(const GcDevView& d, const int* colors, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, to_dev(d), colors);
+void gcl_validate(const GDev& g, const int* colors, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors);
 }
 void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, deg, maxdeg);

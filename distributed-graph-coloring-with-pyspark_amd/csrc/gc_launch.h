@@ -1,43 +1,50 @@
-// gc_launch.h -- host-side view of the device state and the kernel launch wrappers.
+// gc_launch.h -- kernel argument blocks and the host-side launch wrappers.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "gc_internal.h"
 
-struct GcDevView {
+// Graph + run state, passed by value to every kernel.
+struct GDev {
     int n;
     long long nnz;
     const long long* rp;
     const int* col;
     const int* deg;
-    const long long* trp;
+    const long long* trp;  // in-neighbour CSR (== rp/col when symmetric)
     const int* tcol;
     int* color;
     int* cround;
-    ull* key;
-    unsigned char* jp;
+    int* cand;
+    unsigned char* c8;
+    unsigned* c4;
+    unsigned short* kw;
     unsigned int* inF;
     DevCtl* ctl;
 };
 
-void gcl_init(const GcDevView& d, int* seed_light, int grid, hipStream_t s);
-void gcl_seed_prep(const GcDevView& d, int* sl, int* sh, hipStream_t s);
-void gcl_propose_light(const GcDevView& d, const int* list, const ull* cnt, int* heavy, int* wide, long long k,
-                       int grid, hipStream_t s);
-void gcl_propose_block(const GcDevView& d, const int* la, const ull* ca, const int* lb, const ull* cb, long long k,
-                       int words, int grid, hipStream_t s);
-void gcl_resolve_light(const GcDevView& d, const int* list, const ull* cnt, int skip_heavy, int* und, ull* und_cnt,
-                       int kclass, int grid, hipStream_t s);
-void gcl_resolve_block(const GcDevView& d, const int* list, const ull* cnt, int* und, ull* und_cnt, int grid,
-                       hipStream_t s);
-void gcl_commit_light(const GcDevView& d, const int* list, const ull* cnt, int skip_heavy, int* next, ull* next_cnt,
-                      int round, int grid, hipStream_t s);
-void gcl_commit_block(const GcDevView& d, const int* list, const ull* cnt, int* next, ull* next_cnt, int round,
-                      int grid, hipStream_t s);
-void gcl_unc_compact(const GcDevView& d, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
-void gcl_cc_hook(const GcDevView& d, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);
-void gcl_cc_best(const GcDevView& d, const int* list, const ull* cnt, int* parent, ull* best, int grid,
-                 hipStream_t s);
-void gcl_cc_seeds(const GcDevView& d, const int* list, const ull* cnt, int* parent, const ull* best, int* sl,
-                  int* sh, int grid, hipStream_t s);
-void gcl_validate(const GcDevView& d, const int* colors, int grid, hipStream_t s);
+// Work lists of the round pipeline (counts live in DevCtl).
+struct GLists {
+    int* F[2];
+    int* heavy;
+    int* wide;
+    int* undL[3];
+    int* undH[3];
+    int* seeds[2];
+    RoundRec* rec;
+};
+
+void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s);
+void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s);
+void gcl_pack_c4(const GDev& g, hipStream_t s);
+void gcl_propose(const GDev& g, const GLists& L, hipStream_t s);
+void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
+void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
+void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s);
+void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
+void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);
+void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
+void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, const ull* best, int* sl, int* sh,
+                  int grid, hipStream_t s);
+void gcl_validate(const GDev& g, const int* colors, int grid, hipStream_t s);
 void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s);

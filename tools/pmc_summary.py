@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of tools/gpu_profile.sh into per-kernel JSON.
+
+  python tools/pmc_summary.py gpurun_out/<tag> > profiles/<round>/pmc_summary.json
+
+Per kernel name: launches, average duration (kernel trace), and FETCH_SIZE / WRITE_SIZE
+per launch from the two separate --pmc passes.  Units: rocprofv3 reports both counters in
+KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a 16-B-per-lane coalesced streaming
+read (MI355X_MICROARCH.md §HBM); the gathers here are 1-8 B per lane and uncalibrated, so
+the bytes are reported as counted (x1024), with the x2 streaming-read correction given
+separately as an upper bound.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    if not os.path.exists(path):
+        return {}
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name", counter) != counter:
+            continue
+        a = agg[r["Kernel_Name"]]
+        a[0] += 1
+        a[1] += float(r["Counter_Value"])
+    return {k: (c, v) for k, (c, v) in agg.items()}
+
+
+def main(d):
+    stats = {}
+    p = os.path.join(d, "trace", "run_kernel_stats.csv")
+    for r in csv.DictReader(open(p)):
+        stats[r["Name"]] = {"launches": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                            "total_ms": float(r["TotalDurationNs"]) / 1e6, "pct": float(r["Percentage"])}
+    fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = {}
+    for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"]):
+        e = dict(s)
+        if k in fetch:
+            c, v = fetch[k]
+            e["fetch_bytes_per_launch"] = v * 1024 / c
+            e["fetch_bytes_per_launch_x2_upper"] = 2 * v * 1024 / c
+        if k in write:
+            c, v = write[k]
+            e["write_bytes_per_launch"] = v * 1024 / c
+        if "fetch_bytes_per_launch" in e and "write_bytes_per_launch" in e:
+            e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
+        out[k] = e
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
