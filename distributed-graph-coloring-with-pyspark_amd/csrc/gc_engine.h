@@ -16,6 +16,7 @@ struct gc_graph {
     long long* rp = nullptr;
     int* col = nullptr;
     int* deg = nullptr;
+    int* nlow = nullptr;       // lower-rank neighbours first in each row (see gc_graph.hip)
     long long* trp = nullptr;  // in-neighbour CSR; == rp/col when symmetric
     int* tcol = nullptr;
     // run state
@@ -24,7 +25,7 @@ struct gc_graph {
     int* cand = nullptr;
     unsigned char* c8 = nullptr;
     unsigned* c4 = nullptr;
-    unsigned short* kw = nullptr;
+    unsigned char* k8 = nullptr;
     unsigned* inF = nullptr;
     int* F[2] = {nullptr, nullptr};
     int* heavy = nullptr;

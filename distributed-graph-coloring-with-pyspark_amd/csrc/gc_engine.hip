@@ -10,6 +10,7 @@
 // vertices left), a round whose Jones-Plassmann depth exceeded the S sweeps enqueued
 // (more sweeps, then the commit again), a full round-record buffer.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -48,6 +49,7 @@ GDev gc_view(const gc_graph* g) {
     d.rp = g->rp;
     d.col = g->col;
     d.deg = g->deg;
+    d.nlow = g->nlow;
     d.trp = g->trp;
     d.tcol = g->tcol;
     d.color = g->color;
@@ -55,7 +57,7 @@ GDev gc_view(const gc_graph* g) {
     d.cand = g->cand;
     d.c8 = g->c8;
     d.c4 = g->c4;
-    d.kw = g->kw;
+    d.k8 = g->k8;
     d.inF = g->inF;
     d.ctl = g->ctl;
     return d;
@@ -100,7 +102,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->cand, n);
     A(g->c8, n);
     A(g->c4, n / 8 + 2);
-    A(g->kw, n);
+    A(g->k8, n);
     A(g->inF, (n + 63) / 32 + 2);
     A(g->F[0], n);
     A(g->F[1], n);
@@ -172,10 +174,18 @@ struct Run {
     hipStream_t s;
     std::vector<RoundRec> recs;  // drained round records
     long long drained = 0;       // absolute index of the first record not yet drained
+    bool debug = getenv("GC_DEBUG") != nullptr;
 
     int sync_ctl() {
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipStreamSynchronize(s));
+        if (debug) {
+            const DevCtl& h = *g->hctl;
+            fprintf(stderr, "[gc] halt=%d round=%lld U=%lld cur=%d fcnt=%llu/%llu und=%llu/%llu/%llu undh=%llu/%llu/%llu "
+                            "sweeps=%lld enq=%lld maxdepth=%lld\n",
+                    h.halt, h.round, h.U, h.cur, h.fcnt[0], h.fcnt[1], h.und_cnt[0], h.und_cnt[1], h.und_cnt[2],
+                    h.undh_cnt[0], h.undh_cnt[1], h.undh_cnt[2], h.sweeps, h.sweeps_enq, h.maxdepth);
+        }
         return GC_OK;
     }
     int clear_halt() {
@@ -201,6 +211,9 @@ struct Run {
     void launch_commit(int mode, int nsweeps) {
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
         gcl_commit(d, L, mode, nsweeps, s);
+        kt.end();
+        kt.begin(GC_K_OTHER);
+        gcl_close(d, L, mode, s);
         kt.end();
     }
     void launch_sweeps(int from, int to) {  // sweeps from..to inclusive
@@ -269,6 +282,9 @@ struct Run {
         kt.end();
         kt.begin(GC_K_RESEED);
         gcl_commit(d, L, GC_CM_RESEED, 0, s);
+        kt.end();
+        kt.begin(GC_K_RESEED);
+        gcl_close(d, L, GC_CM_RESEED, s);
         kt.end();
         return GC_OK;
     }
@@ -348,6 +364,9 @@ struct Run {
             gc_set_error("unexpected device halt code %d", halt);
             return GC_EHIP;
         }
+        kt.begin(GC_K_OTHER);
+        gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
+        kt.end();
         GC_HIP(hipEventRecord(g->ev1, s));
         if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
         if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));

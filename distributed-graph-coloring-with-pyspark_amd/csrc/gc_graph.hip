@@ -144,7 +144,7 @@ void gc_free_all(gc_graph* g) {
     hipSetDevice(g->device);
     if (g->trp && g->trp != g->rp) hipFree(g->trp);
     if (g->tcol && g->tcol != g->col) hipFree(g->tcol);
-    void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->cand, g->c8, g->c4, g->kw, g->inF, g->F[0],
+    void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->cand, g->c8, g->c4, g->k8, g->nlow, g->inF, g->F[0],
                     g->F[1], g->heavy, g->wide, g->undL[0], g->undL[1], g->undL[2], g->undH[0], g->undH[1],
                     g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->rec, g->ctl};
     for (void* p : ptrs)
@@ -188,7 +188,37 @@ static int new_graph(gc_graph** out, long long n, long long nnz, uint32_t flags,
     return GC_OK;
 }
 
-// deg, maxdeg, column range check, transpose (unless symmetric)
+// Rank is static -- (deg, pos), coloring.py:64 -- so every row is stored with its
+// lower-rank neighbours first and nlow[v] counts them: a Jones-Plassmann sweep then
+// reads only those entries (every other listed neighbour cannot block v).  Mark the
+// entries (k_rank_flags), then stable-partition each row on the mark into a new column
+// array (k_partition_rows).  Order inside a row is irrelevant to every phase (mex, LFMIS,
+// push and validation all work on sets).
+static int partition_rows(gc_graph* g) {
+    hipStream_t s = g->stream;
+    GC_HIP(hipMalloc((void**)&g->nlow, sizeof(int) * (size_t)std::max<long long>(g->n, 1)));
+    if (g->n == 0) return GC_OK;
+    if (g->nnz == 0) {
+        GC_HIP(hipMemsetAsync(g->nlow, 0, sizeof(int) * (size_t)g->n, s));
+        GC_HIP(hipStreamSynchronize(s));
+        return GC_OK;
+    }
+    int* out = nullptr;
+    GC_HIP(hipMalloc((void**)&out, sizeof(int) * (size_t)g->nnz));
+    const int grid = gc_grid_for_waves(g->n, 8192);
+    gcl_rank_flags(g->rp, g->col, g->deg, (int)g->n, g->nlow, grid, s);
+    gcl_partition_rows(g->rp, g->col, g->deg, g->nlow, (int)g->n, out, grid, s);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        hipFree(out);
+        gc_set_error("row partition failed");
+        return GC_EHIP;
+    }
+    hipFree(g->col);
+    g->col = out;
+    return GC_OK;
+}
+
+// deg, maxdeg, column range check, row partition by rank, transpose (unless symmetric)
 int gc_alloc_graph_common(gc_graph* g) {
     hipStream_t s = g->stream;
     GC_HIP(hipMemsetAsync(g->ctl, 0, sizeof(DevCtl), s));
@@ -205,6 +235,8 @@ int gc_alloc_graph_common(gc_graph* g) {
     }
     g->maxdeg = (long long)g->hctl->seedkey;
     if (g->maxdeg >= (1ll << 31)) { gc_set_error("degree too large"); return GC_EINVAL; }
+    int rc0 = partition_rows(g);
+    if (rc0) return rc0;
     if (g->flags & GC_GRAPH_SYMMETRIC) {
         g->trp = g->rp;
         g->tcol = g->col;
@@ -393,5 +425,12 @@ extern "C" int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col
     GC_HIP(hipSetDevice(g->device));
     if (row_ptr) GC_HIP(hipMemcpy(row_ptr, g->rp, sizeof(long long) * (size_t)(g->n + 1), hipMemcpyDeviceToHost));
     if (col && g->nnz) GC_HIP(hipMemcpy(col, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToHost));
+    return GC_OK;
+}
+
+extern "C" int gc_graph_lower_counts(const gc_graph* g, int32_t* nlow_out) {
+    if (!g || !nlow_out) { gc_set_error("null argument"); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    if (g->n) GC_HIP(hipMemcpy(nlow_out, g->nlow, sizeof(int) * (size_t)g->n, hipMemcpyDeviceToHost));
     return GC_OK;
 }

@@ -3,21 +3,22 @@
 // Layout in HBM (per gc_graph, all resident for the handle's lifetime):
 //   rp    int64[n+1]   CSR row offsets (file positions, lists as listed)
 //   col   int32[nnz]   neighbour positions
-//   deg   int32[n]     rp[v+1]-rp[v] (rank compares, binning)
+//   deg   int32[n]     rp[v+1]-rp[v] (binning, algorithmic-byte accounting)
+//   nlow  int32[n]     rows are stored lower-rank neighbours first (rank = (deg, pos),
+//                      static); nlow[v] of them -- the only ones a JP sweep reads
 //   trp/tcol           in-neighbour CSR for the frontier push (aliases rp/col when symmetric)
 // Run state (reused across gc_color calls):
 //   color int32[n]  cround int32[n] (written only when the caller asks for it)
-//   cand  int32[n]  candidate of the current round, only for candidates >= 254
+//   cand  int32[n]  candidate of the current round, only for candidates >= 62
 //   c8    u8[n]     colour mirror gathered by propose: colour, GC_C8_NONE (uncoloured) or
-//                   GC_C8_BIG (colour >= 254; light propose ignores colours >= 64 anyway)
+//                   GC_C8_BIG (colour >= 254, then color[] holds it); color[] itself is
+//                   rebuilt from c8 once at the end (k_finalize)
 //   c4    u32[n/8]  nibble mirror of c8, rebuilt for big rounds while colours < 14
-//   kw    u16[n]    packed proposal word gathered by resolve: cand8 << 8 | state << 6 |
-//                   min(deg, 63); cand8 = GC_C8_NONE for non-proposers, GC_C8_BIG for
-//                   candidates >= 254 (then cand[] holds it)
+//   k8    u8[n]     proposal byte gathered by resolve: cand6 << 2 | JP state
 //   inF   u32[n/32] bit = coloured or already in the frontier (claim bitmap)
 //   lists int32[n]  frontier (x2), heavy, wide, undecided (x3 light, x3 heavy), seeds, E1
 // The narrow mirrors shrink the footprint of the per-edge random gathers against the
-// 4 MB L2 per XCD (C2: 5-10 MB for propose, 20 MB for resolve instead of 40-80 MB).
+// 4 MB L2 per XCD (C2: 5-10 MB for propose and resolve instead of 40-80 MB).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -231,12 +232,14 @@ __device__ __forceinline__ unsigned char gc_c8_of(long long c) {
     return c < 0 ? (unsigned char)GC_C8_NONE : (c >= 254 ? (unsigned char)GC_C8_BIG : (unsigned char)c);
 }
 
-__device__ __forceinline__ unsigned short gc_kw(unsigned cand8, unsigned st, int deg) {
-    return (unsigned short)((cand8 << 8) | (st << 6) | (unsigned)(deg < 63 ? deg : 63));
-}
-__device__ __forceinline__ unsigned gc_kw_cand8(unsigned w) { return w >> 8; }
-__device__ __forceinline__ unsigned gc_kw_state(unsigned w) { return (w >> 6) & 3u; }
-__device__ __forceinline__ unsigned gc_kw_deg6(unsigned w) { return w & 63u; }
+// proposal byte k8 = cand6 << 2 | JP state; cand6 = candidate (< 62), GC_K8_BIG (>= 62:
+// the candidate is in cand[]) or GC_K8_NONE (not proposing this round)
+#define GC_K8_BIG 62u
+#define GC_K8_NONE 63u
+__device__ __forceinline__ unsigned char gc_k8(unsigned c6, unsigned st) { return (unsigned char)((c6 << 2) | st); }
+__device__ __forceinline__ unsigned gc_c6_of(long long c) { return c >= 62 ? GC_K8_BIG : (unsigned)c; }
+__device__ __forceinline__ unsigned gc_k8_cand(unsigned k) { return k >> 2; }
+__device__ __forceinline__ unsigned gc_k8_state(unsigned k) { return k & 3u; }
 
 // rank order of coloring.py:64 (stable sort by deg of a file-ordered group): (deg, pos) asc
 __device__ __forceinline__ bool gc_rank_lt(int du, int u, int dv, int v) {

@@ -58,6 +58,12 @@ __device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, cons
     }
 }
 
+// colour of u from the byte mirror (-1 uncoloured)
+__device__ __forceinline__ int gc_colour(const GDev& g, int u) {
+    const unsigned b = g.c8[u];
+    return b == GC_C8_NONE ? -1 : (b == GC_C8_BIG ? g.color[u] : (int)b);
+}
+
 // ------------------------------------------------------------------------------------
 // init: coloring.py:12-17 (+ argmax seed key for coloring.py:19-35)
 // ------------------------------------------------------------------------------------
@@ -77,7 +83,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
             g.color[v] = iso ? 0 : -1;
             g.cround[v] = iso ? 0 : -1;
             g.c8[v] = iso ? 0 : (unsigned char)GC_C8_NONE;
-            g.kw[v] = push0 ? gc_kw(0u, GC_JP_IN, d) : gc_kw(GC_C8_NONE, GC_JP_UND, d);
+            g.k8[v] = push0 ? gc_k8(0u, GC_JP_IN) : gc_k8(GC_K8_NONE, GC_JP_UND);
             if (!iso) {
                 unc++;
                 const ull k = ((ull)d << 32) | (ull)v;
@@ -114,7 +120,7 @@ __global__ void k_seed_prep(GDev g, int* seed_light, int* seed_heavy) {
     if (sk == 0) return;
     const int s = (int)(sk & 0xFFFFFFFFull);
     const int d = g.deg[s];
-    g.kw[s] = gc_kw(0u, GC_JP_IN, d);
+    g.k8[s] = gc_k8(0u, GC_JP_IN);
     atomicOr(&g.inF[s >> 5], 1u << (s & 31));
     if (d > GC_HEAVY_T) seed_heavy[atomicAdd(&g.ctl->seed_cnt[1], 1ull)] = s;
     else seed_light[atomicAdd(&g.ctl->seed_cnt[0], 1ull)] = s;
@@ -159,10 +165,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_pack_c4(GDev g) {
 // ------------------------------------------------------------------------------------
 // propose (assign_color, coloring.py:44-54)
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex, int d) {
-    const unsigned c8 = gc_c8_of(mex);
-    if (c8 == GC_C8_BIG) g.cand[v] = (int)mex;
-    g.kw[v] = gc_kw(c8, GC_JP_UND, d);
+__device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex) {
+    const unsigned c6 = gc_c6_of(mex);
+    if (c6 == GC_K8_BIG) g.cand[v] = (int)mex;
+    g.k8[v] = gc_k8(c6, GC_JP_UND);
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
@@ -219,7 +225,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
                 iswide = true;
             } else {
                 const int mex = __builtin_ctzll(~m);
-                gc_set_cand(g, v, mex, d);
+                gc_set_cand(g, v, mex);
                 lmax = mex > lmax ? mex : lmax;
                 if (kbound >= 0 && mex >= kbound) lfail++;
                 lsum += (ull)d;
@@ -262,7 +268,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
             if (threadIdx.x == 0) s_first = 0x7FFFFFFF;
             __syncthreads();
             for (long long e = threadIdx.x; e < d; e += blockDim.x) {
-                const long long cc = g.color[g.col[start + e]] - base;
+                const long long cc = gc_colour(g, g.col[start + e]) - base;
                 if (cc >= 0 && cc < 32ll * words) atomicOr(&s_bits[cc >> 5], 1u << (cc & 31));
             }
             __syncthreads();
@@ -273,7 +279,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
             __syncthreads();
         }
         if (threadIdx.x == 0) {
-            gc_set_cand(g, v, mex, d);
+            gc_set_cand(g, v, mex);
             lmax = mex > lmax ? mex : lmax;
             if (kbound >= 0 && mex >= kbound) lfail++;
             lsum += (ull)d;
@@ -291,23 +297,20 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
 // resolve (resolve_collisions, coloring.py:56-70) as Jones-Plassmann sweeps.
 // v is IN iff every same-candidate listed neighbour u of lower rank is OUT, OUT as soon
 // as one is IN.  States only move UND -> IN/OUT, so reading a newer state than the
-// sweep started with is harmless (decisions are final).  Per edge ONE 2-byte gather of
-// the packed word kw[u] = cand8 | state | deg6 decides almost every case; cand[] and
-// deg[] are read only for candidates >= 254 and degrees >= 63.
+// sweep started with is harmless (decisions are final).  Every row lists its lower-rank
+// neighbours first (nlow[v] of them, fixed at graph creation: rank is static), so a
+// sweep walks only those and gathers ONE byte per edge, k8[u] = cand6 << 2 | state;
+// cand[] is read only for candidates >= 62.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned gc_jp_flag(const GDev& g, int u, unsigned wu, int v, unsigned cv8, int cv,
-                                               int dv) {
-    if (u == v || gc_kw_cand8(wu) != cv8) return 0u;
-    if (cv8 == GC_C8_BIG && g.cand[u] != cv) return 0u;
-    const unsigned d6 = gc_kw_deg6(wu);
-    const int du = d6 < 63u ? (int)d6 : g.deg[u];
-    if (!gc_rank_lt(du, u, dv, v)) return 0u;
-    const unsigned st = gc_kw_state(wu);
+__device__ __forceinline__ unsigned gc_jp_flag(const GDev& g, int u, unsigned ku, unsigned cv6, int cv) {
+    if (gc_k8_cand(ku) != cv6) return 0u;
+    if (cv6 == GC_K8_BIG && g.cand[u] != cv) return 0u;
+    const unsigned st = gc_k8_state(ku);
     return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
 }
 
-__device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned wv, unsigned st) {
-    g.kw[v] = (unsigned short)((wv & ~0xC0u) | (st << 6));
+__device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsigned st) {
+    g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
 
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
@@ -317,36 +320,35 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                                             ull* ho_cnt, ull& lsum, ull& lnv) {
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ unsigned s_c8[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_deg[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_f;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const unsigned short* __restrict__ kw = g.kw;
+    const unsigned char* __restrict__ k8 = g.k8;
     // hubs first: one workgroup per vertex
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
         const int v = hlist[i];
         const int d = g.deg[v];
+        const int dl = g.nlow[v];
         const long long start = g.rp[v];
-        const unsigned wv = kw[v];
-        const unsigned cv8 = gc_kw_cand8(wv);
-        const int cv = cv8 == GC_C8_BIG ? g.cand[v] : (int)cv8;
+        const unsigned kv = k8[v];
+        const unsigned cv6 = gc_k8_cand(kv);
+        const int cv = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
         if (threadIdx.x == 0) s_f = 0;
         __syncthreads();
         unsigned f = 0;
-        for (long long e = threadIdx.x; e < d; e += blockDim.x) {
+        for (long long e = threadIdx.x; e < dl; e += blockDim.x) {
             const int u = g.col[start + e];
-            f |= gc_jp_flag(g, u, kw[u], v, cv8, cv, d);
+            f |= gc_jp_flag(g, u, k8[u], cv6, cv);
         }
         if (f) atomicOr(&s_f, f);
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned ff = s_f;
-            if (ff & 1u) gc_set_state(g, v, wv, GC_JP_OUT);
+            if (ff & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
             else if (ff & 2u) ho[atomicAdd(ho_cnt, 1ull)] = v;
-            else gc_set_state(g, v, wv, GC_JP_IN);
+            else gc_set_state(g, v, kv, GC_JP_IN);
             lsum += (ull)d;
             lnv++;
         }
@@ -360,32 +362,30 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
-        const int de = skip ? 0 : d;
-        const unsigned wv = skip ? 0xFFFFu : (unsigned)kw[v];
-        const unsigned cv8 = skip ? 0x100u : gc_kw_cand8(wv);
+        const int dl = skip ? 0 : g.nlow[v];
+        const unsigned kv = skip ? 0xFFu : (unsigned)k8[v];
+        const unsigned cv6 = skip ? 0x100u : gc_k8_cand(kv);
         s_flag[w][lane] = 0;
         s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
-        s_v[w][lane] = v;
-        s_c8[w][lane] = cv8;
-        s_cv[w][lane] = cv8 == GC_C8_BIG ? g.cand[v] : (int)cv8;
-        s_deg[w][lane] = d;
-        const int incl = gc_wave_incl_scan(de);
-        const int excl = incl - de;
+        s_c6[w][lane] = cv6;
+        s_cv[w][lane] = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
+        const int incl = gc_wave_incl_scan(dl);
+        const int excl = incl - dl;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
         gc_chunk_edges(
-            g.col, s_start[w], excl, total, [&](int u) { return (unsigned)kw[u]; },
-            [&](int o, int u, unsigned wu) {
-                const unsigned f = gc_jp_flag(g, u, wu, s_v[w][o], s_c8[w][o], s_cv[w][o], s_deg[w][o]);
+            g.col, s_start[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
+            [&](int o, int u, unsigned ku) {
+                const unsigned f = gc_jp_flag(g, u, ku, s_c6[w][o], s_cv[w][o]);
                 if (f) atomicOr(&s_flag[w][o], f);
             });
         gc_wave_sync();
         bool pend = false;
         if (!skip) {
             const unsigned f = s_flag[w][lane];
-            if (f & 1u) gc_set_state(g, v, wv, GC_JP_OUT);
+            if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
             else if (f & 2u) pend = true;
-            else gc_set_state(g, v, wv, GC_JP_IN);
+            else gc_set_state(g, v, kv, GC_JP_IN);
             lsum += (ull)d;
             lnv++;
         }
@@ -454,6 +454,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
 // commit (color_node + join, coloring.py:37-41, 114-127) fused with the frontier push,
 // and the end-of-round bookkeeping (last workgroup).
 // ------------------------------------------------------------------------------------
+// Committed colours live in the byte mirror c8 (what propose gathers); the int32 colour
+// array is written only for colours >= 254 and rebuilt from c8 by k_finalize.
+__device__ __forceinline__ void gc_commit_colour(GDev& g, int v, int cc) {
+    const unsigned char b = gc_c8_of(cc);
+    g.c8[v] = b;
+    if (b == GC_C8_BIG) g.color[v] = cc;
+    g.k8[v] = (unsigned char)gc_k8(GC_K8_NONE, GC_JP_UND);
+}
+
 __device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
     const unsigned bit = 1u << (x & 31);
     if (inF[x >> 5] & bit) return false;
@@ -549,7 +558,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
     __shared__ int s_acc;
-    __shared__ int s_last;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int last_slot = nsweeps % 3;
@@ -578,15 +586,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
         const int v = hlist[i];
         if (threadIdx.x == 0) {
-            const unsigned wv = g.kw[v];
-            const unsigned js = gc_kw_state(wv);
+            const unsigned kv = g.k8[v];
+            const unsigned js = gc_k8_state(kv);
             s_acc = js == GC_JP_IN;
             if (js == GC_JP_IN) {
-                const int cc = gc_kw_cand8(wv) == GC_C8_BIG ? g.cand[v] : (int)gc_kw_cand8(wv);
-                g.color[v] = cc;
-                g.c8[v] = gc_c8_of(cc);
+                const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+                gc_commit_colour(g, v, cc);
                 if (want_cround) g.cround[v] = round;
-                g.kw[v] = (unsigned short)((GC_C8_NONE << 8) | (wv & 63u));
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
@@ -619,17 +625,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
-        const unsigned wv = skip ? 0u : (unsigned)g.kw[v];
-        const unsigned js = skip ? (unsigned)GC_JP_UND : gc_kw_state(wv);
+        const unsigned kv = skip ? 0u : (unsigned)g.k8[v];
+        const unsigned js = skip ? (unsigned)GC_JP_UND : gc_k8_state(kv);
         const bool acc = js == GC_JP_IN;
         int din = 0;
         long long tstart = 0;
         if (acc) {
-            const int cc = gc_kw_cand8(wv) == GC_C8_BIG ? g.cand[v] : (int)gc_kw_cand8(wv);
-            g.color[v] = cc;
-            g.c8[v] = gc_c8_of(cc);
+            const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+            gc_commit_colour(g, v, cc);
             if (want_cround) g.cround[v] = round;
-            g.kw[v] = (unsigned short)((GC_C8_NONE << 8) | (wv & 63u));
             lmaxc = cc > lmaxc ? cc : lmaxc;
             lacc++;
             tstart = g.trp[v];
@@ -663,19 +667,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     gc_block_add(&c->accepted, lacc, scratch);
     gc_block_add(&c->sumdeg[GC_K_COMMIT], lsum, scratch);
     gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
-    // Last workgroup closes the round.  Everything it reads is a device-scope counter
-    // (read back with atomic RMWs); the block's counter atomics all come from lane 0 of
-    // wave 0 or are returning atomics, so lane 0 draining its own queue before the ticket
-    // orders them -- no agent fence per workgroup (measured ~125 us per commit with one).
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = atomicAdd(&c->ticket, 1ull) == (ull)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (s_last && threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        gc_close_round(L, c, mode);
-    }
+}
+
+// Closes the round (or the INIT / RESEED seeding) after its commit: one thread, so every
+// counter the commit's workgroups updated is visible across the launch boundary.
+__global__ void k_close(GDev g, GLists L, int mode) {
+    DevCtl* c = g.ctl;
+    if (mode == GC_CM_ROUND && c->halt) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) gc_close_round(L, c, mode);
 }
 
 // ------------------------------------------------------------------------------------
@@ -702,7 +701,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_unc_compact(GDev g, int* list, ull
     GcStage st{s_stage[w], 0};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v - lane < g.n; v += stride) {
-        const bool u = v < g.n && g.color[v] == -1;
+        const bool u = v < g.n && g.c8[v] == GC_C8_NONE;
         if (u) {
             parent[v] = (int)v;
             best[v] = 0;
@@ -736,7 +735,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_hook(GDev g, const int* list, c
             if (e < total) {
                 const int u = g.col[s_start[w][o] + (e - eo)];
                 int a = s_v[w][o];
-                if (u != a && g.color[u] == -1) {
+                if (u != a && g.c8[u] == GC_C8_NONE) {
                     int b = u;
                     while (true) {
                         a = cc_find(parent, a);
@@ -774,7 +773,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_seeds(GDev g, const int* list, 
         if (root) {
             s = (int)(best[v] & 0xFFFFFFFFull);
             d = g.deg[s];
-            g.kw[s] = gc_kw(0u, GC_JP_IN, d);
+            g.k8[s] = gc_k8(0u, GC_JP_IN);
             atomicOr(&g.inF[s >> 5], 1u << (s & 31));
         }
         gc_wave_append(root && d > GC_HEAVY_T, s, seed_heavy, &g.ctl->seed_cnt[1]);
@@ -818,9 +817,116 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __rest
     gc_block_add(&g.ctl->conflicts, conf, scratch);
 }
 
+// Final colours from the byte mirror (colours >= 254 were stored directly).
+__global__ void __launch_bounds__(GC_BLOCK) k_finalize(GDev g) {
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < g.n;
+         v += (long long)gridDim.x * blockDim.x) {
+        const unsigned b = g.c8[v];
+        if (b != GC_C8_BIG) g.color[v] = b == GC_C8_NONE ? -1 : (int)b;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // graph helpers
 // ------------------------------------------------------------------------------------
+// Mark every adjacency entry whose neighbour does NOT rank below the row's vertex
+// (bit 31 of col; rank = (deg, pos), coloring.py:64) and count the lower ones.  A
+// segmented radix sort on bit 31 then lists lower-rank neighbours first (gc_graph.hip).
+__global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, int* col, const int* deg, int n,
+                                                         int* nlow) {
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cnt[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
+    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
+         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v = chunk * GC_WAVE + lane;
+        const bool valid = v < n;
+        const int d = valid ? deg[v] : 0;
+        s_start[w][lane] = valid ? rp[v] : 0;
+        s_cnt[w][lane] = 0;
+        s_v[w][lane] = (int)v;
+        s_d[w][lane] = d;
+        const int incl = gc_wave_incl_scan(d);
+        const int excl = incl - d;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            if (e < total) {
+                const long long ei = s_start[w][o] + (e - eo);
+                const int u = col[ei];
+                const bool lower = gc_rank_lt(deg[u], u, s_d[w][o], s_v[w][o]);
+                if (lower) atomicAdd(&s_cnt[w][o], 1);
+                else col[ei] = (int)((unsigned)u | 0x80000000u);
+            }
+        }
+        gc_wave_sync();
+        if (valid) nlow[v] = s_cnt[w][lane];
+    }
+}
+
+// Stable partition of every row on the mark left by k_rank_flags (lower-rank entries
+// first), written to `out` with the marks cleared.  Each 64-slot step ranks a lane among
+// the same-owner, same-side lanes before it with a ballot; running counts per row live
+// in LDS.  Deterministic; rows of any length (a wave walks its 64 rows' edges).
+__global__ void __launch_bounds__(GC_BLOCK) k_partition_rows(const long long* rp, const int* col, const int* deg,
+                                                             const int* nlow, int n, int* out) {
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ long long s_lo[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ long long s_hi[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
+    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
+         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v = chunk * GC_WAVE + lane;
+        const bool valid = v < n;
+        const int d = valid ? deg[v] : 0;
+        const long long st = valid ? rp[v] : 0;
+        s_start[w][lane] = st;
+        s_lo[w][lane] = st;
+        s_hi[w][lane] = st + (valid ? nlow[v] : 0);
+        const int incl = gc_wave_incl_scan(d);
+        const int excl = incl - d;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            const bool ok = e < total;
+            unsigned u = 0;
+            if (ok) u = (unsigned)col[s_start[w][o] + (e - eo)];
+            const bool upper = ok && (u & 0x80000000u);
+            const bool lower = ok && !upper;
+            const ull mlo = __ballot(lower), mhi = __ballot(upper);
+            // lanes of owner o in this step: [max(eo - base, 0), lane]
+            const int first = eo - base > 0 ? eo - base : 0;
+            const ull seg = gc_lanemask_lt() & ~((1ull << first) - 1ull);
+            if (ok) {
+                if (lower) out[s_lo[w][o] + __popcll(mlo & seg)] = (int)u;
+                else out[s_hi[w][o] + __popcll(mhi & seg)] = (int)(u & 0x7FFFFFFFu);
+            }
+            // the last lane of each owner's run in this step advances its counters
+            const int onext = __shfl_down(o, 1, GC_WAVE);
+            const bool last = ok && (lane == GC_WAVE - 1 || e + 1 >= total || onext != o);
+            gc_wave_sync();
+            if (last) {
+                const ull own = seg | (1ull << lane);
+                s_lo[w][o] += __popcll(mlo & own);
+                s_hi[w][o] += __popcll(mhi & own);
+            }
+            gc_wave_sync();
+        }
+    }
+}
+
 __global__ void k_degrees(const long long* rp, int n, int* deg, ull* maxdeg) {
     ull m = 0;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
@@ -856,6 +962,12 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, i);
 }
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s) {
+    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode);
+}
+void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
+}
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s) {
     hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps);
 }
@@ -874,6 +986,13 @@ void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, c
 }
 void gcl_validate(const GDev& g, const int* colors, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors);
+}
+void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, deg, n, nlow);
+}
+void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
+                        int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_partition_rows, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, deg, nlow, n, out);
 }
 void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, deg, maxdeg);

@@ -10,6 +10,7 @@ struct GDev {
     const long long* rp;
     const int* col;
     const int* deg;
+    const int* nlow;  // lower-rank neighbours listed first in each row
     const long long* trp;  // in-neighbour CSR (== rp/col when symmetric)
     const int* tcol;
     int* color;
@@ -17,7 +18,7 @@ struct GDev {
     int* cand;
     unsigned char* c8;
     unsigned* c4;
-    unsigned short* kw;
+    unsigned char* k8;
     unsigned int* inF;
     DevCtl* ctl;
 };
@@ -41,6 +42,11 @@ void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s);
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s);
+void gcl_finalize(const GDev& g, int grid, hipStream_t s);
+void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s);
+void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
+                        int grid, hipStream_t s);
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);
 void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s);

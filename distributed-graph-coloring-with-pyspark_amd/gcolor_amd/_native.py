@@ -22,7 +22,7 @@ KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "va
 
 # Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
 EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
-           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_color", "gc_validate",
+           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_graph_lower_counts", "gc_color", "gc_validate",
            "gc_gen_uniform", "gc_last_error", "gc_device_count", "gc_set_device"]
 
 
@@ -76,6 +76,7 @@ def load():
         "gc_graph_destroy": ([P], None),
         "gc_graph_info": ([P, _I64P, _I64P, _I64P, ctypes.POINTER(U32)], ctypes.c_int),
         "gc_graph_export": ([P, P, P], ctypes.c_int),
+        "gc_graph_lower_counts": ([P, P], ctypes.c_int),
         "gc_color": ([P, ctypes.POINTER(GcOptions), P, P, ctypes.POINTER(GcStats)], ctypes.c_int),
         "gc_validate": ([P, P, _I64P, _I64P], ctypes.c_int),
         "gc_gen_uniform": ([I64, I32, U64, P, P, I64, _I64P], ctypes.c_int),

@@ -138,6 +138,12 @@ class DeviceGraph:
         nat.check("gc_graph_export", self._lib.gc_graph_export(self._h, _ptr(rp), _ptr(col)))
         return rp, col[: self.nnz]
 
+    def lower_counts(self):
+        """nlow[v]: entries at the head of exported row v that rank below v (deg, pos)."""
+        out = np.empty(max(self.n, 1), np.int32)
+        nat.check("gc_graph_lower_counts", self._lib.gc_graph_lower_counts(self._h, _ptr(out)))
+        return out[: self.n]
+
     # ---- hot path -------------------------------------------------------------------------
     def color(self, variant="A", num_colors=None, e1=True, kernel_timing=False, want_rounds=True,
               want_colors=True):

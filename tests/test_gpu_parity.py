@@ -226,3 +226,39 @@ def test_repeat_runs_are_identical():
             b = dg.color("A", kernel_timing=True)
             assert np.array_equal(a.colors, b.colors) and list(a.round_U) == list(b.round_U)
         assert b.kernels["propose"]["ms"] > 0
+
+
+def _check_partition(dg):
+    rp, col = dg.export()
+    nl = dg.lower_counts()
+    deg = np.diff(rp)
+    n = len(rp) - 1
+    src = np.repeat(np.arange(n, dtype=np.int64), deg)
+    lower = (deg[col] < deg[src]) | ((deg[col] == deg[src]) & (col < src))
+    pos = np.arange(len(col), dtype=np.int64) - rp[src]
+    head = pos < nl[src]
+    assert np.array_equal(lower, head), "rows must list exactly their lower-rank neighbours first"
+
+
+@pytest.mark.parametrize("kind", ["golden", "directed", "rmat", "mesh"])
+def test_rows_list_lower_rank_neighbours_first(kind):
+    """Graph creation stores each row lower-rank-first (rank = (deg, pos), coloring.py:64)
+    without changing its multiset; nlow counts the head."""
+    DG = _dg()
+    if kind == "golden":
+        ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s0"))
+    elif kind == "directed":
+        rp, col = _random_directed(2000, 9000, 7)
+    if kind in ("golden", "directed"):
+        with DG.from_csr(rp, col) as dg:
+            rp2, col2 = dg.export()
+            assert np.array_equal(rp, rp2)
+            for v in range(len(rp) - 1):
+                assert sorted(col[rp[v]:rp[v + 1]]) == sorted(col2[rp[v]:rp[v + 1]])
+            _check_partition(dg)
+    elif kind == "rmat":
+        with DG.rmat(12, 16, seed=3) as dg:
+            _check_partition(dg)
+    else:
+        with DG.mesh(9, 7, 5) as dg:
+            _check_partition(dg)
