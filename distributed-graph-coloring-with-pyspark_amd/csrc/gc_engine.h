@@ -37,6 +37,7 @@ struct gc_graph {
     int* parent = nullptr;
     ull* best = nullptr;
     int* vcolors = nullptr;
+    unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;
     DevCtl* ctl = nullptr;

@@ -118,6 +118,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->parent, n);
     A(g->best, n);
     A(g->rec, (size_t)kRoundCap);
+    A(g->fsum, (size_t)gcl_fsort_blocks(g->n) + 1);
 #undef A
     GC_HIP(hipHostMalloc((void**)&g->hsnap, 2 * sizeof(DevCtl), hipHostMallocDefault));
     GC_HIP(hipEventCreateWithFlags(&g->evsnap[0], hipEventDisableTiming));
@@ -175,6 +176,7 @@ struct Run {
     std::vector<RoundRec> recs;  // drained round records
     long long drained = 0;       // absolute index of the first record not yet drained
     bool debug = getenv("GC_DEBUG") != nullptr;
+    bool resort_hint = false;    // enqueue the frontier re-sort kernels (last snapshot's frontier >= n/256)
 
     int sync_ctl() {
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
@@ -224,6 +226,11 @@ struct Run {
         }
     }
     void enqueue_round(int S) {
+        if (resort_hint) {  // device decides; enqueued only while frontiers are within reach of n/64
+            kt.begin(GC_K_OTHER);
+            gcl_fsort(d, L, g->fsum, s);
+            kt.end();
+        }
         kt.begin(GC_K_OTHER);
         gcl_pack_c4(d, s);
         kt.end();
@@ -325,6 +332,7 @@ struct Run {
                 if (sn.halt != GC_RUN) break;
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
                 S = pick_sweeps(sn);
+                resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
                 batch = pick_batch(sn, g->n, batch);
                 slot ^= 1;
             }
@@ -343,6 +351,7 @@ struct Run {
                 halt = h.halt;
             }
             S = pick_sweeps(h);
+            resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
             batch = pick_batch(h, g->n, 1);
             if (halt == GC_RUN) continue;
             if (halt == GC_H_DONE || halt == GC_H_FAILED || halt == GC_H_STALLED) break;

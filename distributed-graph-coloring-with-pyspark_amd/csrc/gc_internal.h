@@ -98,6 +98,7 @@ struct DevCtl {
     long long lastdepth;    // JP passes of the last closed round
     long long sweeps_enq;   // GC_H_SWEEPS: sweeps enqueued for the halted round
     int use_c4;             // this round's propose gathers the nibble mirror
+    int resort;             // this round's frontier is rebuilt in vertex order
     int want_cround;        // commit records the round each vertex was coloured in
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed

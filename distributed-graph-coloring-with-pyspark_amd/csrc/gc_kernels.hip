@@ -127,6 +127,110 @@ __global__ void k_seed_prep(GDev g, int* seed_light, int* seed_heavy) {
 }
 
 // ------------------------------------------------------------------------------------
+// Frontier re-sort for big rounds.  The frontier list is built by appends (losers and
+// newly claimed vertices in arrival order), so the per-vertex metadata reads of propose /
+// resolve / commit would be random.  When the frontier is large (>= n/64) it is rebuilt
+// in vertex order from the bitmaps -- frontier == claimed (inF) and still uncoloured (c8)
+// -- in three passes over n/32 words: per-workgroup counts, one-workgroup scan, ordered
+// write.  Same set, same count; the order is irrelevant to the results.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned gc_front_word(const GDev& g, long long w) {
+    const unsigned m = g.inF[w];
+    if (!m) return 0u;
+    const long long v0 = w * 32;
+    unsigned out = 0u;
+    if (v0 + 32 <= (long long)g.n) {
+        const uint4* p = reinterpret_cast<const uint4*>(g.c8 + v0);
+        const uint4 a = p[0], b = p[1];
+        const unsigned x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            // bytes equal to 0xFF (uncoloured): zero bytes of ~x, exact per byte
+            const unsigned t = ~x[k];
+            const unsigned z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);  // 0x80 where byte == 0
+            const unsigned nib = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+            out |= nib << (4 * k);
+        }
+    } else {
+        for (int k = 0; k < 32 && v0 + k < (long long)g.n; ++k)
+            if (g.c8[v0 + k] == GC_C8_NONE) out |= 1u << k;
+    }
+    return out & m;
+}
+
+__device__ __forceinline__ bool gc_resort_on(const GDev& g, const DevCtl* c) {
+    return (long long)c->fcnt[c->cur] * 64 >= (long long)g.n && c->fcnt[c->cur] > 0;
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_fsort_count(GDev g, unsigned* bsum) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    const bool on = gc_resort_on(g, c);
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->resort = on ? 1 : 0;
+    if (!on) return;
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    const long long words = ((long long)g.n + 31) / 32;
+    const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
+    ull cnt = w < words ? (ull)__popc(gc_front_word(g, w)) : 0ull;
+    cnt = gc_wave_sum(cnt);
+    if (gc_lane() == 0) scratch[threadIdx.x / GC_WAVE] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ull t = 0;
+        for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += scratch[i];
+        bsum[blockIdx.x] = (unsigned)t;
+    }
+}
+
+// exclusive scan of the per-workgroup counts, one workgroup of 1024 threads
+__global__ void __launch_bounds__(1024) k_fsort_scan(GDev g, unsigned* bsum, int nblocks) {
+    DevCtl* c = g.ctl;
+    if (c->halt || !c->resort) return;
+    __shared__ unsigned s_part[1024];
+    const int per = (nblocks + 1023) / 1024;
+    const int b0 = threadIdx.x * per;
+    unsigned local = 0;
+    for (int i = 0; i < per && b0 + i < nblocks; ++i) local += bsum[b0 + i];
+    s_part[threadIdx.x] = local;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        const unsigned y = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    unsigned run = s_part[threadIdx.x] - local;  // exclusive prefix of this thread's run
+    for (int i = 0; i < per && b0 + i < nblocks; ++i) {
+        const unsigned x = bsum[b0 + i];
+        bsum[b0 + i] = run;
+        run += x;
+    }
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_fsort_write(GDev g, const unsigned* bpre, GLists L) {
+    DevCtl* c = g.ctl;
+    if (c->halt || !c->resort) return;
+    __shared__ unsigned s_w[GC_WAVES_PER_BLOCK];
+    const long long words = ((long long)g.n + 31) / 32;
+    const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
+    const unsigned m = w < words ? gc_front_word(g, w) : 0u;
+    const int cnt = __popc(m);
+    const int incl = gc_wave_incl_scan(cnt);
+    if (gc_lane() == GC_WAVE - 1) s_w[threadIdx.x / GC_WAVE] = (unsigned)incl;
+    __syncthreads();
+    unsigned off = bpre[blockIdx.x];
+    for (int i = 0; i < (int)(threadIdx.x / GC_WAVE); ++i) off += s_w[i];
+    off += (unsigned)(incl - cnt);
+    int* out = L.F[c->cur];
+    unsigned mm = m;
+    while (mm) {
+        const int k = __builtin_ctz(mm);
+        mm &= mm - 1u;
+        out[off++] = (int)(w * 32 + k);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // nibble colour mirror for the big rounds of few-colour graphs: 8 vertices per word
 // (half the footprint of c8 against the 4 MB L2 per XCD).  Built when the frontier is
 // large (>= n/32) and every committed colour is < 14, else the round gathers c8.
@@ -323,9 +427,13 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_f;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const unsigned char* __restrict__ k8 = g.k8;
+    // undecided appends staged in LDS: one atomic per 512 entries, not one per wave-chunk
+    // (a single counter takes ~88 returning atomics/us; 86k chunks cost ~1 ms)
+    GcStage st{s_stage[w], 0};
     // hubs first: one workgroup per vertex
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
         const int v = hlist[i];
@@ -389,8 +497,9 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             lsum += (ull)d;
             lnv++;
         }
-        gc_wave_append(pend, v, uo, uo_cnt);
+        gc_stage_push(st, pend, v, uo, uo_cnt);
     }
+    gc_stage_flush(st, uo, uo_cnt);
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
@@ -946,6 +1055,14 @@ void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s) {
 }
 void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s) {
     hipLaunchKernelGGL(k_seed_prep, dim3(1), dim3(64), 0, s, g, sl, sh);
+}
+int gcl_fsort_blocks(long long n) { return (int)(((n + 31) / 32 + GC_BLOCK - 1) / GC_BLOCK); }
+void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s) {
+    const int nb = gcl_fsort_blocks(g.n);
+    if (nb <= 0) return;
+    hipLaunchKernelGGL(k_fsort_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
+    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb);
+    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L);
 }
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);

@@ -36,6 +36,8 @@ struct GLists {
 
 void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s);
 void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s);
+int gcl_fsort_blocks(long long n);
+void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);
 void gcl_pack_c4(const GDev& g, hipStream_t s);
 void gcl_propose(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
