@@ -1,12 +1,12 @@
 // gc_engine.hip -- host engine: the round loop of graph_coloring (coloring.py:73-132) on
 // one MI355X, plus validate_graph_coloring (coloring.py:149-162), behind the C-ABI.
 //
-// The host never waits on a round.  It enqueues batches of rounds -- propose,
-// propose_block, resolve, S sweeps, commit per round -- and each kernel takes its counts
-// from the device control block; the last workgroup of every commit closes the round on
-// the device (record, counter reset, termination).  The host reads the control block
-// back once per batch (batches grow 2 -> 64 rounds) and only steps in for the rare
-// events the device cannot finish alone: an E1 re-seed (zero proposers, uncoloured
+// The host never waits on a round.  It enqueues batches of rounds -- [frontier re-sort],
+// pack_c4, propose, propose_block, resolve, S sweeps, commit, close -- and every kernel
+// takes its counts from the device control block; k_close ends each round on the device
+// (record, counter reset, termination).  The host keeps one batch in flight (1-4 rounds),
+// reads a pinned snapshot of the control block per batch, and only steps in for the
+// rare events the device cannot finish alone: an E1 re-seed (zero proposers, uncoloured
 // vertices left), a round whose Jones-Plassmann depth exceeded the S sweeps enqueued
 // (more sweeps, then the commit again), a full round-record buffer.
 #include <stdio.h>
@@ -133,8 +133,9 @@ namespace {
 // Optional per-launch event bracketing (gc_options.kernel_timing).
 struct KTimer {
     gc_graph* g;
-    bool on;
+    unsigned mask;  // kernel classes to bracket with events (bit GC_K_*)
     gc_stats* st;
+    bool on_now = false;
     std::vector<std::pair<int, size_t>> recs;  // (class, event index of start)
     size_t used = 0;
     hipEvent_t ev() {
@@ -147,16 +148,17 @@ struct KTimer {
     }
     void begin(int cls) {
         if (st) st->k_launches[cls]++;
-        if (!on) return;
+        on_now = (mask >> cls) & 1u;
+        if (!on_now) return;
         recs.push_back({cls, used});
         hipEventRecord(ev(), g->stream);
     }
     void end() {
-        if (!on) return;
+        if (!on_now) return;
         hipEventRecord(ev(), g->stream);
     }
     void collect() {
-        if (!on || !st) return;
+        if (!mask || !st) return;
         for (auto& r : recs) {
             float ms = 0.f;
             hipEventElapsedTime(&ms, g->evpool[r.second], g->evpool[r.second + 1]);
@@ -435,7 +437,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         stats->round_seeds = keep.round_seeds;
         stats->max_color = -1;
     }
-    Run run{g, opt, stats, KTimer{g, opt->kernel_timing != 0, stats, {}, 0}, gc_view(g), gc_lists(g), g->stream,
+    Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
     rc = run.go(colors_out, cround_out);
     if (rc < 0) return rc;

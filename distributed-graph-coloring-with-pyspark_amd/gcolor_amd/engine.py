@@ -151,7 +151,7 @@ class DeviceGraph:
         is unbounded; on a bounded failure ``colors`` is the round-start snapshot."""
         opt = nat.GcOptions(variant=nat.GC_VARIANT_A if variant == "A" else nat.GC_VARIANT_B,
                             e1=1 if e1 else 0, num_colors=-1 if num_colors is None else int(num_colors),
-                            kernel_timing=1 if kernel_timing else 0, reserved=0)
+                            kernel_timing=_timing_mask(kernel_timing), reserved=0)
         st = nat.GcStats()
         cap = ROUND_CAP if want_rounds else 0
         rb = {k: np.zeros(max(cap, 1), np.int64) for k in ("U", "F", "maxmex", "accepted", "seeds")}
@@ -184,6 +184,16 @@ class DeviceGraph:
         arr = None if colors is None else np.ascontiguousarray(colors, dtype=np.int32)
         nat.check("gc_validate", self._lib.gc_validate(self._h, _ptr(arr), ctypes.byref(u), ctypes.byref(c)))
         return u.value, c.value
+
+
+def _timing_mask(kernel_timing):
+    """True = every kernel class; a class name or list of names = only those."""
+    if not kernel_timing:
+        return 0
+    if kernel_timing is True:
+        return 0xFF
+    names = [kernel_timing] if isinstance(kernel_timing, str) else list(kernel_timing)
+    return sum(1 << nat.KERNEL_CLASSES.index(k) for k in names)
 
 
 def uniform_csr(n, max_degree, seed=42):

@@ -75,7 +75,8 @@ typedef struct gc_options {
     int32_t variant;       /* GC_VARIANT_A / GC_VARIANT_B                                  */
     int32_t e1;            /* 1: re-seed on a zero-proposer round (extension E1)           */
     int64_t num_colors;    /* k of graph_coloring(graph, k); < 0 = unbounded               */
-    int32_t kernel_timing; /* 1: bracket every launch with HIP events (per-kernel stats)   */
+    int32_t kernel_timing; /* bit GC_K_x set: bracket that class's launches with HIP events
+                              (gc_stats.k_ms); 0xFF = every class, 0 = none             */
     int32_t reserved;
 } gc_options;
 
