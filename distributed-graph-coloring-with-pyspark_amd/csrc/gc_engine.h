@@ -48,6 +48,7 @@ struct gc_graph {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> evpool;
     bool has_run_state = false;
+    bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
 };
 
 void gc_set_error(const char* fmt, ...);
@@ -62,6 +63,7 @@ void gc_set_error(const char* fmt, ...);
     } while (0)
 
 int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
+int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
 void gc_free_all(gc_graph* g);
 GDev gc_view(const gc_graph* g);

@@ -76,6 +76,7 @@ GLists gc_lists(const gc_graph* g) {
     L.seeds[0] = g->seeds[0];
     L.seeds[1] = g->seeds[1];
     L.rec = g->rec;
+    L.delta = nullptr;
     return L;
 }
 

@@ -26,15 +26,15 @@ __global__ void k_check_cols(const int* col, long long nnz, int n, ull* bad) {
     if (gc_lane() == 0 && b) atomicAdd(bad, b);
 }
 
-__global__ void k_count_targets(const long long* rp, const int* col, int n, ull* cnt) {
-    // one thread per edge via row walk: grid-stride over vertices
-    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x)
+// in-neighbour CSR of the rows [lo, hi): for every target u, the rows in range listing u
+__global__ void k_count_targets(const long long* rp, const int* col, long long lo, long long hi, ull* cnt) {
+    for (long long v = lo + (long long)blockIdx.x * blockDim.x + threadIdx.x; v < hi; v += (long long)gridDim.x * blockDim.x)
         for (long long e = rp[v]; e < rp[v + 1]; ++e) atomicAdd(&cnt[col[e]], 1ull);
 }
 
-__global__ void k_fill_transpose(const long long* rp, const int* col, int n, const long long* trp, ull* cursor,
-                                 int* tcol) {
-    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x)
+__global__ void k_fill_transpose(const long long* rp, const int* col, long long lo, long long hi, const long long* trp,
+                                 ull* cursor, int* tcol) {
+    for (long long v = lo + (long long)blockIdx.x * blockDim.x + threadIdx.x; v < hi; v += (long long)gridDim.x * blockDim.x)
         for (long long e = rp[v]; e < rp[v + 1]; ++e) {
             const int u = col[e];
             const ull p = atomicAdd(&cursor[u], 1ull);
@@ -144,6 +144,12 @@ void gc_free_all(gc_graph* g) {
     hipSetDevice(g->device);
     if (g->trp && g->trp != g->rp) hipFree(g->trp);
     if (g->tcol && g->tcol != g->col) hipFree(g->tcol);
+    if (g->borrowed) {  // a shard's view: the CSR belongs to the replicated graph handle
+        g->rp = nullptr;
+        g->col = nullptr;
+        g->deg = nullptr;
+        g->nlow = nullptr;
+    }
     void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->cand, g->c8, g->c4, g->k8, g->nlow, g->inF, g->F[0],
                     g->F[1], g->heavy, g->wide, g->undL[0], g->undL[1], g->undL[2], g->undH[0], g->undH[1],
                     g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->rec, g->fsum, g->ctl};
@@ -243,19 +249,30 @@ int gc_alloc_graph_common(gc_graph* g) {
         return GC_OK;
     }
     // in-neighbour CSR for the frontier push (directed semantics of listed adjacency)
+    return gc_build_in_csr(g, 0, g->n);
+}
+
+// In-neighbour CSR of the rows [lo, hi) into g->trp / g->tcol: for every vertex u, the
+// rows in [lo, hi) that list u.  [0, n) is the full transpose; a shard builds the part
+// its own rows contribute (gc_shard.hip).
+int gc_build_in_csr(gc_graph* g, long long lo, long long hi) {
+    hipStream_t s = g->stream;
+    long long e0 = 0, e1 = 0;
+    GC_HIP(hipMemcpy(&e0, g->rp + lo, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_HIP(hipMemcpy(&e1, g->rp + hi, sizeof(long long), hipMemcpyDeviceToHost));
     long long* cnt = nullptr;
     GC_HIP(hipMalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
     GC_HIP(hipMalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
-    GC_HIP(hipMalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(g->nnz, 1)));
+    GC_HIP(hipMalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e1 - e0, 1)));
     GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
-    if (g->n > 0)
-        hipLaunchKernelGGL(k_count_targets, dim3(grid_for(g->n)), dim3(GC_BLOCK), 0, s, g->rp, g->col, (int)g->n,
+    if (hi > lo)
+        hipLaunchKernelGGL(k_count_targets, dim3(grid_for(hi - lo)), dim3(GC_BLOCK), 0, s, g->rp, g->col, lo, hi,
                            (ull*)cnt);
     int rc = exclusive_scan_ll(cnt, g->trp, g->n + 1, s);
     if (rc) { hipFree(cnt); return rc; }
     GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
-    if (g->n > 0)
-        hipLaunchKernelGGL(k_fill_transpose, dim3(grid_for(g->n)), dim3(GC_BLOCK), 0, s, g->rp, g->col, (int)g->n,
+    if (hi > lo)
+        hipLaunchKernelGGL(k_fill_transpose, dim3(grid_for(hi - lo)), dim3(GC_BLOCK), 0, s, g->rp, g->col, lo, hi,
                            g->trp, (ull*)cnt, g->tcol);
     GC_HIP(hipGetLastError());
     GC_HIP(hipStreamSynchronize(s));

@@ -57,6 +57,12 @@ typedef unsigned long long ull;
 #define GC_CM_ROUND 0
 #define GC_CM_INIT 1
 #define GC_CM_RESEED 2
+#define GC_CM_ACCEPT 3  // sharded round: colour the winners, publish them, no push
+
+// kinds of exchanged deltas (sharded engine)
+#define GC_KIND_CAND 0
+#define GC_KIND_STATE 1
+#define GC_KIND_COLOUR 2
 
 // per-round record (device), copied to gc_stats at the end
 struct RoundRec {
@@ -91,7 +97,8 @@ struct DevCtl {
     ull uncolored;     // init: #uncoloured; validate: #uncoloured
     ull conflicts;     // validate
     ull list_cnt;      // E1: compacted uncoloured list
-    ull ticket;        // last-workgroup detection in commit
+    ull ticket;        // (unused)
+    ull dcnt;          // sharded: deltas written this phase
     long long sweeps;  // JP sweeps that found work in the current round (first included)
     long long sweep_total;  // sum over rounds of sweeps beyond the first
     long long maxdepth;     // max JP passes of a round (first sweep included)
@@ -189,6 +196,21 @@ __device__ __forceinline__ void gc_stage_push(GcStage& s, bool pred, int val, in
     if (s.cnt + n > GC_STAGE_CAP) gc_stage_flush(s, out, out_cnt);
     if (pred) s.buf[s.cnt + __popcll(m & gc_lanemask_lt())] = val;
     s.cnt += n;
+}
+
+__device__ __forceinline__ long long gc_delta(int v, int val) {
+    return (long long)(((ull)(unsigned)v << 32) | (ull)(unsigned)val);
+}
+
+// Wave-aggregated append of 64-bit entries.  All lanes must call.
+__device__ __forceinline__ void gc_wave_append64(bool pred, long long val, long long* out, ull* out_cnt) {
+    const ull m = __ballot(pred);
+    if (m == 0) return;
+    ull base = 0;
+    const int leader = __ffsll((long long)m) - 1;
+    if (gc_lane() == leader) base = atomicAdd(out_cnt, (ull)__popcll(m));
+    base = __shfl(base, leader, GC_WAVE);
+    if (pred) out[base + __popcll(m & gc_lanemask_lt())] = val;
 }
 
 // Wave-aggregated direct append (rare lists).  All lanes must call.

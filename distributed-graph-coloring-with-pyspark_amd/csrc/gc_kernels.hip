@@ -421,7 +421,7 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 // undecided vertices are appended to (uo, uo_cnt) / (ho, ho_cnt).
 __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ list, long long cnt, int skip_heavy,
                                             const int* hlist, long long hcnt, int* uo, ull* uo_cnt, int* ho,
-                                            ull* ho_cnt, ull& lsum, ull& lnv) {
+                                            ull* ho_cnt, ull& lsum, ull& lnv, long long* dout, ull* dcnt) {
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -457,6 +457,8 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             if (ff & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
             else if (ff & 2u) ho[atomicAdd(ho_cnt, 1ull)] = v;
             else gc_set_state(g, v, kv, GC_JP_IN);
+            if (dout && ((ff & 1u) || !(ff & 2u)))
+                dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (ff & 1u) ? GC_JP_OUT : GC_JP_IN);
             lsum += (ull)d;
             lnv++;
         }
@@ -489,14 +491,17 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             });
         gc_wave_sync();
         bool pend = false;
+        unsigned nst = GC_JP_UND;
         if (!skip) {
             const unsigned f = s_flag[w][lane];
-            if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
+            if (f & 1u) nst = GC_JP_OUT;
             else if (f & 2u) pend = true;
-            else gc_set_state(g, v, kv, GC_JP_IN);
+            else nst = GC_JP_IN;
+            if (nst != GC_JP_UND) gc_set_state(g, v, kv, nst);
             lsum += (ull)d;
             lnv++;
         }
+        if (dout) gc_wave_append64(nst != GC_JP_UND, gc_delta(v, (int)nst), dout, dcnt);
         gc_stage_push(st, pend, v, uo, uo_cnt);
     }
     gc_stage_flush(st, uo, uo_cnt);
@@ -531,7 +536,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
     const int cur = c->cur;
     ull lsum = 0, lnv = 0;
     gc_jp_sweep(g, L.F[cur], (long long)c->fcnt[cur], 1, L.heavy, (long long)c->heavy_cnt, L.undL[0],
-                &c->und_cnt[0], L.undH[0], &c->undh_cnt[0], lsum, lnv);
+                &c->und_cnt[0], L.undH[0], &c->undh_cnt[0], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
     gc_block_add(&c->sumdeg[GC_K_RESOLVE], lsum, scratch);
     gc_block_add(&c->nvert[GC_K_RESOLVE], lnv, scratch);
@@ -553,7 +558,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     if (cl + ch == 0) return;
     ull lsum = 0, lnv = 0;
     gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
-                &c->undh_cnt[out], lsum, lnv);
+                &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
     gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
     gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
@@ -680,12 +685,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     const int cur = c->cur;
     const int round = mode == GC_CM_INIT ? 0 : (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    const int* __restrict__ list = mode == GC_CM_ROUND ? L.F[cur] : L.seeds[0];
-    const long long cnt = (long long)(mode == GC_CM_ROUND ? c->fcnt[cur] : c->seed_cnt[0]);
-    const int* hlist = mode == GC_CM_ROUND ? L.heavy : L.seeds[1];
-    const long long hcnt = (long long)(mode == GC_CM_ROUND ? c->heavy_cnt : c->seed_cnt[1]);
-    const int skip_heavy = mode == GC_CM_ROUND;
-    const int nxt = mode == GC_CM_ROUND ? cur ^ 1 : cur;
+    const bool rnd = mode == GC_CM_ROUND || mode == GC_CM_ACCEPT;
+    const bool push = mode != GC_CM_ACCEPT;  // ACCEPT (sharded): the push runs after the exchange
+    const int* __restrict__ list = rnd ? L.F[cur] : L.seeds[0];
+    const long long cnt = (long long)(rnd ? c->fcnt[cur] : c->seed_cnt[0]);
+    const int* hlist = rnd ? L.heavy : L.seeds[1];
+    const long long hcnt = (long long)(rnd ? c->heavy_cnt : c->seed_cnt[1]);
+    const int skip_heavy = rnd;
+    const int nxt = rnd ? cur ^ 1 : cur;
     int* next = L.F[nxt];
     ull* next_cnt = &c->fcnt[nxt];
     GcStage st{s_stage[w], 0};
@@ -702,6 +709,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
                 gc_commit_colour(g, v, cc);
                 if (want_cround) g.cround[v] = round;
+                if (!push) L.delta[atomicAdd(&c->dcnt, 1ull)] = gc_delta(v, cc);
+                s_acc = push;
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
@@ -737,10 +746,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         const unsigned kv = skip ? 0u : (unsigned)g.k8[v];
         const unsigned js = skip ? (unsigned)GC_JP_UND : gc_k8_state(kv);
         const bool acc = js == GC_JP_IN;
-        int din = 0;
+        int din = 0, cc = 0;
         long long tstart = 0;
         if (acc) {
-            const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+            cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
             gc_commit_colour(g, v, cc);
             if (want_cround) g.cround[v] = round;
             lmaxc = cc > lmaxc ? cc : lmaxc;
@@ -748,7 +757,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             tstart = g.trp[v];
             din = (int)(g.trp[v + 1] - tstart);
             lsum += (ull)din;
+            if (!push) din = 0;
         }
+        if (!push) gc_wave_append64(acc, gc_delta(v, cc), L.delta, &c->dcnt);
         // losers stay in the frontier (they still have a coloured neighbour)
         gc_stage_push(st, js == GC_JP_OUT, v, next, next_cnt);
         s_start[w][lane] = tstart;
@@ -784,6 +795,124 @@ __global__ void k_close(GDev g, GLists L, int mode) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) gc_close_round(L, c, mode);
+}
+
+// ------------------------------------------------------------------------------------
+// Sharded rounds (gc_shard.hip): a rank runs the round kernels on its own
+// frontier; at the three grid-wide seams it publishes (vertex << 32 | value) deltas of
+// its vertices and applies everyone else's.
+// ------------------------------------------------------------------------------------
+// propose seam: (v, candidate) for every frontier entry of this rank
+__global__ void __launch_bounds__(GC_BLOCK) k_delta_cand(GDev g, GLists L) {
+    const DevCtl* c = g.ctl;
+    const int cur = c->cur;
+    const long long cnt = (long long)c->fcnt[cur];
+    const int* list = L.F[cur];
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (long long)gridDim.x * blockDim.x) {
+        const int v = list[i];
+        const unsigned k = g.k8[v];
+        L.delta[i] = gc_delta(v, gc_k8_cand(k) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(k));
+    }
+}
+
+// Apply received deltas to the vertices this rank does not own ([lo, hi) already hold
+// them).  Entries with v < 0 are padding.
+__global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long long* recv, long long count,
+                                                    long long lo, long long hi, int round) {
+    const bool want_cround = g.ctl->want_cround != 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long long)gridDim.x * blockDim.x) {
+        const long long e = recv[i];
+        const int v = (int)(e >> 32);
+        if (v < 0 || (v >= lo && v < hi)) continue;
+        const int val = (int)(unsigned)(e & 0xFFFFFFFFll);
+        if (kind == GC_KIND_CAND) {
+            const unsigned c6 = gc_c6_of(val);
+            if (c6 == GC_K8_BIG) g.cand[v] = val;
+            g.k8[v] = gc_k8(c6, GC_JP_UND);
+        } else if (kind == GC_KIND_STATE) {
+            g.k8[v] = (unsigned char)((g.k8[v] & ~3u) | (unsigned)val);
+        } else {
+            gc_commit_colour(g, v, val);
+            if (want_cround) g.cround[v] = round;
+            atomicMax(&g.ctl->maxcolor, (long long)val);
+        }
+    }
+}
+
+// commit seam: every vertex coloured this round on ANY rank pushes into this rank's
+// in-neighbours (trp/tcol is the rank-local in-neighbour CSR: owned targets only).
+__global__ void __launch_bounds__(GC_BLOCK) k_push_list(GDev g, GLists L, const long long* recv, long long count) {
+    DevCtl* c = g.ctl;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const int nxt = c->cur ^ 1;
+    int* next = L.F[nxt];
+    ull* next_cnt = &c->fcnt[nxt];
+    GcStage st{s_stage[w], 0};
+    const int vpw = gc_vpw(count, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    const long long nch = gc_nchunks(count, vpw);
+    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
+         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long idx = ch * vpw + lane;
+        const int v = (lane < vpw && idx < count) ? (int)(recv[idx] >> 32) : -1;
+        long long tstart = 0;
+        int din = 0;
+        if (v >= 0) {
+            tstart = g.trp[v];
+            din = (int)(g.trp[v + 1] - tstart);
+        }
+        s_start[w][lane] = tstart;
+        const int incl = gc_wave_incl_scan(din);
+        const int excl = incl - din;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            bool claim = false;
+            int x = 0;
+            if (e < total) {
+                x = g.tcol[s_start[w][o] + (e - eo)];
+                claim = gc_claim(g.inF, x);
+            }
+            gc_stage_push(st, claim, x, next, next_cnt);
+        }
+        gc_wave_sync();
+    }
+    gc_stage_flush(st, next, next_cnt);
+}
+
+// per-round counter reset of a shard (one thread)
+__global__ void k_shard_reset(GDev g, long long round) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    DevCtl* c = g.ctl;
+    c->halt = GC_RUN;
+    c->round = round;
+    c->heavy_cnt = 0;
+    c->wide_cnt = 0;
+    c->failcnt = 0;
+    c->accepted = 0;
+    c->maxmex = -1;
+    c->sweeps = 0;
+    c->dcnt = 0;
+    c->list_cnt = 0;
+    c->seed_cnt[0] = 0;
+    c->seed_cnt[1] = 0;
+    for (int k = 0; k < 3; ++k) {
+        c->und_cnt[k] = 0;
+        c->undh_cnt[k] = 0;
+    }
+}
+
+// after the push: the next frontier becomes current, the old slot becomes the output
+__global__ void k_shard_flip(GDev g) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    DevCtl* c = g.ctl;
+    c->fcnt[c->cur] = 0;
+    c->cur ^= 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1079,6 +1208,22 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, i);
 }
+void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
+    hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
+}
+void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
+               hipStream_t s) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round);
+}
+void gcl_push_list(const GDev& g, const GLists& L, const long long* recv, long long count, hipStream_t s) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(k_push_list, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, recv, count);
+}
+void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
+}
+void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s) {
     hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode);
 }

@@ -32,6 +32,7 @@ struct GLists {
     int* undH[3];
     int* seeds[2];
     RoundRec* rec;
+    long long* delta;  // sharded engine: this phase's outgoing (vertex, value) deltas; else null
 };
 
 void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s);
@@ -45,6 +46,12 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s);
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s);
+void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
+void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
+               hipStream_t s);
+void gcl_push_list(const GDev& g, const GLists& L, const long long* recv, long long count, hipStream_t s);
+void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
+void gcl_shard_flip(const GDev& g, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
 void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s);
 void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,

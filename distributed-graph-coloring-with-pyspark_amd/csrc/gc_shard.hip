@@ -1,0 +1,244 @@
+// gc_shard.hip -- one rank's share of a multi-GPU colouring, C-ABI.
+//
+// Every rank holds the whole CSR (a gc_graph handle; R-MAT-28 is ~36 GB of a GPU's
+// 288 GB) and owns a contiguous vertex range [lo, hi).  A shard is a view of that graph
+// with its own run state and a rank-local in-neighbour CSR (the owned rows' targets), so
+// the single-GPU round kernels run unchanged on the rank's own frontier.  A round is cut
+// at its three grid-wide seams (coloring.py:73-132):
+//   propose  -> publish (v, candidate) of the rank's proposers      (coloring.py:44-54)
+//   resolve, each JP sweep -> publish (v, IN|OUT) of decided ones   (coloring.py:56-70)
+//   accept   -> publish (v, colour) of the rank's winners           (coloring.py:114-127)
+// The caller (gcolor_amd/shard.py) all-gathers the deltas over RCCL and hands every rank
+// the full set back: gc_shard_apply / gc_shard_push.  Because the conflict resolution is
+// the lexicographically-first MIS under the global rank (deg, pos), the result does not
+// depend on the partition: it is bit-identical to gc_color on one GPU.
+//
+// Every call is synchronous (the caller needs the counts for the exchange) and works on
+// caller-owned device buffers of int64 deltas (vertex << 32 | value).
+#include <string.h>
+
+#include <algorithm>
+
+#include "gc_engine.h"
+
+struct gc_shard {
+    gc_graph v;  // borrowed CSR + own in-neighbour CSR + own run state
+    long long lo = 0, hi = 0;
+};
+
+static int shard_sync(gc_shard* sh) {
+    gc_graph* g = &sh->v;
+    GC_HIP(hipGetLastError());
+    GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
+    GC_HIP(hipStreamSynchronize(g->stream));
+    return GC_OK;
+}
+
+static GLists shard_lists(gc_shard* sh, int64_t* delta) {
+    GLists L = gc_lists(&sh->v);
+    L.delta = reinterpret_cast<long long*>(delta);
+    return L;
+}
+
+extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** out) {
+    if (!g || !out) { gc_set_error("gc_shard_create: null argument"); return GC_EINVAL; }
+    if (lo < 0 || hi < lo || hi > g->n) { gc_set_error("gc_shard_create: bad range [%lld, %lld)", (long long)lo, (long long)hi); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    gc_shard* sh = new gc_shard();
+    gc_graph& v = sh->v;
+    v.device = g->device;
+    v.n = g->n;
+    v.nnz = g->nnz;
+    v.maxdeg = g->maxdeg;
+    v.flags = g->flags & ~GC_GRAPH_SYMMETRIC;
+    v.borrowed = true;
+    v.rp = g->rp;
+    v.col = g->col;
+    v.deg = g->deg;
+    v.nlow = g->nlow;
+    sh->lo = lo;
+    sh->hi = hi;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&v.ev0)) != hipSuccess || (e = hipEventCreate(&v.ev1)) != hipSuccess ||
+        (e = hipMalloc((void**)&v.ctl, sizeof(DevCtl))) != hipSuccess ||
+        (e = hipHostMalloc((void**)&v.hctl, sizeof(DevCtl), hipHostMallocDefault)) != hipSuccess) {
+        gc_set_error("shard allocation failed: %s", hipGetErrorString(e));
+        gc_free_all(&v);
+        delete sh;
+        return GC_ENOMEM;
+    }
+    int rc = gc_build_in_csr(&v, lo, hi);
+    if (!rc) rc = gc_alloc_run_state(&v);
+    if (rc) {
+        std::string keep = gc_last_error();
+        gc_free_all(&v);
+        delete sh;
+        gc_set_error("%s", keep.c_str());
+        return rc;
+    }
+    *out = sh;
+    return GC_OK;
+}
+
+extern "C" void gc_shard_destroy(gc_shard* sh) {
+    if (!sh) return;
+    gc_free_all(&sh->v);
+    delete sh;
+}
+
+// init + seed on the replicated state (coloring.py:74-76); the seeds push into the
+// rank's own in-neighbours.  U is global (replicated), F is this rank's frontier.
+extern "C" int gc_shard_begin(gc_shard* sh, int64_t num_colors, int32_t track_rounds, int64_t* U_out, int64_t* F_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    DevCtl& h = *g->hctl;
+    memset(&h, 0, sizeof(DevCtl));
+    h.kbound = num_colors;
+    h.e1 = 1;
+    h.rcap = g->rcap;
+    h.maxmex = -1;
+    h.maxcolor = -1;
+    h.fail_round = -1;
+    h.want_cround = track_rounds ? 1 : 0;
+    GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, g->stream));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, nullptr);
+    gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), g->stream);
+    gcl_seed_prep(d, g->seeds[0], g->seeds[1], g->stream);
+    gcl_commit(d, L, GC_CM_INIT, 0, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    if (U_out) *U_out = (int64_t)h.uncolored - (h.seedkey ? 1 : 0);
+    if (F_out) *F_out = (int64_t)h.fcnt[h.cur];
+    return GC_OK;
+}
+
+// propose on the rank's frontier; delta = (v, candidate) per proposer.
+// stats: [0] deltas written, [1] frontier size, [2] max candidate (-1), [3] #candidates >= k
+extern "C" int gc_shard_propose(gc_shard* sh, int64_t round, int64_t* delta, int64_t cap, int64_t* stats) {
+    if (!sh || !delta || !stats) { gc_set_error("null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, delta);
+    gcl_shard_reset(d, round, g->stream);
+    gcl_pack_c4(d, g->stream);
+    gcl_propose(d, L, g->stream);
+    gcl_propose_block(d, L, g->stream);
+    gcl_delta_cand(d, L, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    const DevCtl& h = *g->hctl;
+    stats[0] = (int64_t)h.fcnt[h.cur];
+    stats[1] = (int64_t)h.fcnt[h.cur];
+    stats[2] = h.maxmex;
+    stats[3] = (int64_t)h.failcnt;
+    return GC_OK;
+}
+
+// apply every rank's deltas of one kind to the vertices this rank does not own
+extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, int64_t count, int64_t round) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    if (kind < GC_KIND_CAND || kind > GC_KIND_COLOUR) { gc_set_error("bad delta kind %d", kind); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    if (count > 0 && !recv) { gc_set_error("null delta buffer"); return GC_EINVAL; }
+    gcl_apply(gc_view(g), kind, reinterpret_cast<const long long*>(recv), count, sh->lo, sh->hi, (int)round + 1,
+              g->stream);
+    GC_HIP(hipGetLastError());
+    GC_HIP(hipStreamSynchronize(g->stream));
+    return GC_OK;
+}
+
+// first JP sweep (i = 0) or sweep i >= 1 over the rank's undecided lists;
+// delta = (v, IN|OUT) of the vertices decided.  stats: [0] deltas, [1] still undecided
+extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int64_t* delta, int64_t cap, int64_t* stats) {
+    if (!sh || !delta || !stats || i < 0) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, delta);
+    GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
+    if (i == 0) gcl_resolve(d, L, g->stream);
+    else gcl_sweep(d, L, i, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    const DevCtl& h = *g->hctl;
+    stats[0] = (int64_t)h.dcnt;
+    stats[1] = (int64_t)(h.und_cnt[i % 3] + h.undh_cnt[i % 3]);
+    return GC_OK;
+}
+
+// colour the rank's winners; delta = (v, colour).  stats: [0] deltas (= accepted)
+extern "C" int gc_shard_accept(gc_shard* sh, int64_t round, int64_t* delta, int64_t cap, int64_t* stats) {
+    if (!sh || !delta || !stats) { gc_set_error("null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    const GLists L = shard_lists(sh, delta);
+    GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
+    gcl_commit(gc_view(g), L, GC_CM_ACCEPT, 0, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    stats[0] = (int64_t)g->hctl->dcnt;
+    (void)round;
+    return GC_OK;
+}
+
+// every rank's winners: colour the ones owned elsewhere, push all of them into this
+// rank's in-neighbours (next frontier), make that frontier current.
+extern "C" int gc_shard_push(gc_shard* sh, int64_t round, const int64_t* recv, int64_t count, int64_t* F_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    if (count > 0 && !recv) { gc_set_error("null delta buffer"); return GC_EINVAL; }
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, nullptr);
+    const long long* r = reinterpret_cast<const long long*>(recv);
+    gcl_apply(d, GC_KIND_COLOUR, r, count, sh->lo, sh->hi, (int)round + 1, g->stream);
+    gcl_push_list(d, L, r, count, g->stream);
+    gcl_shard_flip(d, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    if (F_out) *F_out = (int64_t)g->hctl->fcnt[g->hctl->cur];
+    return GC_OK;
+}
+
+// E1 on the replicated state (identical seeds on every rank), seeds pushed into the
+// rank's own in-neighbours.
+extern "C" int gc_shard_reseed(gc_shard* sh, int64_t round, int64_t* nseeds, int64_t* F_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, nullptr);
+    gcl_shard_reset(d, round, g->stream);
+    gcl_unc_compact(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gc_grid_for_waves(g->n), g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    const long long Lc = (long long)g->hctl->list_cnt;
+    gcl_cc_hook(d, g->ulist, &g->ctl->list_cnt, g->parent, gc_grid_for_waves(Lc), g->stream);
+    gcl_cc_best(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gc_grid_for_waves(Lc, 4096), g->stream);
+    gcl_cc_seeds(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, g->seeds[0], g->seeds[1],
+                 gc_grid_for_waves(Lc, 4096), g->stream);
+    gcl_commit(d, L, GC_CM_RESEED, 0, g->stream);
+    if ((rc = shard_sync(sh))) return rc;
+    if (nseeds) *nseeds = (int64_t)(g->hctl->seed_cnt[0] + g->hctl->seed_cnt[1]);
+    if (F_out) *F_out = (int64_t)g->hctl->fcnt[g->hctl->cur];
+    return GC_OK;
+}
+
+// final colours (every rank holds all of them) and optionally the round of colouring
+extern "C" int gc_shard_colors(gc_shard* sh, int32_t* colors_out, int32_t* cround_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    gcl_finalize(gc_view(g), gc_grid_for_waves(g->n, 8192), g->stream);
+    if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, g->stream));
+    if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, g->stream));
+    return shard_sync(sh);
+}

@@ -125,6 +125,38 @@ int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* c
    gc_color on this handle without a host round trip.                                 */
 int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts);
 
+/* ---- multi-GPU shards ------------------------------------------------ */
+/* One rank's share of a colouring on the graph g (every rank holds the whole CSR): the
+   rank owns vertices [lo, hi) and runs the round on its own frontier.  A round is cut at
+   its three grid-wide seams -- propose, each Jones-Plassmann sweep, accept -- where the
+   rank publishes int64 deltas (vertex << 32 | value) of its own vertices into a caller-
+   owned DEVICE buffer (capacity >= hi - lo) and applies everyone's (gc_shard_apply /
+   gc_shard_push).  The caller moves the deltas between ranks (RCCL all-gather in
+   gcolor_amd/shard.py).  The colouring is bit-identical to gc_color on one GPU.
+   Replaces: the Spark shuffle/broadcast of each round (coloring.py:82-83, 110-127).  */
+typedef struct gc_shard gc_shard;
+#define GC_KIND_CAND 0   /* (v, candidate): propose seam                                */
+#define GC_KIND_STATE 1  /* (v, 1 = IN | 2 = OUT): JP sweep seam                        */
+#define GC_KIND_COLOUR 2 /* (v, colour): accept seam (gc_shard_push applies these)      */
+int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** out);
+void gc_shard_destroy(gc_shard* s);
+/* init + seed (coloring.py:12-35) on the replicated state; *U_out global uncoloured,
+   *F_out this rank's frontier                                                         */
+int gc_shard_begin(gc_shard* s, int64_t num_colors, int32_t track_rounds, int64_t* U_out, int64_t* F_out);
+/* stats[4]: deltas written, frontier size, max candidate (-1 none), #candidates >= k    */
+int gc_shard_propose(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
+int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);
+/* i = 0: first sweep over the frontier, i >= 1: sweep over the undecided;
+   stats[2]: deltas written, vertices still undecided on this rank                     */
+int gc_shard_sweep(gc_shard* s, int32_t i, int64_t* delta, int64_t cap, int64_t* stats);
+/* stats[1]: winners coloured (= deltas written)                                        */
+int gc_shard_accept(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
+/* all ranks' winners: colour the remote ones, push into own in-neighbours, next round */
+int gc_shard_push(gc_shard* s, int64_t round, const int64_t* recv, int64_t count, int64_t* F_out);
+/* E1 re-seed on the replicated state (same seeds on every rank)                        */
+int gc_shard_reseed(gc_shard* s, int64_t round, int64_t* nseeds, int64_t* F_out);
+int gc_shard_colors(gc_shard* s, int32_t* colors_out, int32_t* colored_round_out);
+
 /* ---- host-side generator ------------------------------------------------------------ */
 /* The graph.py:30-43 process (per node: target = U{0..D}; draw random partners, keep
    those that are not self, not yet adjacent and below D) with a splitmix64 stream

@@ -1,0 +1,150 @@
+"""CPU stand-in for gcolor_amd.shard.HipShard (TEST INFRASTRUCTURE ONLY).
+
+Same phase interface and delta format as the HIP shard, computed with numpy/Python on
+the rank's replicated copy of the state, so the multi-rank driver
+(gcolor_amd.shard.shard_color) and its torch.distributed / thread transports can be
+tested on CPU (gloo).  The phase semantics restate coloring.py:44-70, 114-127 (see
+oracle/gcolor_oracle.c): the frontier is recomputed from the colours (uncoloured with a
+coloured listed neighbour), independently of the GPU's push-based frontier.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle.oracle import _components_argmax  # noqa: E402
+
+UND, IN, OUT = 0, 1, 2
+
+
+class NumpyShard:
+    def __init__(self, rp, col, lo, hi):
+        self.rp = np.asarray(rp, np.int64)
+        self.col = np.asarray(col, np.int64)
+        self.n = len(self.rp) - 1
+        self.lo, self.hi = int(lo), int(hi)
+        self.deg = np.diff(self.rp)
+        self.adj = [self.col[self.rp[v]:self.rp[v + 1]].tolist() for v in range(self.n)]
+        key = [(int(self.deg[v]), v) for v in range(self.n)]
+        self.lower = [[u for u in self.adj[v] if key[u] < key[v]] for v in range(self.n)]
+        self.delta = torch.empty(max(self.hi - self.lo, 1), dtype=torch.int64)
+
+    # delta entries: vertex << 32 | value (value as unsigned 32 bits)
+    def _emit(self, pairs):
+        for i, (v, val) in enumerate(pairs):
+            self.delta[i] = (v << 32) | (val & 0xFFFFFFFF)
+        return len(pairs)
+
+    @staticmethod
+    def _decode(recv, tot):
+        if recv is None or not tot:
+            return []
+        out = []
+        for e in recv[:tot].tolist():
+            v = e >> 32
+            if v < 0:
+                continue
+            val = e & 0xFFFFFFFF
+            out.append((v, val - (1 << 32) if val >= 1 << 31 else val))
+        return out
+
+    def _owned(self, v):
+        return self.lo <= v < self.hi
+
+    def _frontier(self):
+        c = self.c
+        return [v for v in range(self.lo, self.hi) if c[v] == -1 and any(c[u] >= 0 for u in self.adj[v])]
+
+    def begin(self, k, track):
+        self.k, self.track = k, track
+        self.c = np.where(self.deg == 0, 0, -1).astype(np.int64)
+        self.cround = np.where(self.deg == 0, 0, -1).astype(np.int64)
+        seed = None
+        for v in range(self.n):                       # coloring.py:21-22, ties -> last
+            if self.c[v] == -1 and (seed is None or self.deg[v] >= self.deg[seed]):
+                seed = v
+        if seed is not None:
+            self.c[seed], self.cround[seed] = 0, 0
+        self.cand = np.full(self.n, -1, np.int64)
+        self.state = np.zeros(self.n, np.int64)
+        return int((self.c == -1).sum()), len(self._frontier())
+
+    def propose(self, r):
+        self.cand[:] = -1
+        self.state[:] = UND
+        self.F = self._frontier()
+        pairs, mm, fails = [], -1, 0
+        for v in self.F:
+            used = {int(self.c[u]) for u in self.adj[v] if self.c[u] >= 0}
+            mex = 0
+            while mex in used:
+                mex += 1
+            self.cand[v] = mex
+            mm = max(mm, mex)
+            if self.k >= 0 and mex >= self.k:
+                fails += 1
+            pairs.append((v, mex))
+        return self._emit(pairs), len(self.F), mm, fails
+
+    def apply(self, kind, recv, tot, r):
+        for v, val in self._decode(recv, tot):
+            if self._owned(v):
+                continue
+            if kind == 0:
+                self.cand[v], self.state[v] = val, UND
+            elif kind == 1:
+                self.state[v] = val
+            else:
+                self._colour(v, val, r)
+
+    def _colour(self, v, val, r):
+        self.c[v] = val
+        self.cand[v] = -1
+        if self.track:
+            self.cround[v] = r + 1
+
+    def sweep(self, i):
+        todo = self.F if i == 0 else self.und
+        pairs, und = [], []
+        for v in todo:
+            f = 0
+            for u in self.lower[v]:
+                if self.cand[u] == self.cand[v] and self.cand[u] >= 0:
+                    f |= 1 if self.state[u] == IN else (2 if self.state[u] == UND else 0)
+            if f & 1:
+                self.state[v] = OUT
+                pairs.append((v, OUT))
+            elif f & 2:
+                und.append(v)
+            else:
+                self.state[v] = IN
+                pairs.append((v, IN))
+        self.und = und
+        return self._emit(pairs), len(und)
+
+    def accept(self, r):
+        pairs = []
+        for v in self.F:
+            if self.state[v] == IN:
+                pairs.append((v, int(self.cand[v])))
+        for v, cc in pairs:
+            self._colour(v, cc, r)
+        return self._emit(pairs)
+
+    def push(self, r, recv, tot):
+        for v, val in self._decode(recv, tot):
+            if not self._owned(v):
+                self._colour(v, val, r)
+        return len(self._frontier())
+
+    def reseed(self, r):
+        seeds = _components_argmax(self.adj, self.deg.tolist(), self.c.tolist())
+        for s in seeds:
+            self.c[s] = 0
+            self.cround[s] = r + 1
+        return len(seeds), len(self._frontier())
+
+    def colors(self, track):
+        return self.c.astype(np.int32), (self.cround.astype(np.int32) if track else None)

@@ -1,0 +1,150 @@
+"""Multi-rank driver of the sharded engine (gcolor_amd.shard) on CPU.
+
+The HIP phases are replaced by tests/shard_numpy.NumpyShard (same interface and delta
+format); the driver, the exchange protocol and both transports are the product code.
+Results must equal the single-partition oracle bit for bit: LFMIS under the global rank
+(deg, pos) does not depend on the partition.
+"""
+import json
+import os
+import random
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
+
+sys.path.insert(0, REPO)
+from oracle import oracle  # noqa: E402
+from shard_numpy import NumpyShard  # noqa: E402
+
+from gcolor_amd import shard as sh  # noqa: E402
+
+
+def _random_directed(n, m, seed):
+    rng = np.random.default_rng(seed)
+    src = np.sort(rng.integers(0, n, m))
+    dst = rng.integers(0, n, m)
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    return np.cumsum(rp), dst.astype(np.int32)
+
+
+def run_threads(rp, col, parts, k=None, e1=True):
+    ranges = sh.balanced_ranges(rp, parts)
+    hub = sh.ThreadHub(parts)
+    out, err = [None] * parts, []
+
+    def go(i):
+        try:
+            ops = NumpyShard(rp, col, *ranges[i])
+            out[i] = sh.shard_color(ops, sh.ThreadTransport(hub, i), k, e1, track_rounds=True)
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            hub.barrier.abort()
+
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(parts)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if err:
+        raise err[0]
+    return out
+
+
+def assert_matches_oracle(res, o):
+    assert res.status == o["status"]
+    assert np.array_equal(res.colors, o["colors"])
+    assert np.array_equal(res.colored_round, o["colored_round"])
+    for key in ("U", "F", "maxmex", "accepted", "seeds"):
+        assert list(getattr(res, "round_" + key)) == list(o["round_" + key]), key
+    assert res.reseeds == o["reseeds"]
+    if res.status == oracle.FAILED:
+        assert (res.fail_round, res.fail_count) == (o["fail_round"], o["fail_count"])
+
+
+def test_balanced_ranges_cover_and_balance():
+    rp = np.cumsum(np.r_[0, np.random.default_rng(0).integers(0, 50, 1000)])
+    for parts in (1, 2, 3, 8):
+        rs = sh.balanced_ranges(rp, parts)
+        assert rs[0][0] == 0 and rs[-1][1] == 1000
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+        w = [int(rp[hi] - rp[lo] + hi - lo) for lo, hi in rs]
+        assert max(w) - min(w) <= 2 * (50 + 1)  # each boundary is off by at most one vertex
+    assert sh.balanced_ranges(np.zeros(1, np.int64), 4) == [(0, 0)] * 4
+
+
+GOLD = [n for n in golden_names() if "load_error" not in load_golden(n)["variants"]["A"]["run"]
+        and len(load_golden(n)["graph"]) <= 1000]
+
+
+@pytest.mark.parametrize("name", GOLD)
+@pytest.mark.parametrize("parts", [2, 3])
+def test_threads_match_oracle_on_golden_graphs(name, parts):
+    ids, adj, rp, col = fixture_csr(load_golden(name))
+    res = run_threads(rp, col, parts)
+    o = oracle.c_color(rp, col, "A")
+    for r in res:  # every rank holds the same result
+        assert_matches_oracle(r, o)
+    run = load_golden(name)["variants"]["A"]["run"]
+    if run.get("colors") is not None:
+        assert list(res[0].colors) == run["colors"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_threads_directed_selfloops_bounded_and_stalled(seed):
+    rp, col = _random_directed(300, 900, seed)
+    o = oracle.c_color(rp, col, "A")
+    assert_matches_oracle(run_threads(rp, col, 3)[0], o)
+    for k in (1, int(o["max_color"])):
+        assert_matches_oracle(run_threads(rp, col, 2, k=k)[1], oracle.c_color(rp, col, "A", k=k))
+    s = oracle.c_color(rp, col, "A", e1=False)
+    r = run_threads(rp, col, 2, e1=False)[0]
+    assert r.status == s["status"] and np.array_equal(r.colors, s["colors"])
+
+
+def test_more_ranks_than_vertices():
+    rp = np.array([0, 1, 2], np.int64)
+    col = np.array([1, 0], np.int32)
+    res = run_threads(rp, col, 4)
+    assert_matches_oracle(res[3], oracle.c_color(rp, col, "A"))
+
+
+# ---- two processes over torch.distributed (gloo), the transport the GPU ranks use -------
+def _gloo_worker(rank, world, port, path, out_dir):
+    import torch.distributed as dist
+    sys.path[:0] = [PKG_DIR, REPO, os.path.dirname(os.path.abspath(__file__))]
+    from shard_numpy import NumpyShard as NS
+    from gcolor_amd import shard as shm
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    d = np.load(path)
+    rp, col = d["rp"], d["col"]
+    lo, hi = shm.balanced_ranges(rp, world)[rank]
+    res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, track_rounds=True)
+    out = {"status": res.status, "colors": res.colors.tolist(), "cround": res.colored_round.tolist(),
+           "U": res.round_U, "F": res.round_F, "maxmex": res.round_maxmex, "acc": res.round_accepted,
+           "seeds": res.round_seeds}
+    with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["gen_1000_8_s1", "asymmetric"])
+def test_gloo_world_size_2(case, tmp_path):
+    ids, adj, rp, col = fixture_csr(load_golden(case))
+    path = str(tmp_path / "g.npz")
+    np.savez(path, rp=rp, col=col)
+    port = 29500 + random.randint(0, 2000)
+    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path)), nprocs=2, join=True)
+    o = oracle.c_color(rp, col, "A")
+    for r in range(2):
+        got = json.load(open(tmp_path / f"r{r}.json"))
+        assert got["status"] == o["status"]
+        assert got["colors"] == list(o["colors"])
+        assert got["cround"] == list(o["colored_round"])
+        assert got["U"] == list(o["round_U"]) and got["F"] == list(o["round_F"])
+        assert got["acc"] == list(o["round_accepted"]) and got["seeds"] == list(o["round_seeds"])

@@ -1,0 +1,133 @@
+"""Sharded HIP engine (gc_shard_* through the C-ABI) on the GPU.
+
+Several shards of one colouring run on the one GPU of the box -- as threads of one
+process (ThreadTransport) and as two processes over torch.distributed (gloo) -- and must
+reproduce the single-GPU engine and the oracle bit for bit (LFMIS under the
+global rank does not depend on the partition).
+"""
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
+
+sys.path.insert(0, REPO)
+from oracle import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_directed(n, m, seed):
+    rng = np.random.default_rng(seed)
+    src = np.sort(rng.integers(0, n, m))
+    dst = rng.integers(0, n, m)
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    return np.cumsum(rp), dst.astype(np.int32)
+
+
+def same_as_single(dg, parts, k=None, e1=True):
+    from gcolor_amd import shard as sh
+    one = dg.color("A", num_colors=k, e1=e1)
+    res = sh.color_threads(dg, parts, num_colors=k, e1=e1, track_rounds=True)
+    for r in res:
+        assert r.status == one.status
+        assert np.array_equal(r.colors, one.colors)
+        assert np.array_equal(r.colored_round, one.colored_round)
+        assert list(r.round_U) == list(one.round_U)
+        assert list(r.round_F) == list(one.round_F)
+        assert list(r.round_maxmex) == list(one.round_maxmex)
+        assert list(r.round_accepted) == list(one.round_accepted)
+        assert list(r.round_seeds) == list(one.round_seeds)
+        if one.status == 1:
+            assert (r.fail_round, r.fail_count) == (one.fail_round, one.fail_count)
+    return res[0], one
+
+
+GOLD = [n for n in golden_names() if "load_error" not in load_golden(n)["variants"]["A"]["run"]]
+
+
+@pytest.mark.parametrize("name", GOLD[::3])
+def test_golden_graphs_sharded(name):
+    from gcolor_amd.engine import DeviceGraph
+    ids, adj, rp, col = fixture_csr(load_golden(name))
+    with DeviceGraph.from_csr(rp, col) as dg:
+        r, _ = same_as_single(dg, 3)
+        o = oracle.c_color(rp, col, "A")
+        assert np.array_equal(r.colors, o["colors"])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_directed_multigraph_sharded_bounded_and_stalled(seed):
+    from gcolor_amd.engine import DeviceGraph
+    rp, col = _random_directed(3000, 9000, seed)
+    with DeviceGraph.from_csr(rp, col) as dg:
+        r, one = same_as_single(dg, 2)
+        same_as_single(dg, 4, k=max(one.max_color, 1))
+        same_as_single(dg, 3, e1=False)
+
+
+def test_rmat_hubs_and_wide_mex_sharded():
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(12, 16, seed=5) as dg:
+        r, one = same_as_single(dg, 4)
+        assert dg.max_degree > 256 and one.max_color >= 32
+        assert dg.validate(r.colors) == (0, 0)
+
+
+def test_e1_reseeds_sharded():
+    """random.seed(1); Graph(10000, 8) has components the reference never reaches (Q1)."""
+    from gcolor_amd.engine import DeviceGraph
+    from gcolor_amd.generators import reference_csr
+    rp, col = reference_csr(10000, 8, random.Random(1))
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        r, one = same_as_single(dg, 3)
+        assert one.reseeds > 0 and r.reseeds == one.reseeds
+
+
+def test_uniform_and_mesh_sharded():
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    rp, col = uniform_csr(200_000, 16, 3)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        same_as_single(dg, 8)
+    with DeviceGraph.mesh(20, 16, 12) as dg:
+        r, _ = same_as_single(dg, 3)
+        assert r.max_color + 1 == 2
+
+
+def _gloo_gpu_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    sys.path[:0] = [PKG_DIR, REPO]
+    torch.cuda.set_device(0)
+    from gcolor_amd.engine import DeviceGraph
+    from gcolor_amd import shard as sh
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    with DeviceGraph.rmat(11, 16, seed=9) as dg:
+        rp, _ = dg.export()
+        lo, hi = sh.balanced_ranges(rp, world)[rank]
+        ops = sh.HipShard(dg, lo, hi)
+        res = sh.shard_color(ops, sh.TorchTransport(), None, True, track_rounds=True)
+        ops.close()
+        out = {"colors": res.colors.tolist(), "U": res.round_U, "acc": res.round_accepted,
+               "seeds": res.round_seeds}
+    with open(os.path.join(out_dir, f"g{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def test_two_processes_over_torch_distributed(tmp_path):
+    from gcolor_amd.engine import DeviceGraph
+    port = 31000 + random.randint(0, 2000)
+    torch.multiprocessing.spawn(_gloo_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    with DeviceGraph.rmat(11, 16, seed=9) as dg:
+        one = dg.color("A")
+    for r in range(2):
+        got = json.load(open(tmp_path / f"g{r}.json"))
+        assert got["colors"] == list(one.colors)
+        assert got["U"] == list(one.round_U) and got["acc"] == list(one.round_accepted)
+        assert got["seeds"] == list(one.round_seeds)
