@@ -25,6 +25,8 @@ import platform
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(REPO, "distributed-graph-coloring-with-pyspark_amd")
 sys.path.insert(0, PKG_DIR)
@@ -89,6 +91,89 @@ def cpu_baseline(w, host_csr, dg):
             "colors": int(o["max_color"]) + 1, "seconds": dt}, o
 
 
+def run_sharded(args, world, rank, local_rank, dist, torch):
+    """N > 1: ONE graph, vertex-range shards over the N ranks (gcolor_amd.shard), round
+    deltas all-gathered over RCCL.  Weak scaling: the per-GPU share is the N=1 workload
+    (uniform: n = 10M x N; R-MAT: scale + log2 N; mesh: z x N)."""
+    import math
+    from gcolor_amd import _native
+    from gcolor_amd import shard as sh
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
+    w = dict(WORKLOADS[args.workload])
+    t0 = time.time()
+    if w["kind"] == "uniform":
+        w["n"] *= world
+        rp, col = uniform_csr(w["n"], w["d"], w["seed"])
+        dg = DeviceGraph.from_csr(rp, col, symmetric=True)
+        del col
+        desc = f"uniform (graph.py:30-43 process) n={w['n'] // 10**6}M (= 10M x {world} GPUs), max-degree {w['d']}"
+    elif w["kind"] == "rmat":
+        w["scale"] += int(round(math.log2(world)))
+        dg = DeviceGraph.rmat(w["scale"], w["ef"], seed=w["seed"])
+        rp, _ = dg.export()
+        desc = f"R-MAT scale {w['scale']} (= base + log2 {world}), edge factor {w['ef']}, seed {w['seed']}"
+    else:
+        x, y, z = w["dims"]
+        w["dims"] = (x, y, z * world)
+        dg = DeviceGraph.mesh(*w["dims"])
+        rp, _ = dg.export()
+        desc = f"3-D 7-point mesh {x}x{y}x{z * world} (z-slabs)"
+    gen_s = time.time() - t0
+    m = dg.nnz // 2
+    lo, hi = sh.balanced_ranges(rp, world)[rank]
+    ops = sh.HipShard(dg, lo, hi)
+    comm = sh.TorchTransport()
+
+    def barrier():
+        torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(max(args.warmup, 1)):
+        res = sh.shard_color(ops, comm)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = sh.shard_color(ops, comm)
+    barrier()
+    t = (time.perf_counter() - t0) / args.steps
+    tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt.item())
+    line = None
+    if rank == 0:
+        unc, conf = dg.validate(res.colors)
+        assert unc == 0 and conf == 0, f"invalid colouring: {unc} uncoloured, {conf} conflicts"
+        one = dg.color("A", want_rounds=False, want_colors=True)  # reference run (outside timing)
+        assert np.array_equal(one.colors, res.colors), "sharded colouring differs from the 1-GPU engine"
+        balg = one.balg_bytes + 20.0 * dg.n + 8.0 * dg.nnz
+        achieved = balg / world / t / 1e9
+        line = {
+            "metric": METRIC, "value": m / t, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "config": {"workload": desc, "n": dg.n, "m_undirected": m, "nnz": dg.nnz, "max_degree": dg.max_degree,
+                       "variant": "A (coloring.py)",
+                       "parallelism": f"{world} vertex-range shards, round seams all-gathered over RCCL "
+                                      "(deltas, or proposal-byte slices when denser)",
+                       "rounds": res.rounds, "exchanges_per_step": res.exchanges,
+                       "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
+                       "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2)},
+            "colors_used": res.max_color + 1,
+            "roofline": {"bound": "hbm", "kernel": "whole colouring per GPU (sharded)", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+            "whole_job_hbm_frac": achieved / HBM_PEAK_GBS,
+            "cpu_baseline": None,
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(s + "\n")
+    ops.close()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,6 +182,8 @@ def main():
     ap.add_argument("--workload", default="uniform10M", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--replicas", action="store_true",
+                    help="N>1: colour N independent copies (one per GPU) instead of one sharded graph")
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
@@ -108,8 +195,18 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # GC_BENCH_DEVICE pins every rank to one GPU (rehearsal of the multi-rank path on a
+        # 1-GPU box, with GC_BENCH_BACKEND=gloo); the driver's runs use one GPU per rank
+        dev = int(os.environ.get("GC_BENCH_DEVICE", local_rank))
+        local_rank = dev
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("GC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+        if not args.replicas:
+            return run_sharded(args, world, rank, local_rank, dist, torch)
     else:
         torch.cuda.set_device(0)
 

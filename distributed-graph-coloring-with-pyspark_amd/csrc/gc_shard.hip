@@ -153,23 +153,58 @@ extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, i
     return GC_OK;
 }
 
-// first JP sweep (i = 0) or sweep i >= 1 over the rank's undecided lists;
-// delta = (v, IN|OUT) of the vertices decided.  stats: [0] deltas, [1] still undecided
-extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int64_t* delta, int64_t cap, int64_t* stats) {
-    if (!sh || !delta || !stats || i < 0) { gc_set_error("bad argument"); return GC_EINVAL; }
+// JP sweeps i, i+1, ..., i+count-1 over the rank's lists (i = 0 is the first sweep over
+// the frontier; later sweeps run over the undecided); the rank's later sweeps can decide
+// vertices whose lower-rank neighbours are its own, so several run between two
+// exchanges.  delta = (v, IN|OUT) of every vertex decided.
+// stats: [0] deltas, [1] still undecided on this rank
+extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats) {
+    if (!sh || !delta || !stats || i < 0 || count < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
     const GDev d = gc_view(g);
     const GLists L = shard_lists(sh, delta);
     GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
-    if (i == 0) gcl_resolve(d, L, g->stream);
-    else gcl_sweep(d, L, i, g->stream);
+    for (int j = i; j < i + count; ++j) {
+        if (j == 0) gcl_resolve(d, L, g->stream);
+        else gcl_sweep(d, L, j, g->stream);
+    }
     int rc = shard_sync(sh);
     if (rc) return rc;
     const DevCtl& h = *g->hctl;
+    const int last = (i + count - 1) % 3;
     stats[0] = (int64_t)h.dcnt;
-    stats[1] = (int64_t)(h.und_cnt[i % 3] + h.undh_cnt[i % 3]);
+    stats[1] = (int64_t)(h.und_cnt[last] + h.undh_cnt[last]);
+    return GC_OK;
+}
+
+// Dense form of the propose / sweep seams when most vertices changed: the rank's slice
+// [lo, hi) of the proposal bytes k8 (cand6 << 2 | JP state) instead of 8-byte deltas.
+extern "C" int gc_shard_get_slice(gc_shard* sh, uint8_t* dst) {
+    if (!sh || !dst) { gc_set_error("null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    if (sh->hi > sh->lo)
+        GC_HIP(hipMemcpyAsync(dst, g->k8 + sh->lo, (size_t)(sh->hi - sh->lo), hipMemcpyDeviceToDevice, g->stream));
+    GC_HIP(hipStreamSynchronize(g->stream));
+    return GC_OK;
+}
+
+// src holds `parts` slices of `stride` bytes; slice p covers [starts[p], starts[p]+lens[p])
+// (host arrays).  Every slice but the rank's own is copied into k8.
+extern "C" int gc_shard_put_slices(gc_shard* sh, const uint8_t* src, int64_t stride, const int64_t* starts,
+                                   const int64_t* lens, int32_t parts) {
+    if (!sh || !src || !starts || !lens) { gc_set_error("null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    for (int p = 0; p < parts; ++p) {
+        if (starts[p] == sh->lo || lens[p] <= 0) continue;
+        if (starts[p] < 0 || starts[p] + lens[p] > g->n || lens[p] > stride) { gc_set_error("bad slice %d", p); return GC_EINVAL; }
+        GC_HIP(hipMemcpyAsync(g->k8 + starts[p], src + (size_t)p * (size_t)stride, (size_t)lens[p],
+                              hipMemcpyDeviceToDevice, g->stream));
+    }
+    GC_HIP(hipStreamSynchronize(g->stream));
     return GC_OK;
 }
 

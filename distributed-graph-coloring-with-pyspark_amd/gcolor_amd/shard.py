@@ -49,7 +49,7 @@ def balanced_ranges(rp, parts):
 # transports
 # ------------------------------------------------------------------------------------------
 class TorchTransport:
-    """All-gather over a torch.distributed group: RCCL (``nccl``) on device tensors, or
+    """All-gathers over a torch.distributed group: RCCL (``nccl``) on device tensors, or
     ``gloo`` (device tensors are staged through host memory)."""
 
     def __init__(self, group=None):
@@ -66,29 +66,39 @@ class TorchTransport:
         else:
             self.dist.all_gather(list(out.chunk(self.size)), inp, group=self.group)
 
-    def exchange(self, stats, delta, count):
-        """stats: ints of this rank; delta[:count]: its deltas.  Returns (all ranks' stats
-        as an int64 array [size, len(stats) + 1] whose last column is the counts, the
-        concatenated deltas padded with -1 entries (or None), its length)."""
-        dev = delta.device if delta is not None else torch.device("cpu")
-        cdev = dev if self.backend == "nccl" else torch.device("cpu")
-        s = torch.tensor(list(stats) + [int(count)], dtype=torch.int64, device=cdev)
-        all_s = torch.empty(self.size * s.numel(), dtype=torch.int64, device=cdev)
-        self._allgather(all_s, s)
-        all_s = all_s.view(self.size, -1).cpu().numpy()
-        maxc = int(all_s[:, -1].max())
-        if maxc == 0:
-            return all_s, None, 0
-        send = torch.full((maxc,), -1, dtype=torch.int64, device=cdev)
-        if count:
-            send[:count].copy_(delta[:count])
-        recv = torch.empty(self.size * maxc, dtype=torch.int64, device=cdev)
+    def _cdev(self, dev):
+        return dev if self.backend == "nccl" else torch.device("cpu")
+
+    def gather_stats(self, stats, device):
+        """ints of this rank -> int64 array [size, len(stats)] of every rank's."""
+        cdev = self._cdev(device)
+        s = torch.tensor([int(x) for x in stats], dtype=torch.int64, device=cdev)
+        out = torch.empty(self.size * s.numel(), dtype=torch.int64, device=cdev)
+        self._allgather(out, s)
+        return out.view(self.size, -1).cpu().numpy()
+
+    def _gather_padded(self, send, dev):
+        recv = torch.empty(self.size * send.numel(), dtype=send.dtype, device=send.device)
         self._allgather(recv, send)
         if recv.device != dev:
             recv = recv.to(dev)
         if dev.type == "cuda":
             torch.cuda.current_stream(dev).synchronize()
-        return all_s, recv, int(recv.numel())
+        return recv
+
+    def gather_deltas(self, delta, count, maxc):
+        """delta[:count] of every rank, each padded to maxc with -1 entries."""
+        dev = delta.device
+        send = torch.full((maxc,), -1, dtype=torch.int64, device=self._cdev(dev))
+        if count:
+            send[:count].copy_(delta[:count])
+        return self._gather_padded(send, dev)
+
+    def gather_slices(self, buf):
+        """buf (uint8, the same length on every rank) of every rank, concatenated."""
+        dev = buf.device
+        send = buf if self._cdev(dev) == dev else buf.to(self._cdev(dev))
+        return self._gather_padded(send, dev)
 
 
 class ThreadHub:
@@ -104,20 +114,33 @@ class ThreadTransport:
     def __init__(self, hub, rank):
         self.hub, self.rank, self.size = hub, rank, hub.parts
 
-    def exchange(self, stats, delta, count):
+    def _gather(self, item):
         h = self.hub
-        part = delta[:count].clone() if count else None
-        if part is not None and part.is_cuda:
-            torch.cuda.current_stream(part.device).synchronize()
-        h.box[self.rank] = (list(stats) + [int(count)], part)
+        h.box[self.rank] = item
         h.barrier.wait()
-        all_s = np.array([b[0] for b in h.box], dtype=np.int64)
-        parts = [b[1] for b in h.box if b[1] is not None]
-        recv = torch.cat(parts) if parts else None
-        if recv is not None and recv.is_cuda:
-            torch.cuda.current_stream(recv.device).synchronize()
-        h.barrier.wait()  # every rank has copied the box before it is refilled
-        return all_s, recv, 0 if recv is None else int(recv.numel())
+        got = list(h.box)
+        h.barrier.wait()  # every rank has read the box before it is refilled
+        return got
+
+    @staticmethod
+    def _settle(t):
+        if t is not None and t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+        return t
+
+    def gather_stats(self, stats, device):
+        return np.array(self._gather([int(x) for x in stats]), dtype=np.int64)
+
+    def gather_deltas(self, delta, count, maxc):
+        part = torch.full((maxc,), -1, dtype=torch.int64, device=delta.device)
+        if count:
+            part[:count].copy_(delta[:count])
+        self._settle(part)
+        return self._settle(torch.cat(self._gather(part)))
+
+    def gather_slices(self, buf):
+        part = self._settle(buf.clone())
+        return self._settle(torch.cat(self._gather(part)))
 
 
 # ------------------------------------------------------------------------------------------
@@ -141,6 +164,7 @@ class HipShard:
         self._h = h
         self.cap = max(self.hi - self.lo, 1)
         self.delta = torch.empty(self.cap, dtype=torch.int64, device=self.device)
+        self._slice = None
         self._st = (ctypes.c_int64 * 4)()
         self._a = ctypes.c_int64()
         self._b = ctypes.c_int64()
@@ -170,9 +194,23 @@ class HipShard:
         if count:
             nat.check("gc_shard_apply", self._lib.gc_shard_apply(self._h, kind, _p(recv), count, r))
 
-    def sweep(self, i):
-        nat.check("gc_shard_sweep", self._lib.gc_shard_sweep(self._h, i, _p(self.delta), self.cap, self._st))
+    def sweep(self, i, count=1):
+        nat.check("gc_shard_sweep", self._lib.gc_shard_sweep(self._h, i, count, _p(self.delta), self.cap, self._st))
         return self._st[0], self._st[1]
+
+    def slice_buffer(self, stride):
+        if self._slice is None or self._slice.numel() != stride:
+            self._slice = torch.zeros(stride, dtype=torch.uint8, device=self.device)
+        return self._slice
+
+    def get_slice(self, buf):
+        nat.check("gc_shard_get_slice", self._lib.gc_shard_get_slice(self._h, _p(buf)))
+
+    def put_slices(self, recv, stride, starts, lens):
+        ct = self._ct
+        a = (ct.c_int64 * len(starts))(*starts)
+        b = (ct.c_int64 * len(lens))(*lens)
+        nat.check("gc_shard_put_slices", self._lib.gc_shard_put_slices(self._h, _p(recv), stride, a, b, len(starts)))
 
     def accept(self, r):
         nat.check("gc_shard_accept", self._lib.gc_shard_accept(self._h, r, _p(self.delta), self.cap, self._st))
@@ -214,6 +252,7 @@ class ShardResult:
     reseeds: int = 0
     jp_sweeps: int = 0
     exchanges: int = 0
+    dense_exchanges: int = 0
 
     @property
     def rounds(self):
@@ -224,12 +263,25 @@ class ShardResult:
         return int(self.colors.max()) if len(self.colors) else -1
 
 
-def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False):
+K8_BIG = 62  # candidates >= 62 do not fit the 6-bit proposal byte (gc_internal.h)
+
+
+def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=4):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
-    same ShardResult (records with the single-GPU semantics of gc_color)."""
+    same ShardResult (records with the single-GPU semantics of gc_color).
+
+    Each seam is a stats all-gather then a data all-gather: the deltas, or -- when the
+    padded deltas would outweigh them (``dense=None``; True/False force it) -- every
+    rank's slice of the proposal bytes, copied back in place without a scatter.  Up to
+    ``local_sweeps`` JP sweeps run between two exchanges of the sweep seam."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
+    dev = ops.delta.device
+    rng = comm.gather_stats([ops.lo, ops.hi], dev)
+    starts = [int(x) for x in rng[:, 0]]
+    lens = [int(x) for x in rng[:, 1] - rng[:, 0]]
+    stride = max(max(lens), 1)
 
     def rec(u, f, mm, acc, seeds):
         res.round_U.append(int(u))
@@ -238,9 +290,21 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False):
         res.round_accepted.append(int(acc))
         res.round_seeds.append(int(seeds))
 
-    def xchg(stats, count):
+    def seam(S, kind, r, may_slice=True):
+        """data half of a seam (S = every rank's stats, counts last) -> apply."""
         res.exchanges += 1
-        return comm.exchange(stats, ops.delta, count)
+        maxc = int(S[:, -1].max())
+        if maxc == 0:
+            return
+        use = may_slice and (dense if dense is not None else 8 * maxc > stride)
+        if use:
+            buf = ops.slice_buffer(stride)
+            ops.get_slice(buf)
+            ops.put_slices(comm.gather_slices(buf), stride, starts, lens)
+            res.dense_exchanges += 1
+        else:
+            recv = comm.gather_deltas(ops.delta, int(S[comm.rank, -1]), maxc)
+            ops.apply(kind, recv, int(recv.numel()), r)
 
     max_rounds = 4 * ops.n + 16
     r = 0
@@ -251,7 +315,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False):
         if r > max_rounds:
             raise RuntimeError("round limit exceeded")
         cnt, f_loc, mm, fails = ops.propose(r)
-        S, recv, tot = xchg([f_loc, mm, fails], cnt)
+        S = comm.gather_stats([f_loc, mm, fails, cnt], dev)
         F, maxmex, fails = int(S[:, 0].sum()), int(S[:, 1].max()), int(S[:, 2].sum())
         if F == 0:  # no proposer anywhere: the reference spins (coloring.py:93-95) -> E1
             if not e1:
@@ -268,21 +332,22 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False):
             rec(U, F, maxmex, 0, 0)
             res.status, res.fail_round, res.fail_count = FAILED, r, fails
             break
-        ops.apply(KIND_CAND, recv, tot, r)
-        cnt, und = ops.sweep(0)
-        S, recv, tot = xchg([und], cnt)
-        ops.apply(KIND_STATE, recv, tot, r)
-        und, i = int(S[:, 0].sum()), 1
-        while und > 0:
-            cnt, und = ops.sweep(i)
-            S, recv, tot = xchg([und], cnt)
-            ops.apply(KIND_STATE, recv, tot, r)
-            und, i = int(S[:, 0].sum()), i + 1
+        seam(S, KIND_CAND, r, may_slice=maxmex < K8_BIG)
+        i = 0
+        while True:
+            cnt, und = ops.sweep(i, local_sweeps if i else 1)
+            i += local_sweeps if i else 1
+            S = comm.gather_stats([und, cnt], dev)
+            seam(S, KIND_STATE, r)
+            if int(S[:, 0].sum()) == 0:
+                break
             res.jp_sweeps += 1
         cnt = ops.accept(r)
-        S, recv, tot = xchg([], cnt)
+        S = comm.gather_stats([cnt], dev)
         acc = int(S[:, -1].sum())
-        ops.push(r, recv, tot)
+        res.exchanges += 1
+        recv = comm.gather_deltas(ops.delta, cnt, int(S[:, -1].max())) if acc else None
+        ops.push(r, recv, 0 if recv is None else int(recv.numel()))
         rec(U, F, maxmex, acc, 0)
         U -= acc
         r += 1
@@ -290,7 +355,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False):
     return res
 
 
-def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False):
+def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False, **kw):
     """``parts`` shards of one colouring on the current GPU, driven by threads: the test
     and rehearsal path of the multi-GPU engine on one device."""
     rp, _ = dg.export()
@@ -303,7 +368,7 @@ def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False):
 
     def run(i):
         try:
-            out[i] = shard_color(shards[i], ThreadTransport(hub, i), num_colors, e1, track_rounds)
+            out[i] = shard_color(shards[i], ThreadTransport(hub, i), num_colors, e1, track_rounds, **kw)
         except BaseException as e:  # noqa: BLE001 - surface the first failure
             err.append(e)
             hub.barrier.abort()

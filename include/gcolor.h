@@ -146,9 +146,14 @@ int gc_shard_begin(gc_shard* s, int64_t num_colors, int32_t track_rounds, int64_
 /* stats[4]: deltas written, frontier size, max candidate (-1 none), #candidates >= k    */
 int gc_shard_propose(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
 int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);
-/* i = 0: first sweep over the frontier, i >= 1: sweep over the undecided;
+/* sweeps i .. i+count-1 (i = 0: first sweep over the frontier, then over the undecided);
    stats[2]: deltas written, vertices still undecided on this rank                     */
-int gc_shard_sweep(gc_shard* s, int32_t i, int64_t* delta, int64_t cap, int64_t* stats);
+int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats);
+/* dense seam: the rank's slice [lo, hi) of the proposal bytes (cand6 << 2 | JP state)
+   into dst (device, hi - lo bytes); put_slices copies the other ranks' slices back    */
+int gc_shard_get_slice(gc_shard* s, uint8_t* dst);
+int gc_shard_put_slices(gc_shard* s, const uint8_t* src, int64_t stride, const int64_t* starts,
+                        const int64_t* lens, int32_t parts);
 /* stats[1]: winners coloured (= deltas written)                                        */
 int gc_shard_accept(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
 /* all ranks' winners: colour the remote ones, push into own in-neighbours, next round */

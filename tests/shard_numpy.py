@@ -105,24 +105,45 @@ class NumpyShard:
         if self.track:
             self.cround[v] = r + 1
 
-    def sweep(self, i):
-        todo = self.F if i == 0 else self.und
-        pairs, und = [], []
-        for v in todo:
-            f = 0
-            for u in self.lower[v]:
-                if self.cand[u] == self.cand[v] and self.cand[u] >= 0:
-                    f |= 1 if self.state[u] == IN else (2 if self.state[u] == UND else 0)
-            if f & 1:
-                self.state[v] = OUT
-                pairs.append((v, OUT))
-            elif f & 2:
-                und.append(v)
-            else:
-                self.state[v] = IN
-                pairs.append((v, IN))
-        self.und = und
-        return self._emit(pairs), len(und)
+    def sweep(self, i, count=1):
+        pairs = []
+        for j in range(i, i + count):
+            todo = self.F if j == 0 else self.und
+            und = []
+            for v in todo:
+                f = 0
+                for u in self.lower[v]:
+                    if self.cand[u] == self.cand[v] and self.cand[u] >= 0:
+                        f |= 1 if self.state[u] == IN else (2 if self.state[u] == UND else 0)
+                if f & 1:
+                    self.state[v] = OUT
+                    pairs.append((v, OUT))
+                elif f & 2:
+                    und.append(v)
+                else:
+                    self.state[v] = IN
+                    pairs.append((v, IN))
+            self.und = und
+        return self._emit(pairs), len(self.und)
+
+    # dense seam: proposal bytes cand6 << 2 | state (63 = no candidate), the rank's slice
+    def slice_buffer(self, stride):
+        return torch.zeros(stride, dtype=torch.uint8)
+
+    def get_slice(self, buf):
+        c = self.cand[self.lo:self.hi]
+        c6 = np.where(c < 0, 63, c)
+        assert (c6 <= 63).all() and not ((c6 >= 62) & (c >= 0)).any()
+        buf[:self.hi - self.lo] = torch.from_numpy(((c6 << 2) | self.state[self.lo:self.hi]).astype(np.uint8))
+
+    def put_slices(self, recv, stride, starts, lens):
+        for p, (s0, ln) in enumerate(zip(starts, lens)):
+            if s0 == self.lo or ln <= 0:
+                continue
+            b = recv[p * stride:p * stride + ln].numpy().astype(np.int64)
+            c6 = b >> 2
+            self.cand[s0:s0 + ln] = np.where(c6 == 63, -1, c6)
+            self.state[s0:s0 + ln] = b & 3
 
     def accept(self, r):
         pairs = []

@@ -31,10 +31,10 @@ def _random_directed(n, m, seed):
     return np.cumsum(rp), dst.astype(np.int32)
 
 
-def same_as_single(dg, parts, k=None, e1=True):
+def same_as_single(dg, parts, k=None, e1=True, **kw):
     from gcolor_amd import shard as sh
     one = dg.color("A", num_colors=k, e1=e1)
-    res = sh.color_threads(dg, parts, num_colors=k, e1=e1, track_rounds=True)
+    res = sh.color_threads(dg, parts, num_colors=k, e1=e1, track_rounds=True, **kw)
     for r in res:
         assert r.status == one.status
         assert np.array_equal(r.colors, one.colors)
@@ -70,6 +70,10 @@ def test_directed_multigraph_sharded_bounded_and_stalled(seed):
         r, one = same_as_single(dg, 2)
         same_as_single(dg, 4, k=max(one.max_color, 1))
         same_as_single(dg, 3, e1=False)
+        r, _ = same_as_single(dg, 3, dense=True, local_sweeps=1)
+        assert r.dense_exchanges > 0
+        r, _ = same_as_single(dg, 2, dense=False, local_sweeps=6)
+        assert r.dense_exchanges == 0
 
 
 def test_rmat_hubs_and_wide_mex_sharded():
@@ -77,6 +81,7 @@ def test_rmat_hubs_and_wide_mex_sharded():
     with DeviceGraph.rmat(12, 16, seed=5) as dg:
         r, one = same_as_single(dg, 4)
         assert dg.max_degree > 256 and one.max_color >= 32
+        same_as_single(dg, 3, dense=True)  # candidates >= 62 keep their seam sparse
         assert dg.validate(r.colors) == (0, 0)
 
 
@@ -115,6 +120,15 @@ def _gloo_gpu_worker(rank, world, port, out_dir):
         ops.close()
         out = {"colors": res.colors.tolist(), "U": res.round_U, "acc": res.round_accepted,
                "seeds": res.round_seeds}
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(50_000, 16, 4)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        lo, hi = sh.balanced_ranges(rp, world)[rank]
+        ops = sh.HipShard(dg, lo, hi)
+        res = sh.shard_color(ops, sh.TorchTransport(), None, True)  # dense seams in big rounds
+        ops.close()
+        out["uniform"] = res.colors.tolist()
+        out["dense"] = res.dense_exchanges
     with open(os.path.join(out_dir, f"g{rank}.json"), "w") as f:
         json.dump(out, f)
     dist.destroy_process_group()
@@ -131,3 +145,10 @@ def test_two_processes_over_torch_distributed(tmp_path):
         assert got["colors"] == list(one.colors)
         assert got["U"] == list(one.round_U) and got["acc"] == list(one.round_accepted)
         assert got["seeds"] == list(one.round_seeds)
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(50_000, 16, 4)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        one = dg.color("A")
+    for r in range(2):
+        got = json.load(open(tmp_path / f"g{r}.json"))
+        assert got["uniform"] == list(one.colors) and got["dense"] > 0
