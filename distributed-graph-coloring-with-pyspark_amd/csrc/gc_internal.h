@@ -57,7 +57,7 @@ typedef unsigned long long ull;
 #define GC_CM_ROUND 0
 #define GC_CM_INIT 1
 #define GC_CM_RESEED 2
-#define GC_CM_ACCEPT 3  // sharded round: colour the winners, publish them, no push
+#define GC_CM_SHARD 3   // sharded round: the rank's frontier, no halt / sweep checks
 
 // kinds of exchanged deltas (sharded engine)
 #define GC_KIND_CAND 0

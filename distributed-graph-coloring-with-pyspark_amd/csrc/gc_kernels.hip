@@ -685,8 +685,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     const int cur = c->cur;
     const int round = mode == GC_CM_INIT ? 0 : (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    const bool rnd = mode == GC_CM_ROUND || mode == GC_CM_ACCEPT;
-    const bool push = mode != GC_CM_ACCEPT;  // ACCEPT (sharded): the push runs after the exchange
+    const bool rnd = mode == GC_CM_ROUND || mode == GC_CM_SHARD;
     const int* __restrict__ list = rnd ? L.F[cur] : L.seeds[0];
     const long long cnt = (long long)(rnd ? c->fcnt[cur] : c->seed_cnt[0]);
     const int* hlist = rnd ? L.heavy : L.seeds[1];
@@ -709,8 +708,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
                 gc_commit_colour(g, v, cc);
                 if (want_cround) g.cround[v] = round;
-                if (!push) L.delta[atomicAdd(&c->dcnt, 1ull)] = gc_delta(v, cc);
-                s_acc = push;
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
@@ -757,9 +754,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             tstart = g.trp[v];
             din = (int)(g.trp[v + 1] - tstart);
             lsum += (ull)din;
-            if (!push) din = 0;
         }
-        if (!push) gc_wave_append64(acc, gc_delta(v, cc), L.delta, &c->dcnt);
         // losers stay in the frontier (they still have a coloured neighbour)
         gc_stage_push(st, js == GC_JP_OUT, v, next, next_cnt);
         s_start[w][lane] = tstart;
@@ -839,50 +834,81 @@ __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long
     }
 }
 
-// commit seam: every vertex coloured this round on ANY rank pushes into this rank's
-// in-neighbours (trp/tcol is the rank-local in-neighbour CSR: owned targets only).
-__global__ void __launch_bounds__(GC_BLOCK) k_push_list(GDev g, GLists L, const long long* recv, long long count) {
+// End of a sharded round, after the last sweep seam: every rank holds every proposer's
+// final JP state, so the winners of the OTHER ranks are read off the replicated proposal
+// bytes (state IN, a candidate) instead of being exchanged: each is coloured here too
+// and pushes into this rank's in-neighbours (trp/tcol is the rank-local in-neighbour CSR:
+// owned targets only).  The rank's own winners went through k_commit (GC_CM_SHARD).
+// One 4-byte word of k8 per lane, 256 vertices per wave step.
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L, long long lo, long long hi) {
     DevCtl* c = g.ctl;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int nxt = c->cur ^ 1;
     int* next = L.F[nxt];
     ull* next_cnt = &c->fcnt[nxt];
+    const int round = (int)(c->round + 1);
+    const bool want_cround = c->want_cround != 0;
     GcStage st{s_stage[w], 0};
-    const int vpw = gc_vpw(count, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
-    const long long nch = gc_nchunks(count, vpw);
-    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
-         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long idx = ch * vpw + lane;
-        const int v = (lane < vpw && idx < count) ? (int)(recv[idx] >> 32) : -1;
-        long long tstart = 0;
-        int din = 0;
-        if (v >= 0) {
-            tstart = g.trp[v];
-            din = (int)(g.trp[v + 1] - tstart);
+    long long lmaxc = -1;
+    ull lacc = 0;
+    const long long n = g.n;
+    const long long steps = (n + 4 * GC_WAVE - 1) / (4 * GC_WAVE);
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v0 = sidx * 4 * GC_WAVE + 4 * lane;
+        // skip steps inside the owned range (their winners were committed by k_commit)
+        if (sidx * 4 * GC_WAVE >= lo && (sidx + 1) * 4 * GC_WAVE <= hi) continue;
+        unsigned word = 0xFCFCFCFCu;  // (NONE, UND) x 4
+        if (v0 + 3 < n) {
+            word = *reinterpret_cast<const unsigned*>(g.k8 + v0);
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (v0 + k < n) word = (word & ~(0xFFu << (8 * k))) | ((unsigned)g.k8[v0 + k] << (8 * k));
         }
-        s_start[w][lane] = tstart;
-        const int incl = gc_wave_incl_scan(din);
-        const int excl = incl - din;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            bool claim = false;
-            int x = 0;
-            if (e < total) {
-                x = g.tcol[s_start[w][o] + (e - eo)];
-                claim = gc_claim(g.inF, x);
+        for (int k = 0; k < 4; ++k) {
+            const long long v = v0 + k;
+            const unsigned b = (word >> (8 * k)) & 0xFFu;
+            const bool win = v < n && (v < lo || v >= hi) && gc_k8_state(b) == GC_JP_IN && gc_k8_cand(b) != GC_K8_NONE;
+            if (!__ballot(win)) continue;
+            long long tstart = 0;
+            int din = 0;
+            if (win) {
+                const int cc = gc_k8_cand(b) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(b);
+                gc_commit_colour(g, (int)v, cc);
+                if (want_cround) g.cround[v] = round;
+                lmaxc = cc > lmaxc ? cc : lmaxc;
+                lacc++;
+                tstart = g.trp[v];
+                din = (int)(g.trp[v + 1] - tstart);
             }
-            gc_stage_push(st, claim, x, next, next_cnt);
+            s_start[w][lane] = tstart;
+            const int incl = gc_wave_incl_scan(din);
+            const int excl = incl - din;
+            const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+            gc_wave_sync();
+            for (int base = 0; base < total; base += GC_WAVE) {
+                const int e = base + lane;
+                const int o = gc_owner(excl, e);
+                const int eo = __shfl(excl, o, GC_WAVE);
+                bool claim = false;
+                int x = 0;
+                if (e < total) {
+                    x = g.tcol[s_start[w][o] + (e - eo)];
+                    claim = gc_claim(g.inF, x);
+                }
+                gc_stage_push(st, claim, x, next, next_cnt);
+            }
+            gc_wave_sync();
         }
-        gc_wave_sync();
     }
     gc_stage_flush(st, next, next_cnt);
+    __syncthreads();
+    gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
+    gc_block_add(&c->accepted, lacc, scratch);
 }
 
 // per-round counter reset of a shard (one thread)
@@ -1216,9 +1242,8 @@ void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, 
     if (count <= 0) return;
     hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round);
 }
-void gcl_push_list(const GDev& g, const GLists& L, const long long* recv, long long count, hipStream_t s) {
-    if (count <= 0) return;
-    hipLaunchKernelGGL(k_push_list, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, recv, count);
+void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_scan_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi);
 }
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);

@@ -49,7 +49,7 @@ void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s);
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                hipStream_t s);
-void gcl_push_list(const GDev& g, const GLists& L, const long long* recv, long long count, hipStream_t s);
+void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, hipStream_t s);
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
 void gcl_shard_flip(const GDev& g, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);

@@ -4,17 +4,18 @@
 // 288 GB) and owns a contiguous vertex range [lo, hi).  A shard is a view of that graph
 // with its own run state and a rank-local in-neighbour CSR (the owned rows' targets), so
 // the single-GPU round kernels run unchanged on the rank's own frontier.  A round is cut
-// at its three grid-wide seams (coloring.py:73-132):
+// at its grid-wide seams (coloring.py:73-132):
 //   propose  -> publish (v, candidate) of the rank's proposers      (coloring.py:44-54)
-//   resolve, each JP sweep -> publish (v, IN|OUT) of decided ones   (coloring.py:56-70)
-//   accept   -> publish (v, colour) of the rank's winners           (coloring.py:114-127)
-// The caller (gcolor_amd/shard.py) all-gathers the deltas over RCCL and hands every rank
-// the full set back: gc_shard_apply / gc_shard_push.  Because the conflict resolution is
-// the lexicographically-first MIS under the global rank (deg, pos), the result does not
-// depend on the partition: it is bit-identical to gc_color on one GPU.
+//   resolve, JP sweeps -> publish (v, IN|OUT) of decided ones       (coloring.py:56-70)
+// The caller (gcolor_amd/shard.py) all-gathers them over RCCL -- as int64 deltas
+// (vertex << 32 | value) into gc_shard_apply, or as every rank's slice of the proposal
+// bytes (gc_shard_get_slice / put_slices) when most vertices changed -- so after the last
+// sweep seam every rank holds every proposer's final state and gc_shard_finish colours
+// all winners (coloring.py:114-127) with no further exchange.  Because the conflict
+// resolution is the lexicographically-first MIS under the global rank (deg, pos), the
+// result does not depend on the partition: it is bit-identical to gc_color on one GPU.
 //
-// Every call is synchronous (the caller needs the counts for the exchange) and works on
-// caller-owned device buffers of int64 deltas (vertex << 32 | value).
+// Every call is synchronous (the caller needs the counts for the exchange).
 #include <string.h>
 
 #include <algorithm>
@@ -125,6 +126,7 @@ extern "C" int gc_shard_propose(gc_shard* sh, int64_t round, int64_t* delta, int
     const GDev d = gc_view(g);
     const GLists L = shard_lists(sh, delta);
     gcl_shard_reset(d, round, g->stream);
+    gcl_fsort(d, L, g->fsum, g->stream);  // big rounds: the rank's frontier in vertex order
     gcl_pack_c4(d, g->stream);
     gcl_propose(d, L, g->stream);
     gcl_propose_block(d, L, g->stream);
@@ -156,12 +158,12 @@ extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, i
 // JP sweeps i, i+1, ..., i+count-1 over the rank's lists (i = 0 is the first sweep over
 // the frontier; later sweeps run over the undecided); the rank's later sweeps can decide
 // vertices whose lower-rank neighbours are its own, so several run between two
-// exchanges.  delta = (v, IN|OUT) of every vertex decided.
-// stats: [0] deltas, [1] still undecided on this rank
+// exchanges.  delta = (v, IN|OUT) of every vertex decided, or null when the seam will
+// move slices instead.  stats: [0] deltas, [1] still undecided on this rank
 extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats) {
-    if (!sh || !delta || !stats || i < 0 || count < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
+    if (!sh || !stats || i < 0 || count < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
-    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    if (delta && cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
     const GDev d = gc_view(g);
     const GLists L = shard_lists(sh, delta);
@@ -199,7 +201,7 @@ extern "C" int gc_shard_put_slices(gc_shard* sh, const uint8_t* src, int64_t str
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
     for (int p = 0; p < parts; ++p) {
-        if (starts[p] == sh->lo || lens[p] <= 0) continue;
+        if (lens[p] <= 0 || (starts[p] == sh->lo && lens[p] == sh->hi - sh->lo)) continue;  // own slice
         if (starts[p] < 0 || starts[p] + lens[p] > g->n || lens[p] > stride) { gc_set_error("bad slice %d", p); return GC_EINVAL; }
         GC_HIP(hipMemcpyAsync(g->k8 + starts[p], src + (size_t)p * (size_t)stride, (size_t)lens[p],
                               hipMemcpyDeviceToDevice, g->stream));
@@ -208,38 +210,24 @@ extern "C" int gc_shard_put_slices(gc_shard* sh, const uint8_t* src, int64_t str
     return GC_OK;
 }
 
-// colour the rank's winners; delta = (v, colour).  stats: [0] deltas (= accepted)
-extern "C" int gc_shard_accept(gc_shard* sh, int64_t round, int64_t* delta, int64_t cap, int64_t* stats) {
-    if (!sh || !delta || !stats) { gc_set_error("null argument"); return GC_EINVAL; }
-    gc_graph* g = &sh->v;
-    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
-    GC_HIP(hipSetDevice(g->device));
-    const GLists L = shard_lists(sh, delta);
-    GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
-    gcl_commit(gc_view(g), L, GC_CM_ACCEPT, 0, g->stream);
-    int rc = shard_sync(sh);
-    if (rc) return rc;
-    stats[0] = (int64_t)g->hctl->dcnt;
-    (void)round;
-    return GC_OK;
-}
-
-// every rank's winners: colour the ones owned elsewhere, push all of them into this
-// rank's in-neighbours (next frontier), make that frontier current.
-extern "C" int gc_shard_push(gc_shard* sh, int64_t round, const int64_t* recv, int64_t count, int64_t* F_out) {
+// End of the round (coloring.py:114-127): colour every winner -- the rank's own through
+// its frontier (losers stay in it), the other ranks' read off the replicated proposal
+// bytes -- push them into this rank's in-neighbours and make that frontier current.
+// acc_out: winners of ALL ranks (the same on every rank); F_out: the rank's new frontier.
+extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int64_t* acc_out, int64_t* F_out) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
-    if (count > 0 && !recv) { gc_set_error("null delta buffer"); return GC_EINVAL; }
     const GDev d = gc_view(g);
     const GLists L = shard_lists(sh, nullptr);
-    const long long* r = reinterpret_cast<const long long*>(recv);
-    gcl_apply(d, GC_KIND_COLOUR, r, count, sh->lo, sh->hi, (int)round + 1, g->stream);
-    gcl_push_list(d, L, r, count, g->stream);
+    gcl_commit(d, L, GC_CM_SHARD, 0, g->stream);
+    gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->stream);
     gcl_shard_flip(d, g->stream);
     int rc = shard_sync(sh);
     if (rc) return rc;
+    if (acc_out) *acc_out = (int64_t)g->hctl->accepted;
     if (F_out) *F_out = (int64_t)g->hctl->fcnt[g->hctl->cur];
+    (void)round;
     return GC_OK;
 }
 

@@ -1,24 +1,28 @@
 """Multi-GPU colouring: vertex-range shards, one rank per GPU.
 
 Every rank holds the whole CSR (a ``DeviceGraph``) and owns a contiguous, nnz-balanced
-range of vertices.  A round is the single-GPU round (coloring.py:73-132) cut at its three
-grid-wide seams.  At each seam every rank publishes what changed on its own vertices,
-as int64 deltas ``vertex << 32 | value``, and applies everyone else's:
+range of vertices.  A round is the single-GPU round (coloring.py:73-132) cut at its
+grid-wide seams.  At each seam every rank publishes what changed on its own vertices and
+takes everyone else's:
 
     propose               (v, candidate)   all-gather -> apply     coloring.py:44-54
     first sweep, sweeps   (v, IN | OUT)    all-gather -> apply     coloring.py:56-70
-    accept                (v, colour)      all-gather -> push      coloring.py:114-127
 
-The round scalars (frontier size, max proposal, failures, undecided, accepted) travel in a
-small all-gather next to each delta all-gather.  Conflict resolution is the
-lexicographically-first MIS under the global rank (deg, pos), so the colouring does not
-depend on the partition: it is bit-identical to one GPU.  E1 re-seeding runs on every
-rank over the replicated state, so every rank plants the same seeds.
+as int64 deltas ``vertex << 32 | value`` -- or, when the padded deltas would outweigh
+it, as every rank's slice of the proposal bytes (cand6 << 2 | state), copied back in
+place.  After the last sweep seam every rank holds every proposer's final state, so each
+colours ALL the round's winners itself (coloring.py:114-127) and pushes them into its own
+in-neighbours: no exchange at commit.  The round scalars (frontier size, max proposal,
+failures, undecided) travel in a small all-gather before each data all-gather.
+Conflict resolution is the lexicographically-first MIS under the global rank (deg, pos),
+so the colouring does not depend on the partition: it is bit-identical to one GPU.  E1
+re-seeding runs on every rank over the replicated state, so every rank plants the same
+seeds.
 
 ``shard_color(ops, comm)`` is the SPMD driver.
 * ``ops`` is one rank's phase implementation: ``HipShard`` here (libgcolor.so); the
   CPU stand-in used by the ``gloo`` tests lives in ``tests/``.
-* ``comm`` moves the deltas: ``TorchTransport`` (torch.distributed; RCCL over xGMI with
+* ``comm`` moves the data: ``TorchTransport`` (torch.distributed; RCCL over xGMI with
   ``nccl``, or ``gloo``), or ``ThreadTransport`` for several shards in one process.
 """
 import threading
@@ -194,13 +198,15 @@ class HipShard:
         if count:
             nat.check("gc_shard_apply", self._lib.gc_shard_apply(self._h, kind, _p(recv), count, r))
 
-    def sweep(self, i, count=1):
-        nat.check("gc_shard_sweep", self._lib.gc_shard_sweep(self._h, i, count, _p(self.delta), self.cap, self._st))
+    def sweep(self, i, count=1, emit=True):
+        nat.check("gc_shard_sweep", self._lib.gc_shard_sweep(self._h, i, count, _p(self.delta) if emit else None,
+                                                             self.cap, self._st))
         return self._st[0], self._st[1]
 
     def slice_buffer(self, stride):
+        # empty, not zeros: a fill on torch's stream would race the shard stream's copy
         if self._slice is None or self._slice.numel() != stride:
-            self._slice = torch.zeros(stride, dtype=torch.uint8, device=self.device)
+            self._slice = torch.empty(stride, dtype=torch.uint8, device=self.device)
         return self._slice
 
     def get_slice(self, buf):
@@ -212,24 +218,22 @@ class HipShard:
         b = (ct.c_int64 * len(lens))(*lens)
         nat.check("gc_shard_put_slices", self._lib.gc_shard_put_slices(self._h, _p(recv), stride, a, b, len(starts)))
 
-    def accept(self, r):
-        nat.check("gc_shard_accept", self._lib.gc_shard_accept(self._h, r, _p(self.delta), self.cap, self._st))
-        return self._st[0]
-
-    def push(self, r, recv, count):
-        nat.check("gc_shard_push", self._lib.gc_shard_push(self._h, r, _p(recv), count, self._ct.byref(self._a)))
-        return self._a.value
+    def finish(self, r):
+        ct = self._ct
+        nat.check("gc_shard_finish", self._lib.gc_shard_finish(self._h, r, ct.byref(self._a), ct.byref(self._b)))
+        return self._a.value, self._b.value
 
     def reseed(self, r):
         ct = self._ct
         nat.check("gc_shard_reseed", self._lib.gc_shard_reseed(self._h, r, ct.byref(self._a), ct.byref(self._b)))
         return self._a.value, self._b.value
 
-    def colors(self, track_rounds):
-        colors = np.empty(self.n, np.int32)
-        cround = np.empty(self.n, np.int32) if track_rounds else None
+    def colors(self, track_rounds, fetch=True):
+        """Final colours (and rounds) to host; fetch=False only settles them in HBM."""
+        colors = np.empty(self.n, np.int32) if fetch else None
+        cround = np.empty(self.n, np.int32) if track_rounds and fetch else None
         nat.check("gc_shard_colors", self._lib.gc_shard_colors(
-            self._h, colors.ctypes.data_as(self._ct.c_void_p),
+            self._h, None if colors is None else colors.ctypes.data_as(self._ct.c_void_p),
             None if cround is None else cround.ctypes.data_as(self._ct.c_void_p)))
         return colors, cround
 
@@ -266,14 +270,17 @@ class ShardResult:
 K8_BIG = 62  # candidates >= 62 do not fit the 6-bit proposal byte (gc_internal.h)
 
 
-def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=4):
+def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
+                want_colors=True):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
     Each seam is a stats all-gather then a data all-gather: the deltas, or -- when the
     padded deltas would outweigh them (``dense=None``; True/False force it) -- every
-    rank's slice of the proposal bytes, copied back in place without a scatter.  Up to
-    ``local_sweeps`` JP sweeps run between two exchanges of the sweep seam."""
+    rank's slice of the proposal bytes, copied back in place without a scatter.
+    ``local_sweeps`` JP sweeps run between two exchanges of the sweep seam (more than one
+    pays where neighbours are mostly rank-local, e.g. meshes cut into slabs).
+    ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them later)."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -290,21 +297,22 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
         res.round_accepted.append(int(acc))
         res.round_seeds.append(int(seeds))
 
-    def seam(S, kind, r, may_slice=True):
-        """data half of a seam (S = every rank's stats, counts last) -> apply."""
+    def slices():
+        res.exchanges += 1
+        res.dense_exchanges += 1
+        buf = ops.slice_buffer(stride)
+        ops.get_slice(buf)
+        ops.put_slices(comm.gather_slices(buf), stride, starts, lens)
+
+    def deltas(S, kind, r):
         res.exchanges += 1
         maxc = int(S[:, -1].max())
-        if maxc == 0:
-            return
-        use = may_slice and (dense if dense is not None else 8 * maxc > stride)
-        if use:
-            buf = ops.slice_buffer(stride)
-            ops.get_slice(buf)
-            ops.put_slices(comm.gather_slices(buf), stride, starts, lens)
-            res.dense_exchanges += 1
-        else:
+        if maxc:
             recv = comm.gather_deltas(ops.delta, int(S[comm.rank, -1]), maxc)
             ops.apply(kind, recv, int(recv.numel()), r)
+
+    def slice_for(maxc):  # a slice seam moves stride bytes per rank, deltas 8 * maxc
+        return dense if dense is not None else 8 * maxc > stride
 
     max_rounds = 4 * ops.n + 16
     r = 0
@@ -332,26 +340,32 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             rec(U, F, maxmex, 0, 0)
             res.status, res.fail_round, res.fail_count = FAILED, r, fails
             break
-        seam(S, KIND_CAND, r, may_slice=maxmex < K8_BIG)
-        i = 0
+        # candidates >= 62 live in cand[], outside the proposal bytes: deltas only
+        if maxmex < K8_BIG and slice_for(int(S[:, -1].max())):
+            slices()
+        else:
+            deltas(S, KIND_CAND, r)
+        # JP sweeps; a rank decides at most what it has left, so the seam's form is known
+        # before the sweep runs (and a slice seam writes no deltas)
+        i, left = 0, int(S[:, 0].max())
         while True:
-            cnt, und = ops.sweep(i, local_sweeps if i else 1)
+            sl = slice_for(left)
+            cnt, und = ops.sweep(i, local_sweeps if i else 1, emit=not sl)
             i += local_sweeps if i else 1
             S = comm.gather_stats([und, cnt], dev)
-            seam(S, KIND_STATE, r)
+            if sl:
+                slices()
+            else:
+                deltas(S, KIND_STATE, r)
             if int(S[:, 0].sum()) == 0:
                 break
+            left = int(S[:, 0].max())
             res.jp_sweeps += 1
-        cnt = ops.accept(r)
-        S = comm.gather_stats([cnt], dev)
-        acc = int(S[:, -1].sum())
-        res.exchanges += 1
-        recv = comm.gather_deltas(ops.delta, cnt, int(S[:, -1].max())) if acc else None
-        ops.push(r, recv, 0 if recv is None else int(recv.numel()))
+        acc, _ = ops.finish(r)
         rec(U, F, maxmex, acc, 0)
         U -= acc
         r += 1
-    res.colors, res.colored_round = ops.colors(track_rounds)
+    res.colors, res.colored_round = ops.colors(track_rounds, want_colors)
     return res
 
 

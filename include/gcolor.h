@@ -128,16 +128,18 @@ int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t*
 /* ---- multi-GPU shards ------------------------------------------------ */
 /* One rank's share of a colouring on the graph g (every rank holds the whole CSR): the
    rank owns vertices [lo, hi) and runs the round on its own frontier.  A round is cut at
-   its three grid-wide seams -- propose, each Jones-Plassmann sweep, accept -- where the
-   rank publishes int64 deltas (vertex << 32 | value) of its own vertices into a caller-
-   owned DEVICE buffer (capacity >= hi - lo) and applies everyone's (gc_shard_apply /
-   gc_shard_push).  The caller moves the deltas between ranks (RCCL all-gather in
-   gcolor_amd/shard.py).  The colouring is bit-identical to gc_color on one GPU.
+   its grid-wide seams -- propose and the Jones-Plassmann sweeps -- where the rank
+   publishes what changed on its own vertices: int64 deltas (vertex << 32 | value) in a
+   caller-owned DEVICE buffer (capacity >= hi - lo), or its slice of the proposal bytes,
+   and takes everyone's back (gc_shard_apply / gc_shard_put_slices).  After the last
+   sweep seam every rank colours all winners itself (gc_shard_finish).  The caller moves
+   the data between ranks (RCCL all-gather in gcolor_amd/shard.py).  The colouring is
+   bit-identical to gc_color on one GPU.
    Replaces: the Spark shuffle/broadcast of each round (coloring.py:82-83, 110-127).  */
 typedef struct gc_shard gc_shard;
 #define GC_KIND_CAND 0   /* (v, candidate): propose seam                                */
 #define GC_KIND_STATE 1  /* (v, 1 = IN | 2 = OUT): JP sweep seam                        */
-#define GC_KIND_COLOUR 2 /* (v, colour): accept seam (gc_shard_push applies these)      */
+#define GC_KIND_COLOUR 2 /* (v, colour): colours set elsewhere                          */
 int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** out);
 void gc_shard_destroy(gc_shard* s);
 /* init + seed (coloring.py:12-35) on the replicated state; *U_out global uncoloured,
@@ -147,17 +149,16 @@ int gc_shard_begin(gc_shard* s, int64_t num_colors, int32_t track_rounds, int64_
 int gc_shard_propose(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
 int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);
 /* sweeps i .. i+count-1 (i = 0: first sweep over the frontier, then over the undecided);
-   stats[2]: deltas written, vertices still undecided on this rank                     */
+   delta may be NULL (slice seam).  stats[2]: deltas written, still undecided here      */
 int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats);
-/* dense seam: the rank's slice [lo, hi) of the proposal bytes (cand6 << 2 | JP state)
+/* slice seam: the rank's slice [lo, hi) of the proposal bytes (cand6 << 2 | JP state)
    into dst (device, hi - lo bytes); put_slices copies the other ranks' slices back    */
 int gc_shard_get_slice(gc_shard* s, uint8_t* dst);
 int gc_shard_put_slices(gc_shard* s, const uint8_t* src, int64_t stride, const int64_t* starts,
                         const int64_t* lens, int32_t parts);
-/* stats[1]: winners coloured (= deltas written)                                        */
-int gc_shard_accept(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
-/* all ranks' winners: colour the remote ones, push into own in-neighbours, next round */
-int gc_shard_push(gc_shard* s, int64_t round, const int64_t* recv, int64_t count, int64_t* F_out);
+/* end of round: colour ALL ranks' winners (read off the replicated proposal bytes), push
+   them into the rank's in-neighbours; *acc_out = winners (global), *F_out = new frontier */
+int gc_shard_finish(gc_shard* s, int64_t round, int64_t* acc_out, int64_t* F_out);
 /* E1 re-seed on the replicated state (same seeds on every rank)                        */
 int gc_shard_reseed(gc_shard* s, int64_t round, int64_t* nseeds, int64_t* F_out);
 int gc_shard_colors(gc_shard* s, int32_t* colors_out, int32_t* colored_round_out);

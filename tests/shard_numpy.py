@@ -105,7 +105,7 @@ class NumpyShard:
         if self.track:
             self.cround[v] = r + 1
 
-    def sweep(self, i, count=1):
+    def sweep(self, i, count=1, emit=True):
         pairs = []
         for j in range(i, i + count):
             todo = self.F if j == 0 else self.und
@@ -124,7 +124,7 @@ class NumpyShard:
                     self.state[v] = IN
                     pairs.append((v, IN))
             self.und = und
-        return self._emit(pairs), len(self.und)
+        return (self._emit(pairs) if emit else 0), len(self.und)
 
     # dense seam: proposal bytes cand6 << 2 | state (63 = no candidate), the rank's slice
     def slice_buffer(self, stride):
@@ -132,33 +132,25 @@ class NumpyShard:
 
     def get_slice(self, buf):
         c = self.cand[self.lo:self.hi]
-        c6 = np.where(c < 0, 63, c)
-        assert (c6 <= 63).all() and not ((c6 >= 62) & (c >= 0)).any()
+        c6 = np.where(c < 0, 63, np.minimum(c, 62))  # 62: the candidate is in cand (BIG)
         buf[:self.hi - self.lo] = torch.from_numpy(((c6 << 2) | self.state[self.lo:self.hi]).astype(np.uint8))
 
     def put_slices(self, recv, stride, starts, lens):
         for p, (s0, ln) in enumerate(zip(starts, lens)):
-            if s0 == self.lo or ln <= 0:
+            if ln <= 0 or (s0 == self.lo and ln == self.hi - self.lo):  # own slice
                 continue
             b = recv[p * stride:p * stride + ln].numpy().astype(np.int64)
             c6 = b >> 2
-            self.cand[s0:s0 + ln] = np.where(c6 == 63, -1, c6)
+            cur = self.cand[s0:s0 + ln]
+            self.cand[s0:s0 + ln] = np.where(c6 == 63, -1, np.where(c6 == 62, cur, c6))
             self.state[s0:s0 + ln] = b & 3
 
-    def accept(self, r):
-        pairs = []
-        for v in self.F:
-            if self.state[v] == IN:
-                pairs.append((v, int(self.cand[v])))
-        for v, cc in pairs:
-            self._colour(v, cc, r)
-        return self._emit(pairs)
-
-    def push(self, r, recv, tot):
-        for v, val in self._decode(recv, tot):
-            if not self._owned(v):
-                self._colour(v, val, r)
-        return len(self._frontier())
+    def finish(self, r):
+        # every proposer's final state is replicated: all ranks colour all winners
+        win = [v for v in range(self.n) if self.state[v] == IN and self.cand[v] >= 0]
+        for v in win:
+            self._colour(v, int(self.cand[v]), r)
+        return len(win), len(self._frontier())
 
     def reseed(self, r):
         seeds = _components_argmax(self.adj, self.deg.tolist(), self.c.tolist())
@@ -167,5 +159,7 @@ class NumpyShard:
             self.cround[s] = r + 1
         return len(seeds), len(self._frontier())
 
-    def colors(self, track):
+    def colors(self, track, fetch=True):
+        if not fetch:
+            return None, None
         return self.c.astype(np.int32), (self.cround.astype(np.int32) if track else None)

@@ -82,7 +82,7 @@ def timed(obj, name):
 
 
 ops = sh.HipShard(dg, 0, dg.n)
-for name in ("begin", "propose", "apply", "sweep", "accept", "push", "reseed", "colors", "get_slice", "put_slices"):
+for name in ("begin", "propose", "apply", "sweep", "finish", "reseed", "colors", "get_slice", "put_slices"):
     timed(ops, name)
 hub = sh.ThreadHub(1)
 tr = sh.ThreadTransport(hub, 0)
