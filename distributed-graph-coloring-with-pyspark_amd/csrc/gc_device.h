@@ -1,0 +1,50 @@
+// gc_device.h -- device helpers shared by the kernel files (variant A rounds, variant B).
+#pragma once
+#include "gcolor.h"
+#include "gc_internal.h"
+#include "gc_launch.h"
+
+// ------------------------------------------------------------------------------------
+// chunk geometry shared by the light kernels
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ long long gc_nchunks(long long cnt, int vpw) { return (cnt + vpw - 1) / vpw; }
+
+// Iterate the edge slots [0, total) of a wave chunk, two 64-slot groups per step so each
+// lane has two independent col[] -> gather chains in flight.  load(u) returns the
+// gathered value; apply(o, u, val) consumes it for owner lane o.
+template <typename Load, typename Apply>
+__device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, const long long* s_start, int excl,
+                                               int total, Load load, Apply apply) {
+    const int lane = gc_lane();
+    for (int base = 0; base < total; base += 2 * GC_WAVE) {
+        const int e0 = base + lane, e1 = e0 + GC_WAVE;
+        const int o0 = gc_owner(excl, e0);
+        const int o1 = gc_owner(excl, e1);
+        const int x0 = __shfl(excl, o0, GC_WAVE);
+        const int x1 = __shfl(excl, o1, GC_WAVE);
+        const bool v0 = e0 < total, v1 = e1 < total;
+        int u0 = 0, u1 = 0;
+        if (v0) u0 = col[s_start[o0] + (e0 - x0)];
+        if (v1) u1 = col[s_start[o1] + (e1 - x1)];
+        decltype(load(0)) g0{}, g1{};
+        if (v0) g0 = load(u0);
+        if (v1) g1 = load(u1);
+        if (v0) apply(o0, u0, g0);
+        if (v1) apply(o1, u1, g1);
+    }
+}
+
+// colour of u from the byte mirror (-1 uncoloured)
+__device__ __forceinline__ int gc_colour(const GDev& g, int u) {
+    const unsigned b = g.c8[u];
+    return b == GC_C8_NONE ? -1 : (b == GC_C8_BIG ? g.color[u] : (int)b);
+}
+
+// Committed colours live in the byte mirror c8 (what propose gathers); the int32 colour
+// array is written only for colours >= 254 and rebuilt from c8 by k_finalize.
+__device__ __forceinline__ void gc_commit_colour(GDev& g, int v, int cc) {
+    const unsigned char b = gc_c8_of(cc);
+    g.c8[v] = b;
+    if (b == GC_C8_BIG) g.color[v] = cc;
+    g.k8[v] = (unsigned char)gc_k8(GC_K8_NONE, GC_JP_UND);
+}

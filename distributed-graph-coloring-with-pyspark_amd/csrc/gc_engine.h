@@ -65,6 +65,8 @@ void gc_set_error(const char* fmt, ...);
 int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
+int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
+                       gc_stats* st);  // gc_variant_b.hip
 void gc_free_all(gc_graph* g);
 GDev gc_view(const gc_graph* g);
 GLists gc_lists(const gc_graph* g);

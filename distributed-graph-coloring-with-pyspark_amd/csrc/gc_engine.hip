@@ -419,8 +419,8 @@ struct Run {
 extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
                         gc_stats* stats) {
     if (!g || !opt) { gc_set_error("gc_color: null argument"); return GC_EINVAL; }
-    if (opt->variant != GC_VARIANT_A) {
-        gc_set_error("gc_color: variant %d not available on this build", opt->variant);
+    if (opt->variant != GC_VARIANT_A && opt->variant != GC_VARIANT_B) {
+        gc_set_error("gc_color: unknown variant %d", opt->variant);
         return GC_EINVAL;
     }
     GC_HIP(hipSetDevice(g->device));
@@ -438,6 +438,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         stats->round_seeds = keep.round_seeds;
         stats->max_color = -1;
     }
+    if (opt->variant == GC_VARIANT_B) return gc_color_variant_b(g, opt, colors_out, cround_out, stats);
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
     rc = run.go(colors_out, cround_out);

@@ -106,6 +106,7 @@ struct DevCtl {
     long long sweeps_enq;   // GC_H_SWEEPS: sweeps enqueued for the halted round
     int use_c4;             // this round's propose gathers the nibble mirror
     int resort;             // this round's frontier is rebuilt in vertex order
+    int fsort_all;          // variant B: rebuild the list as EVERY claimed uncoloured vertex, and count it
     int want_cround;        // commit records the round each vertex was coloured in
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed

@@ -1,0 +1,170 @@
+"""GPU parity of variant B (coloring_optimized.py) through the C-ABI.
+
+Bit-exact against the CPU oracle (oracle/gcolor_oracle.c, variant 1) and the golden
+vectors recorded by running the reference's coloring_optimized.py: final colours,
+per-round uncoloured / proposer / accepted counts, max proposal, the round each vertex
+was coloured, bounded-attempt failure round / count / snapshot.  The arrival-order fold
+(coloring_optimized.py:120-126, 168-200) runs as dependency-ordered admission / eviction
+passes (csrc/gc_variant_b.hip); these cases drive long dependency chains (hubs, cliques,
+directed lists with self-loops and duplicates) through it.
+"""
+import io
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import fixture_csr, golden_names, load_golden
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle  # noqa: E402
+from test_gpu_parity import _random_directed, assert_same_run  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _dg():
+    from gcolor_amd.engine import DeviceGraph
+    return DeviceGraph
+
+
+GOLD_B = [n for n in golden_names() if "B" in load_golden(n)["variants"]
+          and "load_error" not in load_golden(n)["variants"]["B"]["run"]]
+
+
+@pytest.mark.parametrize("name", GOLD_B)
+def test_golden_graphs_variant_b(name):
+    rec = load_golden(name)
+    ids, adj, rp, col = fixture_csr(rec)
+    with _dg().from_csr(rp, col) as dg:
+        o = oracle.c_color(rp, col, "B")
+        g = dg.color("B")
+        assert_same_run(g, o)
+        run = rec["variants"]["B"]["run"]
+        if run.get("colors") is not None:  # the reference terminated: direct golden check too
+            assert list(g.colors) == run["colors"]
+            assert list(g.round_U) == run["rounds_U"]
+            assert list(g.colored_round) == run["colored_round"]
+        for k in range(0, int(o["max_color"]) + 2):
+            assert_same_run(dg.color("B", num_colors=k), oracle.c_color(rp, col, "B", k=k))
+
+
+def test_shipped_colors_json_is_the_failed_k2_snapshot():
+    """The reference's colors.json == variant B's failed k=2 snapshot."""
+    rec = load_golden("graph_json")
+    ids, adj, rp, col = fixture_csr(rec)
+    with _dg().from_csr(rp, col) as dg:
+        g = dg.color("B", num_colors=2)
+        assert not g.ok
+        assert list(g.colors) == rec["variants"]["B"]["cli"]["output_colors"] == [0, 0, 1, -1, 1, -1, 0, 1, 1, 1]
+
+
+def test_survey_pins_seed0_10000_variant_b():
+    """Known-answer pin from SURVEY.md §8a (random.seed(0); Graph(10000, 8)), variant B."""
+    rec = load_golden("gen_10000_8_s0")
+    ids, adj, rp, col = fixture_csr(rec)
+    with _dg().from_csr(rp, col) as dg:
+        g = dg.color("B")
+        assert list(g.round_U) == [9958, 7243, 4256, 1670, 208, 1, 0]
+        assert g.max_color + 1 == 6
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_directed_multigraphs_with_selfloops_variant_b(seed):
+    rp, col = _random_directed(3000, 9000, seed)
+    with _dg().from_csr(rp, col) as dg:
+        o = oracle.c_color(rp, col, "B")
+        assert_same_run(dg.color("B"), o)
+        for k in (0, 1, 2, int(o["max_color"])):
+            assert_same_run(dg.color("B", num_colors=k), oracle.c_color(rp, col, "B", k=k))
+
+
+@pytest.mark.parametrize("n,d,seed", [(200_000, 16, 1), (50_000, 40, 3)])
+def test_uniform_graphs_variant_b(n, d, seed):
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(n, d, seed)
+    with _dg().from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("B")
+        assert_same_run(g, oracle.c_color(rp, col, "B"))
+        assert dg.validate() == (0, 0)
+
+
+@pytest.mark.parametrize("scale", [8, 12])
+def test_rmat_graphs_variant_b(scale):
+    with _dg().rmat(scale, 16, seed=scale) as dg:
+        rp, col = dg.export()
+        g = dg.color("B")
+        assert_same_run(g, oracle.c_color(rp, col, "B"))
+        assert dg.validate() == (0, 0)
+
+
+def test_heavy_vertices_and_wide_mex_variant_b():
+    n = 150 + 6000
+    adj = [[] for _ in range(n)]
+    for i in range(150):
+        for j in range(150):
+            if i != j:
+                adj[i].append(j)
+    for leaf in range(150, n):
+        adj[0].append(leaf)
+        adj[leaf].append(0)
+    for leaf in range(151, n, 7):
+        adj[leaf].append(leaf - 1)
+        adj[leaf - 1].append(leaf)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    with _dg().from_csr(rp, col) as dg:
+        o = oracle.c_color(rp, col, "B")
+        assert_same_run(dg.color("B"), o)
+        assert o["max_color"] >= 100
+
+
+def test_mesh_and_edgeless_variant_b():
+    DG = _dg()
+    with DG.mesh(16, 8, 4) as dg:
+        rp, col = dg.export()
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+    rp = np.zeros(4, np.int64)
+    col = np.zeros(0, np.int32)
+    with DG.from_csr(rp, col) as dg:
+        g = dg.color("B")
+        assert g.ok and list(g.colors) == [0, 0, 0] and list(g.round_U) == [0]
+
+
+CLI_B = [n for n in GOLD_B if not load_golden(n)["variants"]["B"]["cli"]["hang"]
+         and not load_golden(n)["variants"]["B"]["cli"].get("exception")]
+
+
+@pytest.mark.parametrize("name", CLI_B[::4])
+def test_cli_variant_b_matches_reference(name, tmp_path):
+    """`--variant B` reproduces coloring_optimized.py's transcript and output file."""
+    import hashlib
+    from gcolor_amd import cli
+    rec = load_golden(name)
+    cli_rec = rec["variants"]["B"]["cli"]
+    gpath = tmp_path / "g.json"
+    with open(gpath, "w") as f:
+        json.dump([{"id": i, "neighbors": nb, "color": -1} for i, nb in rec["graph"]], f, indent=4)
+    argv = list(cli_rec["argv"])
+    if "--input" in argv:
+        argv[argv.index("--input") + 1] = str(gpath)
+    else:
+        argv += ["--seed", str(rec["params"]["seed"])]
+        argv[argv.index("--output-graph") + 1] = str(tmp_path / "gen.json")
+    out_c = tmp_path / "c.json"
+    argv[argv.index("--output-coloring") + 1] = str(out_c)
+    buf = io.StringIO()
+    code = 0
+    try:
+        cli.main(argv + ["--variant", "B", "--compat-output"], out=buf)
+    except SystemExit as e:
+        code = e.code
+    assert (code or 0) == cli_rec["exit"]
+    lines = buf.getvalue().splitlines()
+    norm = [("Iteration time: <t> seconds" if ln.startswith("Iteration time") else
+             "Total execution time: <t> seconds" if ln.startswith("Total execution time") else ln) for ln in lines]
+    assert norm == cli_rec["stdout"]
+    if "output_sha256" in cli_rec:
+        assert hashlib.sha256(out_c.read_bytes()).hexdigest() == cli_rec["output_sha256"]
