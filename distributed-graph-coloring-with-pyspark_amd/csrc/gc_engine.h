@@ -27,6 +27,7 @@ struct gc_graph {
     unsigned* c4 = nullptr;
     unsigned char* k8 = nullptr;
     unsigned* inF = nullptr;
+    unsigned char* mark = nullptr;  // big-round push marks (zero between rounds)
     int* F[2] = {nullptr, nullptr};
     int* heavy = nullptr;
     int* wide = nullptr;

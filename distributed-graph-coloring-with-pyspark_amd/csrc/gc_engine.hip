@@ -59,6 +59,7 @@ GDev gc_view(const gc_graph* g) {
     d.c4 = g->c4;
     d.k8 = g->k8;
     d.inF = g->inF;
+    d.mark = g->mark;
     d.ctl = g->ctl;
     return d;
 }
@@ -105,6 +106,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->c4, n / 8 + 2);
     A(g->k8, n);
     A(g->inF, (n + 63) / 32 + 2);
+    A(g->mark, n + 64);
     A(g->F[0], n);
     A(g->F[1], n);
     A(g->heavy, n);
@@ -213,12 +215,23 @@ struct Run {
         return GC_OK;
     }
 
+    // big = the host also enqueues the big-round frontier build (k_pull, k_front_*): the
+    // device then decides per round (gc_big_on) whether the commit pushes or marks.
     void launch_commit(int mode, int nsweeps) {
+        const int big = mode == GC_CM_ROUND && resort_hint;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
-        gcl_commit(d, L, mode, nsweeps, s);
+        gcl_commit(d, L, mode, nsweeps, s, big);
         kt.end();
+        if (big) {
+            kt.begin(GC_K_COMMIT);
+            gcl_pull(d, big, s);
+            kt.end();
+            kt.begin(GC_K_OTHER);
+            gcl_front_build(d, L, g->fsum, s);
+            kt.end();
+        }
         kt.begin(GC_K_OTHER);
-        gcl_close(d, L, mode, s);
+        gcl_close(d, L, mode, s, big);
         kt.end();
     }
     void launch_sweeps(int from, int to) {  // sweeps from..to inclusive
@@ -310,6 +323,7 @@ struct Run {
         h.maxcolor = -1;
         h.fail_round = -1;
         h.want_cround = cround_out != nullptr;
+        h.pull_off = getenv("GC_NO_PULL") ? 1 : 0;
         GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, s));
         GC_HIP(hipEventRecord(g->ev0, s));
         // init + seed (coloring.py:74-76)

@@ -107,6 +107,8 @@ struct DevCtl {
     int use_c4;             // this round's propose gathers the nibble mirror
     int resort;             // this round's frontier is rebuilt in vertex order
     int fsort_all;          // variant B: rebuild the list as EVERY claimed uncoloured vertex, and count it
+    int pull_off;           // never pull the frontier (GC_NO_PULL: A/B measurements)
+    int sorted;             // the current frontier list is in vertex order (built by k_front_*)
     int want_cround;        // commit records the round each vertex was coloured in
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed

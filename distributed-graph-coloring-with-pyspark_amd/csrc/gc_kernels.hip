@@ -51,6 +51,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
             g.cround[v] = iso ? 0 : -1;
             g.c8[v] = iso ? 0 : (unsigned char)GC_C8_NONE;
             g.k8[v] = push0 ? gc_k8(0u, GC_JP_IN) : gc_k8(GC_K8_NONE, GC_JP_UND);
+            g.mark[v] = 0;
             if (!iso) {
                 unc++;
                 const ull k = ((ull)d << 32) | (ull)v;
@@ -132,7 +133,8 @@ __device__ __forceinline__ bool gc_resort_on(const GDev& g, const DevCtl* c) {
 __global__ void __launch_bounds__(GC_BLOCK) k_fsort_count(GDev g, unsigned* bsum) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    const bool on = c->fsort_all ? true : gc_resort_on(g, c);  // fsort_all: list = every claimed uncoloured vertex
+    // fsort_all: list = every claimed uncoloured vertex; a list built by k_front_* is in order already
+    const bool on = c->fsort_all ? true : (gc_resort_on(g, c) && !c->sorted);
     if (blockIdx.x == 0 && threadIdx.x == 0) c->resort = on ? 1 : 0;
     if (!on) return;
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
@@ -150,9 +152,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_fsort_count(GDev g, unsigned* bsum
 }
 
 // exclusive scan of the per-workgroup counts, one workgroup of 1024 threads
-__global__ void __launch_bounds__(1024) k_fsort_scan(GDev g, unsigned* bsum, int nblocks) {
+__device__ __forceinline__ bool gc_big_on(const GDev& g, const DevCtl* c);
+__device__ __forceinline__ bool gc_front_on(const GDev& g, const DevCtl* c, int allow_big);
+
+// build = 0: the re-sort of the current list; build = 1: the next frontier of a big round
+// (k_front_count), whose total becomes its count.
+__global__ void __launch_bounds__(1024) k_fsort_scan(GDev g, unsigned* bsum, int nblocks, int build) {
     DevCtl* c = g.ctl;
-    if (c->halt || !c->resort) return;
+    if (build ? !gc_front_on(g, c, 1) : (c->halt || !c->resort)) return;
     __shared__ unsigned s_part[1024];
     const int per = (nblocks + 1023) / 1024;
     const int b0 = threadIdx.x * per;
@@ -166,7 +173,10 @@ __global__ void __launch_bounds__(1024) k_fsort_scan(GDev g, unsigned* bsum, int
         s_part[threadIdx.x] += y;
         __syncthreads();
     }
-    if (c->fsort_all && threadIdx.x == 1023) c->fcnt[c->cur] = s_part[1023];  // the list is rebuilt, not re-sorted
+    if (threadIdx.x == 1023) {
+        if (build) c->fcnt[c->cur ^ 1] = s_part[1023];
+        else if (c->fsort_all) c->fcnt[c->cur] = s_part[1023];  // the list is rebuilt, not re-sorted
+    }
     unsigned run = s_part[threadIdx.x] - local;  // exclusive prefix of this thread's run
     for (int i = 0; i < per && b0 + i < nblocks; ++i) {
         const unsigned x = bsum[b0 + i];
@@ -175,9 +185,9 @@ __global__ void __launch_bounds__(1024) k_fsort_scan(GDev g, unsigned* bsum, int
     }
 }
 
-__global__ void __launch_bounds__(GC_BLOCK) k_fsort_write(GDev g, const unsigned* bpre, GLists L) {
+__global__ void __launch_bounds__(GC_BLOCK) k_fsort_write(GDev g, const unsigned* bpre, GLists L, int build) {
     DevCtl* c = g.ctl;
-    if (c->halt || !c->resort) return;
+    if (build ? !gc_front_on(g, c, 1) : (c->halt || !c->resort)) return;
     __shared__ unsigned s_w[GC_WAVES_PER_BLOCK];
     const long long words = ((long long)g.n + 31) / 32;
     const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
@@ -189,7 +199,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_fsort_write(GDev g, const unsigned
     unsigned off = bpre[blockIdx.x];
     for (int i = 0; i < (int)(threadIdx.x / GC_WAVE); ++i) off += s_w[i];
     off += (unsigned)(incl - cnt);
-    int* out = L.F[c->cur];
+    int* out = L.F[build ? c->cur ^ 1 : c->cur];
     unsigned mm = m;
     while (mm) {
         const int k = __builtin_ctz(mm);
@@ -621,11 +631,32 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
 }
 
+// The frontier of a big round (F >= n/64, with the host's allow_big) is not appended to:
+// it is every claimed uncoloured vertex, rebuilt in vertex order from the claim bitmap by
+// k_front_count / k_fsort_scan / k_fsort_write after the commit -- losers are claimed
+// already, newly reached vertices get claimed without atomics:
+//   push  each winner marks its in-neighbours with plain byte stores (mark[x] = 1), which
+//         k_front_count merges into inF;
+//   pull  once the dormant set -- uncoloured vertices with no coloured listed neighbour,
+//         U - F of them -- is small next to the frontier, the winners' in-edges mostly hit
+//         vertices already claimed; the dormant vertices scan their own rows instead
+//         (k_pull) and claim themselves.
+// Small rounds keep the claim-and-append push.  The next frontier is the same set in
+// every case.
+__device__ __forceinline__ bool gc_big_on(const GDev& g, const DevCtl* c) { return gc_resort_on(g, c); }
+__device__ __forceinline__ bool gc_front_on(const GDev& g, const DevCtl* c, int allow_big) {
+    return allow_big && !c->halt && gc_big_on(g, c);
+}
+__device__ __forceinline__ bool gc_pull_on(const DevCtl* c) {
+    const long long F = (long long)c->fcnt[c->cur];
+    return 2 * (c->U - F) <= F && !c->pull_off;
+}
+
 // mode GC_CM_ROUND: light = F[cur] (hubs skipped), heavy = the heavy list, output F[cur^1];
 // GC_CM_INIT / GC_CM_RESEED: light = seeds[0], heavy = seeds[1], output F[cur].
 // nsweeps: sweeps enqueued for this round; undecided vertices left in the last sweep's
 // slot mean the host must enqueue more sweeps first (GC_H_SWEEPS, resume after nsweeps).
-__global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps) {
+__global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps, int allow_big) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
@@ -654,6 +685,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     const int nxt = rnd ? cur ^ 1 : cur;
     int* next = L.F[nxt];
     ull* next_cnt = &c->fcnt[nxt];
+    const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);  // next list: k_front_*
+    const bool mark = big && !gc_pull_on(c);                              // else k_pull claims
     GcStage st{s_stage[w], 0};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
@@ -671,12 +704,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
-            } else if (js == GC_JP_OUT) {
+            } else if (js == GC_JP_OUT && !big) {
                 next[atomicAdd(next_cnt, 1ull)] = v;
             }
         }
         __syncthreads();
-        if (s_acc) {
+        if (s_acc && (mark || !big)) {
             const long long ts = g.trp[v], te = g.trp[v + 1];
             for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
                 const long long e = e0 + threadIdx.x;
@@ -684,7 +717,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 int x = 0;
                 if (e < te) {
                     x = g.tcol[e];
-                    claim = gc_claim(g.inF, x);
+                    if (mark) g.mark[x] = 1;
+                    else claim = gc_claim(g.inF, x);
                 }
                 gc_stage_push(st, claim, x, next, next_cnt);
             }
@@ -714,9 +748,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             tstart = g.trp[v];
             din = (int)(g.trp[v + 1] - tstart);
             lsum += (ull)din;
+            if (big && !mark) din = 0;
         }
         // losers stay in the frontier (they still have a coloured neighbour)
-        gc_stage_push(st, js == GC_JP_OUT, v, next, next_cnt);
+        gc_stage_push(st, js == GC_JP_OUT && !big, v, next, next_cnt);
         s_start[w][lane] = tstart;
         const int incl = gc_wave_incl_scan(din);
         const int excl = incl - din;
@@ -730,7 +765,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             int x = 0;
             if (e < total) {
                 x = g.tcol[s_start[w][o] + (e - eo)];
-                claim = gc_claim(g.inF, x);
+                if (mark) g.mark[x] = 1;
+                else claim = gc_claim(g.inF, x);
             }
             gc_stage_push(st, claim, x, next, next_cnt);
         }
@@ -744,12 +780,84 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
 }
 
+// Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
+// uncoloured with no coloured listed neighbour before this round -- scans its own row for
+// a neighbour coloured now and claims itself.  A wave owns 64 consecutive vertices, i.e.
+// two whole inF words, so the claims are plain stores.
+__global__ void __launch_bounds__(GC_BLOCK) k_pull(GDev g, int allow_big) {
+    DevCtl* c = g.ctl;
+    if (!gc_front_on(g, c, allow_big) || !gc_pull_on(c)) return;
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long n = g.n;
+    const long long steps = (n + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v = sidx * GC_WAVE + lane;
+        const unsigned word = v < n ? g.inF[v >> 5] : 0xFFFFFFFFu;
+        const bool dorm = v < n && !((word >> (v & 31)) & 1u);
+        if (!__ballot(dorm)) continue;
+        bool hit = false;
+        if (dorm && g.c8[v] == GC_C8_NONE) {
+            const long long ee = g.rp[v + 1];
+            for (long long e = g.rp[v]; e < ee && !hit; ++e) hit = g.c8[g.col[e]] != GC_C8_NONE;
+        }
+        const ull m = __ballot(hit);
+        if (lane == 0 && (unsigned)m) g.inF[v >> 5] = word | (unsigned)m;
+        if (lane == 32 && (unsigned)(m >> 32)) g.inF[v >> 5] = word | (unsigned)(m >> 32);
+    }
+}
+
+// Next frontier of a big round, pass 1: merge this word's marks into the claim bitmap
+// (clearing them) and count its claimed uncoloured vertices per workgroup.  Passes 2/3 are
+// k_fsort_scan / k_fsort_write with build = 1 (next list slot, count from the scan).
+__global__ void __launch_bounds__(GC_BLOCK) k_front_count(GDev g, unsigned* bsum) {
+    DevCtl* c = g.ctl;
+    if (!gc_front_on(g, c, 1)) return;
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    const long long words = ((long long)g.n + 31) / 32;
+    const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
+    ull cnt = 0;
+    if (w < words) {
+        const long long v0 = w * 32;
+        unsigned mk = 0u;
+        if (v0 + 32 <= (long long)g.n) {
+            uint4* p = reinterpret_cast<uint4*>(g.mark + v0);
+            const uint4 a = p[0], b = p[1];
+            const unsigned x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)  // mark bytes are 0 or 1
+                mk |= ((x[k] & 1u) | ((x[k] >> 7) & 2u) | ((x[k] >> 14) & 4u) | ((x[k] >> 21) & 8u)) << (4 * k);
+            if (mk) p[0] = p[1] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            for (int k = 0; k < 32 && v0 + k < (long long)g.n; ++k)
+                if (g.mark[v0 + k]) {
+                    mk |= 1u << k;
+                    g.mark[v0 + k] = 0;
+                }
+        }
+        if (mk) g.inF[w] |= mk;  // this thread owns the word
+        cnt = (ull)__popc(gc_front_word(g, w));
+    }
+    cnt = gc_wave_sum(cnt);
+    if (gc_lane() == 0) scratch[threadIdx.x / GC_WAVE] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ull t = 0;
+        for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += scratch[i];
+        bsum[blockIdx.x] = (unsigned)t;
+    }
+}
+
 // Closes the round (or the INIT / RESEED seeding) after its commit: one thread, so every
 // counter the commit's workgroups updated is visible across the launch boundary.
-__global__ void k_close(GDev g, GLists L, int mode) {
+__global__ void k_close(GDev g, GLists L, int mode, int allow_big) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) gc_close_round(L, c, mode);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
+        gc_close_round(L, c, mode);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1176,8 +1284,15 @@ void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s) {
     const int nb = gcl_fsort_blocks(g.n);
     if (nb <= 0) return;
     hipLaunchKernelGGL(k_fsort_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
-    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb);
-    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L);
+    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 0);
+    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 0);
+}
+void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s) {
+    const int nb = gcl_fsort_blocks(g.n);
+    if (nb <= 0) return;
+    hipLaunchKernelGGL(k_front_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
+    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 1);
+    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 1);
 }
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
@@ -1209,14 +1324,17 @@ void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
 }
 void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
-void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s) {
-    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode);
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big) {
+    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big);
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
 }
-void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s) {
-    hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps);
+void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
+    hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
+}
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big) {
+    hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

@@ -20,6 +20,7 @@ struct GDev {
     unsigned* c4;
     unsigned char* k8;
     unsigned int* inF;
+    unsigned char* mark;  // big rounds: in-neighbours of the winners (0/1), merged into inF
     DevCtl* ctl;
 };
 
@@ -44,8 +45,10 @@ void gcl_propose(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
-void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s);
-void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s);
+void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
+void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0);
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0);
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                hipStream_t s);
