@@ -48,3 +48,10 @@ __device__ __forceinline__ void gc_commit_colour(GDev& g, int v, int cc) {
     if (b == GC_C8_BIG) g.color[v] = cc;
     g.k8[v] = (unsigned char)gc_k8(GC_K8_NONE, GC_JP_UND);
 }
+
+// counters shared across workgroups: read with an atomic RMW, written agent-scope
+__device__ __forceinline__ ull gc_aread(ull* p) { return atomicAdd(p, 0ull); }
+template <typename T>
+__device__ __forceinline__ void gc_st(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

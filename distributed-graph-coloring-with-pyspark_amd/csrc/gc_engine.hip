@@ -219,6 +219,11 @@ struct Run {
     // device then decides per round (gc_big_on) whether the commit pushes or marks.
     void launch_commit(int mode, int nsweeps) {
         const int big = mode == GC_CM_ROUND && resort_hint;
+        if (mode == GC_CM_ROUND) {
+            kt.begin(GC_K_SWEEP);
+            gcl_sweep_tail(d, L, nsweeps, s);
+            kt.end();
+        }
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
         gcl_commit(d, L, mode, nsweeps, s, big);
         kt.end();
@@ -273,7 +278,7 @@ struct Run {
     // was decided by the first sweep (meshes), else twice the last round's depth
     static int pick_sweeps(const DevCtl& h) {
         if (h.maxdepth <= 1) return 0;
-        return (int)std::min<long long>(64, h.lastdepth + 2);
+        return (int)std::min<long long>(64, h.lastbig + 2);  // the small-list tail runs in k_sweep_tail
     }
     // rounds per batch: small while the frontier is tiny or the colouring is nearly done
     static int pick_batch(const DevCtl& h, long long n, int prev) {

@@ -34,6 +34,8 @@ typedef unsigned long long ull;
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
 #define GC_ROUND_GRID 2048
+#define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
+#define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
 #define GC_BLOCK_GRID 1024
 // dynamic LDS words of the workgroup-per-vertex mex bitmap (128 Ki colours per window)
 #define GC_MEX_WORDS 4096
@@ -104,6 +106,9 @@ struct DevCtl {
     long long maxdepth;     // max JP passes of a round (first sweep included)
     long long lastdepth;    // JP passes of the last closed round
     long long sweeps_enq;   // GC_H_SWEEPS: sweeps enqueued for the halted round
+    long long bigsweeps;    // this round: last full-grid sweep whose input exceeded the tail limits
+    long long lastbig;      // bigsweeps of the last closed round (host: full-grid sweeps to enqueue)
+    long long tail_last;    // this round: index of the last sweep run (k_sweep_tail)
     int use_c4;             // this round's propose gathers the nibble mirror
     int resort;             // this round's frontier is rebuilt in vertex order
     int fsort_all;          // variant B: rebuild the list as EVERY claimed uncoloured vertex, and count it

@@ -532,12 +532,53 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
         c->und_cnt[z] = 0;
         c->undh_cnt[z] = 0;
         if (cl + ch > 0) c->sweeps += 1;
+        if (cl > GC_TAIL_MAX || ch > GC_TAIL_HMAX) c->bigsweeps = i;
     }
     if (cl + ch == 0) return;
     ull lsum = 0, lnv = 0;
     gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                 &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
+    gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
+    gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
+}
+
+// The rest of a round's sweeps in ONE workgroup, after the host's S full-grid sweeps: the
+// deep end of a JP resolution is a chain of sweeps over a few hundred vertices each, which
+// as separate 2048-workgroup launches cost a launch gap apiece (and the sweeps enqueued
+// beyond the round's depth ran idle).  Here they run back to back, a workgroup barrier
+// apart, while the undecided lists stay within GC_TAIL_MAX / GC_TAIL_HMAX; a bigger list
+// is left to full-grid sweeps (the commit then asks the host for them, GC_H_SWEEPS).
+// Counters are read with atomic RMWs and cleared with agent-scope stores; list entries and
+// states written before a barrier are visible to the whole workgroup after it.
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ long long s_cl, s_ch;
+    int j = S;
+    ull lsum = 0, lnv = 0;
+    for (;;) {
+        const int in = j % 3;
+        if (threadIdx.x == 0) {
+            s_cl = (long long)gc_aread(&c->und_cnt[in]);
+            s_ch = (long long)gc_aread(&c->undh_cnt[in]);
+        }
+        __syncthreads();
+        const long long cl = s_cl, ch = s_ch;
+        if (cl + ch == 0 || cl > GC_TAIL_MAX || ch > GC_TAIL_HMAX) break;
+        ++j;
+        const int out = j % 3, z = (j + 1) % 3;  // out was cleared by the sweep before
+        if (threadIdx.x == 0) {
+            gc_st(&c->und_cnt[z], 0ull);
+            gc_st(&c->undh_cnt[z], 0ull);
+            gc_st(&c->sweeps, c->sweeps + 1);
+        }
+        gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
+                    &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gc_st(&c->tail_last, (long long)j);
     gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
     gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
 }
@@ -553,11 +594,6 @@ __device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
     return !(atomicOr(&inF[x >> 5], bit) & bit);
 }
 
-__device__ __forceinline__ ull gc_aread(ull* p) { return atomicAdd(p, 0ull); }
-template <typename T>
-__device__ __forceinline__ void gc_st(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ void gc_record(const GLists& L, DevCtl* c, long long U, long long F, long long maxmex,
                                           long long acc, long long seeds, long long sweeps) {
@@ -603,6 +639,8 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
         gc_st(&c->sweep_total, c->sweep_total + (sw > 0 ? sw - 1 : 0));
         if (sw > c->maxdepth) gc_st(&c->maxdepth, sw);
         gc_st(&c->lastdepth, sw);
+        gc_st(&c->lastbig, c->bigsweeps);
+        gc_st(&c->bigsweeps, 0ll);
         gc_record(L, c, U, F, c->maxmex, acc, 0, sw);
         U -= acc;
         gc_st(&c->fcnt[cur], 0ull);  // becomes the next round's output slot
@@ -665,10 +703,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ int s_acc;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const int last_slot = nsweeps % 3;
+    const long long last = mode == GC_CM_ROUND ? c->tail_last : nsweeps;  // k_sweep_tail ran before
+    const int last_slot = (int)(last % 3);
     if (mode == GC_CM_ROUND && (c->und_cnt[last_slot] | c->undh_cnt[last_slot])) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            c->sweeps_enq = nsweeps;
+            c->sweeps_enq = last;
             c->halt = GC_H_SWEEPS;
         }
         return;
@@ -1329,6 +1368,9 @@ void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allo
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
+}
+void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep_tail, dim3(1), dim3(GC_BLOCK), 0, s, g, L, S);
 }
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
