@@ -15,6 +15,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 GC_OK, GC_FAILED, GC_STALLED = 0, 1, 2
 GC_EINVAL, GC_EHIP, GC_ENOMEM, GC_ERCCL, GC_EROUNDS = -1, -2, -3, -4, -5
+GC_EUNSUPPORTED, GC_EKEY, GC_EIO = -6, -7, -8
 GC_GRAPH_SYMMETRIC = 1
 GC_VARIANT_A, GC_VARIANT_B = 0, 1
 GC_NKERNELS = 8
@@ -26,7 +27,9 @@ EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", 
            "gc_gen_uniform", "gc_last_error", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
            "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors",
-           "gc_shard_get_slice", "gc_shard_put_slices"]
+           "gc_shard_get_slice", "gc_shard_put_slices",
+           "gc_json_read_graph", "gc_json_write_coloring", "gc_json_write_graph", "gc_csr_write", "gc_csr_read",
+           "gc_csr_free"]
 
 
 class GcOptions(ctypes.Structure):
@@ -35,6 +38,12 @@ class GcOptions(ctypes.Structure):
 
 
 _I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+class GcCsr(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("nnz", ctypes.c_int64), ("row_ptr", ctypes.POINTER(ctypes.c_int64)),
+                ("col", ctypes.POINTER(ctypes.c_int32)), ("ids", ctypes.POINTER(ctypes.c_int64)),
+                ("flags", ctypes.c_uint32)]
 
 
 class GcStats(ctypes.Structure):
@@ -97,6 +106,12 @@ def load():
         "gc_shard_finish": ([P, I64, _I64P, _I64P], ctypes.c_int),
         "gc_shard_reseed": ([P, I64, _I64P, _I64P], ctypes.c_int),
         "gc_shard_colors": ([P, P, P], ctypes.c_int),
+        "gc_json_read_graph": ([ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(GcCsr))], ctypes.c_int),
+        "gc_json_write_coloring": ([ctypes.c_char_p, P, P, I64], ctypes.c_int),
+        "gc_json_write_graph": ([ctypes.c_char_p, P, P, P, I64, P], ctypes.c_int),
+        "gc_csr_write": ([ctypes.c_char_p, P, P, P, I64, I64, U32], ctypes.c_int),
+        "gc_csr_read": ([ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(GcCsr))], ctypes.c_int),
+        "gc_csr_free": ([ctypes.POINTER(GcCsr)], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

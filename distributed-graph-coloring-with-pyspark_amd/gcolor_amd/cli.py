@@ -4,7 +4,8 @@ Same flags, stdout lines, exit codes and JSON files as the reference.  Additive 
 ``--variant {A,B}`` (A = coloring.py, B = coloring_optimized.py), ``--seed`` (seeds
 Python's ``random`` before generation so ``Graph(N, D)`` is reproducible),
 ``--compat-output`` (write the reference's exact output file, see below), ``--no-e1``,
-``--device``.
+``--device``.  ``--input`` also takes a binary CSR file (``.gcsr``, detected by its magic
+bytes) and ``--output-graph x.gcsr`` writes one.
 
 The reference decrements k from K0 and reruns the whole colouring until an attempt fails
 (coloring.py:211-231).  Attempt k is the unbounded run cut at the first round whose
@@ -74,7 +75,7 @@ def transcript(K0, full, full_ms, full_val, bounded=None, bounded_ms=0.0, bounde
 
 def build_parser():
     p = argparse.ArgumentParser(description="Graph Coloring CLI")
-    p.add_argument("--input", type=str, help="Input graph file (JSON)")
+    p.add_argument("--input", type=str, help="Input graph file (JSON, or binary .gcsr)")
     p.add_argument("--node-count", type=int, help="Number of nodes for graph generation")
     p.add_argument("--max-degree", type=int, help="Maximum degree for graph generation")
     p.add_argument("--output-graph", type=str, help="Output file to serialize the generated graph")
@@ -101,7 +102,7 @@ def main(argv=None, out=None):
     # Load or generate graph (coloring.py:174-187)
     if args.input:
         try:
-            ids, rp, col = graphio.load_graph_json(args.input)
+            ids, rp, col = graphio.load_graph(args.input)
         except Exception as e:  # same message and status as coloring.py:179-181
             say(f"Error loading graph: {e}")
             sys.exit(1)
@@ -113,7 +114,10 @@ def main(argv=None, out=None):
         rp, col = reference_csr(args.node_count, args.max_degree)
         ids = list(range(args.node_count))
         if args.output_graph:
-            graphio.write_graph_json(args.output_graph, ids, rp, col)
+            if args.output_graph.endswith(".gcsr"):  # binary CSR
+                graphio.write_csr(args.output_graph, rp, col, symmetric=True)
+            else:
+                graphio.write_graph_json(args.output_graph, ids, rp, col)
 
     from .engine import DeviceGraph  # the HIP library; fails loudly without it
     if args.device is not None:

@@ -37,6 +37,9 @@ extern "C" {
 #define GC_ENOMEM (-3)
 #define GC_ERCCL (-4)
 #define GC_EROUNDS (-5)
+#define GC_EUNSUPPORTED (-6) /* JSON the native reader leaves to Python's json + graph.py rules  */
+#define GC_EKEY (-7)         /* neighbour id that is no node id: KeyError (gc_last_error() = id)  */
+#define GC_EIO (-8)
 
 /* ---- graph -------------------------------------------------------------------------- */
 typedef struct gc_graph gc_graph;
@@ -170,6 +173,35 @@ int gc_shard_colors(gc_shard* s, int32_t* colors_out, int32_t* colored_round_out
    always enough); *nnz_out receives the entry count.                                 */
 int gc_gen_uniform(int64_t n, int32_t max_degree, uint64_t seed, int64_t* row_ptr, int32_t* col,
                    int64_t col_cap, int64_t* nnz_out);
+
+/* ---- graph files ------------------------------------------- */
+/* A host CSR owned by the library (free with gc_csr_free).  ids: the JSON node ids in
+   file order (NULL for a GCSR file written without ids: ids = positions).            */
+typedef struct gc_csr {
+    int64_t n, nnz;
+    int64_t* row_ptr; /* int64[n+1] */
+    int32_t* col;     /* int32[nnz], file positions */
+    int64_t* ids;     /* int64[n] or NULL */
+    uint32_t flags;   /* GC_GRAPH_SYMMETRIC when the writer asserted it */
+} gc_csr;
+/* The reference's JSON graph -> CSR over file positions.
+   Replaces: Graph.deserialize_graph, graph.py:15-28 (json.load + id -> Node linking).
+   Exact on what it accepts (int64 ids, integer neighbour lists, strict JSON); a repeated
+   id resolves to its LAST node (graph.py:23); the first unknown neighbour id in file
+   order returns GC_EKEY with the id as the message (graph.py:25 KeyError).  Anything
+   else returns GC_EUNSUPPORTED and the caller applies Python's own rules.            */
+int gc_json_read_graph(const char* path, gc_csr** out);
+/* json.dump(result, f, indent=4) of [{"id", "color"}] (coloring.py:238-241) and of
+   [{"id", "neighbors", "color"}] (graph.py:10-12, node.py:8-13), byte-identical to
+   Python's encoder.  ids may be NULL (ids = positions); colors NULL writes -1.        */
+int gc_json_write_coloring(const char* path, const int64_t* ids, const int32_t* colors, int64_t n);
+int gc_json_write_graph(const char* path, const int64_t* ids, const int64_t* row_ptr, const int32_t* col,
+                        int64_t n, const int32_t* colors);
+/* Binary CSR (.gcsr) for graphs beyond JSON scale; layout in csrc/gc_io_host.cpp.     */
+int gc_csr_write(const char* path, const int64_t* row_ptr, const int32_t* col, const int64_t* ids, int64_t n,
+                 int64_t nnz, uint32_t flags);
+int gc_csr_read(const char* path, gc_csr** out);
+void gc_csr_free(gc_csr* c);
 
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gc_last_error(void);

@@ -51,7 +51,7 @@ def test_json_roundtrip_and_output_bytes(name, tmp_path):
         json.dump([{"id": i, "neighbors": nb, "color": -1} for i, nb in rec["graph"]], f, indent=4)
     ids, rp, col = graphio.load_graph_json(str(gpath))
     ids2, _, rp2, col2 = fixture_csr(rec)
-    assert ids == ids2 and np.array_equal(rp, rp2) and np.array_equal(col, col2)
+    assert list(ids) == list(ids2) and np.array_equal(rp, rp2) and np.array_equal(col, col2)
     for v, vr in rec["variants"].items():
         cli_rec = vr["cli"]
         if "output_sha256" not in cli_rec:

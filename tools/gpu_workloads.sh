@@ -1,0 +1,6 @@
+set -euo pipefail
+mkdir -p gpurun_out/r01_wl
+for w in rmat24 rmat26 mesh256 mesh512; do
+  timeout -k 10 280 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --json-out gpurun_out/r01_wl/bench_$w.json > gpurun_out/r01_wl/bench_$w.log 2>&1
+  tail -1 gpurun_out/r01_wl/bench_$w.log | cut -c1-400
+done
