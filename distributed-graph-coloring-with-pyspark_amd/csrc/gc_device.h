@@ -55,3 +55,37 @@ template <typename T>
 __device__ __forceinline__ void gc_st(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// hubs (gc_hubs.hip): set colour cc in hub x's forbidden-colour bitmap (colours past the
+// bitmap are not tracked: such a hub scans its row when its mex could lie beyond it)
+__device__ __forceinline__ void gc_hub_mark(const GDev& g, int x, int cc) {
+    if (cc >= 32 * g.hub_w) return;
+    unsigned* p = g.hbits + (long long)x * g.hub_w + (cc >> 5);
+    const unsigned bit = 1u << (cc & 31);
+    if (!(*p & bit)) atomicOr(p, bit);
+}
+// every hub listing v, strided over the calling threads
+__device__ __forceinline__ void gc_hub_mark_row(const GDev& g, int v, int cc, int t0, int step) {
+    const long long e1 = g.hin_rp[v + 1];
+    for (long long e = g.hin_rp[v] + t0; e < e1; e += step) gc_hub_mark(g, g.hin_col[e], cc);
+}
+// heavy entries the one-workgroup tail sweeps may take
+__device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.hub_w ? GC_TAIL_HMAX_HUB : GC_TAIL_HMAX; }
+
+// Which hubs sweep i (>= 1) takes, from values fixed before the kernel (gc_hubs.hip): hubs
+// off -- the undecided heavy list; hubs already started (hub_start < i) -- likewise; not
+// started and the lights converged (cl == 0) -- every hub proposer, and this sweep starts
+// them (returns true: the caller records hub_start = i); lights still undecided -- none.
+// The caller's thread 0 may store hub_start = i while other workgroups evaluate this: they
+// read either the old value (>= i) or i, and take the same branch either way.
+__device__ __forceinline__ bool gc_hub_gate(const GDev& g, const DevCtl* c, long long i, long long cl,
+                                            const int*& hl, long long& ch, const GLists& L) {
+    if (!g.hub_w || __hip_atomic_load(const_cast<long long*>(&c->hub_start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i) return false;
+    if (cl == 0) {
+        hl = L.heavy;
+        ch = (long long)c->heavy_cnt;
+        return true;
+    }
+    ch = 0;
+    return false;
+}

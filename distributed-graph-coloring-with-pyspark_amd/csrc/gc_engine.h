@@ -38,6 +38,21 @@ struct gc_graph {
     int* parent = nullptr;
     ull* best = nullptr;
     int* vcolors = nullptr;
+    // hubs (gc_hubs.hip), built on the first variant-A colouring that wants them
+    int hub_t = -1;            // threshold they were built for (-1: none)
+    int hub_w = 0;             // bitmap words per hub
+    long long nhub = 0;
+    int* hid = nullptr;
+    int* hub_v = nullptr;
+    long long* hin_rp = nullptr;
+    int* hin_col = nullptr;
+    unsigned* hbits = nullptr;
+    unsigned* hkill = nullptr;
+    long long* hlow_rp = nullptr;
+    int* hlow_col = nullptr;
+    int* hcur = nullptr;
+    int* hpc = nullptr;
+    int* hpend = nullptr;
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;
@@ -66,6 +81,8 @@ void gc_set_error(const char* fmt, ...);
 int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
+int gc_hubs_prepare(gc_graph* g, GDev& d);  // gc_hubs.hip: build (once) + reset; fills d's hub fields
+void gc_hubs_free(gc_graph* g);
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
                        gc_stats* st);  // gc_variant_b.hip
 void gc_free_all(gc_graph* g);

@@ -61,6 +61,19 @@ GDev gc_view(const gc_graph* g) {
     d.inF = g->inF;
     d.mark = g->mark;
     d.ctl = g->ctl;
+    d.heavy_t = GC_HEAVY_T;
+    d.hub_w = 0;
+    d.hid = nullptr;
+    d.hub_v = nullptr;
+    d.hin_rp = nullptr;
+    d.hin_col = nullptr;
+    d.hbits = nullptr;
+    d.hkill = nullptr;
+    d.hlow_rp = nullptr;
+    d.hlow_col = nullptr;
+    d.hcur = nullptr;
+    d.hpc = nullptr;
+    d.hpend = nullptr;
     return d;
 }
 
@@ -325,6 +338,7 @@ struct Run {
         h.e1 = opt->e1 ? 1 : 0;
         h.rcap = g->rcap;
         h.maxmex = -1;
+        h.hub_start = GC_HUB_NOT_STARTED;
         h.maxcolor = -1;
         h.fail_round = -1;
         h.want_cround = cround_out != nullptr;
@@ -460,6 +474,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     if (opt->variant == GC_VARIANT_B) return gc_color_variant_b(g, opt, colors_out, cround_out, stats);
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
+    if ((rc = gc_hubs_prepare(g, run.d))) return rc;
     rc = run.go(colors_out, cround_out);
     if (rc < 0) return rc;
     if (stats && stats->round_cap < (long long)run.recs.size() && (stats->round_U || stats->round_F)) {

@@ -144,6 +144,7 @@ void gc_free_all(gc_graph* g) {
     hipSetDevice(g->device);
     if (g->trp && g->trp != g->rp) hipFree(g->trp);
     if (g->tcol && g->tcol != g->col) hipFree(g->tcol);
+    gc_hubs_free(g);
     if (g->borrowed) {  // a shard's view: the CSR belongs to the replicated graph handle
         g->rp = nullptr;
         g->col = nullptr;

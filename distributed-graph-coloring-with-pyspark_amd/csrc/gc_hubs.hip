@@ -1,0 +1,247 @@
+// gc_hubs.hip -- push-maintained state of the high-degree vertices (variant A, one GPU).
+//
+// On power-law graphs (R-MAT) the rank (deg, pos) of coloring.py:64 puts hubs last: a hub
+// loses round after round and stays in the frontier for hundreds of rounds.  Done as the
+// reference states it, every one of those rounds re-reads the hub's whole row twice --
+// assign_color's set of neighbour colours (coloring.py:44-54) and resolve_collisions'
+// same-colour check (coloring.py:56-70) -- and the JP sweeps re-read the low part again
+// per sweep: on R-MAT-24 that is ~40x nnz of gathers.  Hubs (deg > heavy_t) instead keep
+// the two facts those reads establish, and the low-degree side pushes them:
+//   hbits  forbidden-colour bitmap: when u is coloured c (any commit: seed, round, E1),
+//          u sets bit c in every hub that lists u (hin = the hub-restricted transpose).
+//          The hub's mex is the first zero bit -- the same value as the mex of its coloured
+//          neighbours' colours, because the bitmap holds exactly those colours (< 4096;
+//          beyond that the hub falls back to the row scan).
+//   hkill  conflict resolution: a light vertex's low row holds only light vertices (every
+//          hub ranks above it), so the lights' Jones-Plassmann sweeps never wait on a hub.
+//          Hubs therefore sit out the sweeps until the lights have converged; a light that
+//          decides IN flags every hub that lists it and proposes its candidate (hkill, via
+//          its hin row).  Then a hub is OUT if flagged, and otherwise runs JP against the
+//          lower-rank HUBS of its row only (hlow, built once): exactly the LFMIS rule of
+//          coloring.py:56-70 over its whole low row, because every light entry is decided
+//          by then and the flag says whether one of them won the same colour.
+// Both are sets and flags: the order of pushes cannot change a mex or a JP decision, so
+// results stay bit-identical to the row-scan engine (and to the oracle).  The cost moves
+// to the low-degree side -- one walk of a vertex's hin row when it is coloured (bitmaps)
+// and one when it wins (flags) -- instead of every hub re-reading its row every round.
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <rocprim/rocprim.hpp>
+
+#include "gc_device.h"
+#include "gc_engine.h"
+
+namespace {
+
+__global__ void k_hub_flag(const int* deg, long long n, int T, long long* f) {
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (long long)gridDim.x * blockDim.x)
+        f[v] = v < n && deg[v] > T ? 1 : 0;
+}
+
+__global__ void k_hub_ids(const int* deg, long long n, int T, const long long* pos, int* hid, int* hub_v) {
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
+        const bool h = deg[v] > T;
+        hid[v] = h ? (int)pos[v] : -1;
+        if (h) hub_v[pos[v]] = (int)v;
+    }
+}
+
+// one wave per hub row
+__global__ void k_hub_count(const long long* rp, const int* col, const int* hub_v, long long H, ull* cnt) {
+    const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
+    for (long long x = (long long)blockIdx.x * (blockDim.x / GC_WAVE) + threadIdx.x / GC_WAVE; x < H; x += waves) {
+        const int h = hub_v[x];
+        for (long long e = rp[h] + gc_lane(); e < rp[h + 1]; e += GC_WAVE) atomicAdd(&cnt[col[e]], 1ull);
+    }
+}
+
+__global__ void k_hub_fill(const long long* rp, const int* col, const int* hub_v, long long H, const long long* hin_rp,
+                           ull* cursor, int* hin_col) {
+    const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
+    for (long long x = (long long)blockIdx.x * (blockDim.x / GC_WAVE) + threadIdx.x / GC_WAVE; x < H; x += waves) {
+        const int h = hub_v[x];
+        for (long long e = rp[h] + gc_lane(); e < rp[h + 1]; e += GC_WAVE) {
+            const int u = col[e];
+            hin_col[hin_rp[u] + (long long)atomicAdd(&cursor[u], 1ull)] = (int)x;
+        }
+    }
+}
+
+// hub x's low row restricted to hubs: count, then fill (wave per hub, ballot compaction)
+__global__ void k_hlow_count(const long long* rp, const int* col, const int* nlow, const int* hid, const int* hub_v,
+                             long long H, long long* cnt) {
+    const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
+    for (long long x = (long long)blockIdx.x * (blockDim.x / GC_WAVE) + threadIdx.x / GC_WAVE; x < H; x += waves) {
+        const int h = hub_v[x];
+        long long k = 0;
+        for (long long e = rp[h] + gc_lane(); e < rp[h] + nlow[h]; e += GC_WAVE) k += hid[col[e]] >= 0;
+        k = gc_wave_sum(k);
+        if (gc_lane() == 0) cnt[x] = k;
+    }
+}
+
+__global__ void k_hlow_fill(const long long* rp, const int* col, const int* nlow, const int* hid, const int* hub_v,
+                            long long H, const long long* hlow_rp, int* hlow_col) {
+    const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
+    for (long long x = (long long)blockIdx.x * (blockDim.x / GC_WAVE) + threadIdx.x / GC_WAVE; x < H; x += waves) {
+        const int h = hub_v[x];
+        long long o = hlow_rp[x];
+        const long long e1 = rp[h] + nlow[h];
+        for (long long e0 = rp[h]; e0 < e1; e0 += GC_WAVE) {
+            const long long e = e0 + gc_lane();
+            const int u = e < e1 ? col[e] : 0;
+            const bool p = e < e1 && hid[u] >= 0;
+            const ull m = __ballot(p);
+            if (p) hlow_col[o + __popcll(m & gc_lanemask_lt())] = u;
+            o += __popcll(m);
+        }
+    }
+}
+
+int scan_ll(const long long* in, long long* out, long long count, hipStream_t s) {
+    size_t bytes = 0;
+    GC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s));
+    void* tmp = nullptr;
+    GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+    hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
+    hipStreamSynchronize(s);
+    hipFree(tmp);
+    GC_HIP(e);
+    return GC_OK;
+}
+
+int grid_of(long long items) {
+    return (int)std::max<long long>(1, std::min<long long>((items + GC_BLOCK - 1) / GC_BLOCK, 8192));
+}
+
+// threshold from GC_HUB_T ("off" or < 0 disables), default GC_HUB_T; GC_HUB_W sizes the
+// bitmaps (tests shrink it to reach the row-scan fallback)
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    if (!e || !*e) return dflt;
+    if (strcmp(e, "off") == 0) return -1;
+    return atoi(e);
+}
+
+int build(gc_graph* g, int T, int W) {
+    hipStream_t s = g->stream;
+    const long long n = g->n;
+    long long *pos = nullptr, *flag = nullptr;
+    GC_HIP(hipMalloc((void**)&pos, sizeof(long long) * (size_t)(n + 1)));
+    GC_HIP(hipMalloc((void**)&flag, sizeof(long long) * (size_t)(n + 1)));
+    hipLaunchKernelGGL(k_hub_flag, dim3(grid_of(n + 1)), dim3(GC_BLOCK), 0, s, g->deg, n, T, flag);
+    int rc = scan_ll(flag, pos, n + 1, s);
+    hipFree(flag);
+    long long H = 0;
+    if (!rc && hipMemcpy(&H, pos + n, sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess) rc = GC_EHIP;
+    if (rc || H == 0) {
+        hipFree(pos);
+        g->hub_t = T;
+        g->nhub = 0;
+        return rc;
+    }
+    // memory: hid/hub_v, the hub transpose (one entry per hub-row entry), bitmaps, blockers
+    size_t freeb = 0, totalb = 0;
+    hipMemGetInfo(&freeb, &totalb);
+    const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (20.0 + 4.0 * (W + GC_BLOCK)) * (double)H;
+    if (need > 0.5 * (double)freeb) {  // no room: row scans as before
+        hipFree(pos);
+        g->hub_t = T;
+        g->nhub = 0;
+        return GC_OK;
+    }
+    g->nhub = H;
+    GC_HIP(hipMalloc((void**)&g->hid, sizeof(int) * (size_t)std::max<long long>(n, 1)));
+    GC_HIP(hipMalloc((void**)&g->hub_v, sizeof(int) * (size_t)H));
+    hipLaunchKernelGGL(k_hub_ids, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, g->deg, n, T, pos, g->hid, g->hub_v);
+    // hub transpose: reuse pos as the per-target counter
+    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
+    const int hgrid = (int)std::max<long long>(1, std::min<long long>((H + 3) / 4, 8192));
+    hipLaunchKernelGGL(k_hub_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, (ull*)pos);
+    GC_HIP(hipMalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
+    if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { hipFree(pos); return rc; }
+    long long E = 0;
+    GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
+    hipMemGetInfo(&freeb, &totalb);
+    const double need2 = 4.0 * (double)E + (20.0 + 4.0 * (W + GC_BLOCK)) * (double)H;
+    if (need2 > 0.6 * (double)freeb) {
+        hipFree(pos);
+        gc_hubs_free(g);
+        g->hub_t = T;
+        g->nhub = 0;
+        return GC_OK;
+    }
+    GC_HIP(hipMalloc((void**)&g->hin_col, sizeof(int) * (size_t)std::max<long long>(E, 1)));
+    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
+    hipLaunchKernelGGL(k_hub_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, g->hin_rp,
+                       (ull*)pos, g->hin_col);
+    GC_HIP(hipMalloc((void**)&g->hbits, sizeof(unsigned) * (size_t)H * W));
+    GC_HIP(hipMalloc((void**)&g->hkill, sizeof(unsigned) * (size_t)H));
+    GC_HIP(hipMalloc((void**)&g->hcur, sizeof(int) * (size_t)H));
+    GC_HIP(hipMalloc((void**)&g->hpc, sizeof(int) * (size_t)H));
+    GC_HIP(hipMalloc((void**)&g->hpend, sizeof(int) * (size_t)H * GC_BLOCK));
+    // lower-rank hubs of each hub row (pos reused: H + 1 counts)
+    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
+    hipLaunchKernelGGL(k_hlow_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
+                       pos);
+    GC_HIP(hipMalloc((void**)&g->hlow_rp, sizeof(long long) * (size_t)(H + 1)));
+    if ((rc = scan_ll(pos, g->hlow_rp, H + 1, s))) { hipFree(pos); return rc; }
+    long long EL = 0;
+    GC_HIP(hipMemcpy(&EL, g->hlow_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_HIP(hipMalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
+                       g->hlow_rp, g->hlow_col);
+    GC_HIP(hipGetLastError());
+    GC_HIP(hipStreamSynchronize(s));
+    hipFree(pos);
+    g->hub_t = T;
+    g->hub_w = W;
+    return GC_OK;
+}
+
+}  // namespace
+
+void gc_hubs_free(gc_graph* g) {
+    void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
+                    g->hcur, g->hpc, g->hpend};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend = nullptr;
+    g->hin_rp = g->hlow_rp = nullptr;
+    g->hbits = g->hkill = nullptr;
+    g->nhub = 0;
+    g->hub_t = -1;
+}
+
+int gc_hubs_prepare(gc_graph* g, GDev& d) {
+    const int T = env_int("GC_HUB_T", GC_HUB_T);
+    const int W = std::max(1, env_int("GC_HUB_W", GC_HUB_W));
+    if (T < 0 || g->maxdeg <= T || g->borrowed) return GC_OK;
+    if (g->hub_t != T || (g->nhub && g->hub_w != W)) {
+        gc_hubs_free(g);
+        int rc = build(g, T, W);
+        if (rc) {
+            gc_hubs_free(g);
+            return rc;
+        }
+    }
+    if (g->nhub == 0) return GC_OK;
+    GC_HIP(hipMemsetAsync(g->hbits, 0, sizeof(unsigned) * (size_t)g->nhub * g->hub_w, g->stream));
+    d.heavy_t = T;
+    d.hub_w = g->hub_w;
+    d.hid = g->hid;
+    d.hub_v = g->hub_v;
+    d.hin_rp = g->hin_rp;
+    d.hin_col = g->hin_col;
+    d.hbits = g->hbits;
+    d.hkill = g->hkill;
+    d.hlow_rp = g->hlow_rp;
+    d.hlow_col = g->hlow_col;
+    d.hcur = g->hcur;
+    d.hpc = g->hpc;
+    d.hpend = g->hpend;
+    return GC_OK;
+}
+

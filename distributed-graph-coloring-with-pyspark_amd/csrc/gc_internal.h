@@ -30,6 +30,11 @@ typedef unsigned long long ull;
 #define GC_WAVES_PER_BLOCK (GC_BLOCK / GC_WAVE)
 // Vertices with deg > GC_HEAVY_T take the workgroup-per-vertex path.
 #define GC_HEAVY_T 2048
+// hubs (gc_hubs.hip): default threshold, bitmap words (4096 colours)
+#define GC_HUB_T 1024
+#define GC_HUB_W 128
+#define GC_HUB_NOT_STARTED (1ll << 40)
+#define GC_TAIL_HMAX_HUB 32  // tail sweeps may take this many hubs (their sweeps read short lists)
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
@@ -115,6 +120,8 @@ struct DevCtl {
     int pull_off;           // never pull the frontier (GC_NO_PULL: A/B measurements)
     int sorted;             // the current frontier list is in vertex order (built by k_front_*)
     int want_cround;        // commit records the round each vertex was coloured in
+    int pad1;
+    long long hub_start;    // hubs on: the sweep of this round that started the hubs' JP (the lights had converged)
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };

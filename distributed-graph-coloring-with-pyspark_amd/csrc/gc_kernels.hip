@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
-        const bool isheavy = d > GC_HEAVY_T;
+        const bool isheavy = d > g.heavy_t;
         gc_wave_append(isheavy, v, L.heavy, &c->heavy_cnt);
         const int de = isheavy ? 0 : d;
         s_mask[w][lane] = 0;
@@ -345,6 +345,26 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
         const int d = g.deg[v];
         const long long start = g.rp[v];
         long long mex = -1;
+        const int x = (g.hub_w && i < na) ? g.hid[v] : -1;
+        if (x >= 0) {
+            // hub (gc_hubs.hip): forbidden colours pushed by its neighbours' commits; clear
+            // its conflict flag for this round
+            if (threadIdx.x == 0) {
+                g.hkill[x] = 0u;
+                g.hcur[x] = 0;
+                g.hpc[x] = 0;
+                s_first = 0x7FFFFFFF;
+            }
+            __syncthreads();
+            if (maxc + 2 <= 32ll * g.hub_w) {  // mex <= maxcolor + 1: a zero bit lies in range
+                const unsigned* hb = g.hbits + (long long)x * g.hub_w;
+                for (int t = threadIdx.x; t < words; t += blockDim.x)
+                    if (~hb[t]) atomicMin(&s_first, t);
+                __syncthreads();
+                mex = 32ll * s_first + __builtin_ctz(~hb[s_first]);
+            }
+            __syncthreads();
+        }
         for (long long base = 0; mex < 0; base += 32ll * words) {
             for (int t = threadIdx.x; t < words; t += blockDim.x) s_bits[t] = 0;
             if (threadIdx.x == 0) s_first = 0x7FFFFFFF;
@@ -395,6 +415,61 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
     g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
 
+// JP step of hub x against the lower-rank hubs of its row (hlow), resumable across the
+// round's sweeps: hpend holds up to GC_BLOCK entries that were undecided with the hub's
+// candidate when last seen, hcur how far the row has been read (everything before it is
+// decided-not-IN or in hpend).  A sweep re-checks hpend, then reads on from hcur while
+// no winner turned up and the undecided entries still fit.  Returns 1 (OUT: a same-
+// candidate lower-rank hub is IN), 2 (undecided) or 0 (IN).  Whole workgroup, uniform.
+__device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
+    __shared__ int s_n, s_add;
+    __shared__ unsigned s_out;
+    const int t = threadIdx.x;
+    const unsigned char* __restrict__ k8 = g.k8;
+    int* pend = g.hpend + (long long)x * GC_BLOCK;
+    const int cnt = g.hpc[x];
+    if (t == 0) {
+        s_n = 0;
+        s_out = 0u;
+    }
+    __syncthreads();
+    {  // pending entries, compacted in place (all read before any is rewritten)
+        const int u = t < cnt ? pend[t] : -1;
+        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
+        if (fl & 1u) s_out = 1u;
+        __syncthreads();
+        if (fl == 2u) pend[atomicAdd(&s_n, 1)] = u;
+        __syncthreads();
+    }
+    const long long base = g.hlow_rp[x];
+    const int len = (int)(g.hlow_rp[x + 1] - base);
+    int cur = g.hcur[x];
+    while (!s_out && cur < len) {
+        const int e = cur + t;
+        const int u = e < len ? g.hlow_col[base + e] : -1;
+        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
+        if (t == 0) s_add = 0;
+        __syncthreads();
+        if (fl & 1u) s_out = 1u;
+        if (fl == 2u) atomicAdd(&s_add, 1);
+        __syncthreads();
+        const int n = s_n, add = s_add;
+        if (s_out || n + add > GC_BLOCK) break;  // winner found / no room: stop here
+        __syncthreads();
+        if (fl == 2u) pend[n + atomicAdd(&s_n, 1) - n] = u;
+        cur = cur + GC_BLOCK < len ? cur + GC_BLOCK : len;
+        __syncthreads();
+    }
+    const unsigned out = s_out;
+    const int n = s_n;
+    __syncthreads();
+    if (t == 0) {
+        g.hcur[x] = cur;
+        g.hpc[x] = n;
+    }
+    return out ? 1u : ((n > 0 || cur < len) ? 2u : 0u);
+}
+
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
 // undecided vertices are appended to (uo, uo_cnt) / (ho, ho_cnt).
 __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ list, long long cnt, int skip_heavy,
@@ -424,9 +499,15 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         if (threadIdx.x == 0) s_f = 0;
         __syncthreads();
         unsigned f = 0;
-        for (long long e = threadIdx.x; e < dl; e += blockDim.x) {
-            const int u = g.col[start + e];
-            f |= gc_jp_flag(g, u, k8[u], cv6, cv);
+        const int x = g.hub_w ? g.hid[v] : -1;
+        if (x >= 0) {  // hub (gc_hubs.hip): every light entry is decided; flagged = one won cv
+            if (g.hkill[x]) f = 1u;
+            else f = gc_hub_jp(g, x, cv6, cv);  // whole workgroup, same value on every thread
+        } else {
+            for (long long e = threadIdx.x; e < dl; e += blockDim.x) {
+                const int u = g.col[start + e];
+                f |= gc_jp_flag(g, u, k8[u], cv6, cv);
+            }
         }
         if (f) atomicOr(&s_f, f);
         __syncthreads();
@@ -449,7 +530,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
-        const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
+        const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
         const int dl = skip ? 0 : g.nlow[v];
         const unsigned kv = skip ? 0xFFu : (unsigned)k8[v];
         const unsigned cv6 = skip ? 0x100u : gc_k8_cand(kv);
@@ -481,6 +562,27 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         }
         if (dout) gc_wave_append64(nst != GC_JP_UND, gc_delta(v, (int)nst), dout, dcnt);
         gc_stage_push(st, pend, v, uo, uo_cnt);
+        if (g.hub_w) {  // a light winner flags the hubs listing it that propose its colour
+            int dh = 0;
+            long long hs = 0;
+            if (nst == GC_JP_IN) {
+                hs = g.hin_rp[v];
+                dh = (int)(g.hin_rp[v + 1] - hs);
+            }
+            gc_wave_sync();
+            s_start[w][lane] = hs;
+            const int hincl = gc_wave_incl_scan(dh);
+            const int hexcl = hincl - dh;
+            const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
+            gc_wave_sync();
+            gc_chunk_edges(
+                g.hin_col, s_start[w], hexcl, htotal, [&](int hx) { return (unsigned)k8[g.hub_v[hx]]; },
+                [&](int o, int hx, unsigned kh) {
+                    if (gc_k8_cand(kh) != s_c6[w][o]) return;
+                    if (s_c6[w][o] == GC_K8_BIG && g.cand[g.hub_v[hx]] != s_cv[w][o]) return;
+                    if (!g.hkill[hx]) g.hkill[hx] = 1u;
+                });
+        }
     }
     gc_stage_flush(st, uo, uo_cnt);
 }
@@ -513,7 +615,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
     }
     const int cur = c->cur;
     ull lsum = 0, lnv = 0;
-    gc_jp_sweep(g, L.F[cur], (long long)c->fcnt[cur], 1, L.heavy, (long long)c->heavy_cnt, L.undL[0],
+    // hubs sit out the sweeps until the lights have converged (gc_hubs.hip)
+    gc_jp_sweep(g, L.F[cur], (long long)c->fcnt[cur], 1, L.heavy, g.hub_w ? 0ll : (long long)c->heavy_cnt, L.undL[0],
                 &c->und_cnt[0], L.undH[0], &c->undh_cnt[0], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
     gc_block_add(&c->sumdeg[GC_K_RESOLVE], lsum, scratch);
@@ -527,16 +630,20 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     if (c->halt) return;
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
     const int in = (i - 1) % 3, out = i % 3, z = (i + 1) % 3;
-    const long long cl = (long long)c->und_cnt[in], ch = (long long)c->undh_cnt[in];
+    const long long cl = (long long)c->und_cnt[in];
+    long long ch = (long long)c->undh_cnt[in];
+    const int* hl = L.undH[in];
+    const bool hub_start = gc_hub_gate(g, c, i, cl, hl, ch, L);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         c->und_cnt[z] = 0;
         c->undh_cnt[z] = 0;
         if (cl + ch > 0) c->sweeps += 1;
-        if (cl > GC_TAIL_MAX || ch > GC_TAIL_HMAX) c->bigsweeps = i;
+        if (cl > GC_TAIL_MAX || ch > gc_tail_hmax(g)) c->bigsweeps = i;
+        if (hub_start) c->hub_start = i;
     }
     if (cl + ch == 0) return;
     ull lsum = 0, lnv = 0;
-    gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
+    gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                 &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
     gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
@@ -565,16 +672,21 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S
             s_ch = (long long)gc_aread(&c->undh_cnt[in]);
         }
         __syncthreads();
-        const long long cl = s_cl, ch = s_ch;
-        if (cl + ch == 0 || cl > GC_TAIL_MAX || ch > GC_TAIL_HMAX) break;
+        const long long cl = s_cl;
+        long long ch = s_ch;
+        const int* hl = L.undH[in];
+        const bool hub_start = gc_hub_gate(g, c, j + 1, cl, hl, ch, L);
+        if (cl + ch == 0 || cl > GC_TAIL_MAX || ch > gc_tail_hmax(g)) break;
         ++j;
         const int out = j % 3, z = (j + 1) % 3;  // out was cleared by the sweep before
+        __syncthreads();  // every thread has read hub_start before thread 0 moves it
         if (threadIdx.x == 0) {
             gc_st(&c->und_cnt[z], 0ull);
             gc_st(&c->undh_cnt[z], 0ull);
             gc_st(&c->sweeps, c->sweeps + 1);
+            if (hub_start) gc_st(&c->hub_start, (long long)j);
         }
-        gc_jp_sweep(g, L.undL[in], cl, 0, L.undH[in], ch, L.undL[out], &c->und_cnt[out], L.undH[out],
+        gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                     &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
         __syncthreads();
     }
@@ -659,6 +771,7 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->accepted, 0ull);
     gc_st(&c->maxmex, -1ll);
     gc_st(&c->sweeps, 0ll);
+    gc_st(&c->hub_start, GC_HUB_NOT_STARTED);
     for (int k = 0; k < 3; ++k) {
         gc_st(&c->und_cnt[k], 0ull);
         gc_st(&c->undh_cnt[k], 0ull);
@@ -699,13 +812,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     if (mode == GC_CM_ROUND && c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
-    __shared__ int s_acc;
+    __shared__ int s_acc, s_accc;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const long long last = mode == GC_CM_ROUND ? c->tail_last : nsweeps;  // k_sweep_tail ran before
     const int last_slot = (int)(last % 3);
-    if (mode == GC_CM_ROUND && (c->und_cnt[last_slot] | c->undh_cnt[last_slot])) {
+    if (mode == GC_CM_ROUND &&
+        ((c->und_cnt[last_slot] | c->undh_cnt[last_slot]) || (g.hub_w && c->heavy_cnt && c->hub_start > last))) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             c->sweeps_enq = last;
             c->halt = GC_H_SWEEPS;
@@ -739,6 +854,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             if (js == GC_JP_IN) {
                 const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
                 gc_commit_colour(g, v, cc);
+                s_accc = cc;
                 if (want_cround) g.cround[v] = round;
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
@@ -748,6 +864,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             }
         }
         __syncthreads();
+        if (s_acc && g.hub_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
         if (s_acc && (mark || !big)) {
             const long long ts = g.trp[v], te = g.trp[v + 1];
             for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
@@ -772,7 +889,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
-        const bool skip = v < 0 || (skip_heavy && d > GC_HEAVY_T);
+        const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
         const unsigned kv = skip ? 0u : (unsigned)g.k8[v];
         const unsigned js = skip ? (unsigned)GC_JP_UND : gc_k8_state(kv);
         const bool acc = js == GC_JP_IN;
@@ -808,6 +925,26 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 else claim = gc_claim(g.inF, x);
             }
             gc_stage_push(st, claim, x, next, next_cnt);
+        }
+        if (g.hub_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
+            int dh = 0;
+            if (acc) {
+                tstart = g.hin_rp[v];
+                dh = (int)(g.hin_rp[v + 1] - tstart);
+            }
+            gc_wave_sync();
+            s_start[w][lane] = tstart;
+            s_cc[w][lane] = cc;
+            const int hincl = gc_wave_incl_scan(dh);
+            const int hexcl = hincl - dh;
+            const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
+            gc_wave_sync();
+            for (int base = 0; base < htotal; base += GC_WAVE) {
+                const int e = base + lane;
+                const int o = gc_owner(hexcl, e);
+                const int eo = __shfl(hexcl, o, GC_WAVE);
+                if (e < htotal) gc_hub_mark(g, g.hin_col[s_start[w][o] + (e - eo)], s_cc[w][o]);
+            }
         }
         gc_wave_sync();
     }

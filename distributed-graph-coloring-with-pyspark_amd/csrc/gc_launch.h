@@ -22,6 +22,23 @@ struct GDev {
     unsigned int* inF;
     unsigned char* mark;  // big rounds: in-neighbours of the winners (0/1), merged into inF
     DevCtl* ctl;
+    // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
+    // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
+    // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
+    // list, both pushed to it, instead of re-reading its whole row every round / sweep.
+    int heavy_t;
+    int hub_w;                // words per hub bitmap (0 = hubs off)
+    const int* hid;           // hub index of v, -1 if v is no hub
+    const int* hub_v;         // vertex of hub index x
+    const long long* hin_rp;  // for every u: the hubs (indices) whose rows list u
+    const int* hin_col;
+    unsigned* hbits;          // hub x: bit c set <=> a listed neighbour is coloured c (c < 32*hub_w)
+    unsigned* hkill;          // hub x, this round: a lower-rank light neighbour it lists won its candidate
+    const long long* hlow_rp; // hub x: the lower-rank HUBS its row lists (vertex ids)
+    const int* hlow_col;
+    int* hcur;                // hub x, this round: hlow entries read so far (gc_hub_jp)
+    int* hpc;                 //   undecided same-candidate entries kept in hpend
+    int* hpend;               //   GC_BLOCK slots per hub
 };
 
 // Work lists of the round pipeline (counts live in DevCtl).

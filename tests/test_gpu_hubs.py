@@ -1,0 +1,111 @@
+"""GPU parity of the hub path (csrc/gc_hubs.hip) against the CPU oracle.
+
+Hubs keep pushed state instead of re-reading their rows: a forbidden-colour bitmap
+(colours of coloured listed neighbours) for assign_color's mex (coloring.py:44-54), and
+for resolve_collisions (coloring.py:56-70) a flag raised by light winners of the hub's
+candidate, after which the hub's Jones-Plassmann sweeps read only the lower-rank hubs it
+lists.  The threshold (GC_HUB_T) and the bitmap width (GC_HUB_W words) are shrunk here so
+that small graphs put most vertices on the hub path (hub-hub JP chains, light-only and
+hub-only rounds) and reach the row-scan fallback for colours past the bitmap.  Every run must match the oracle bit for
+bit: colours, per-round records, the round each vertex was coloured, bounded attempts.
+"""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import _dg, _random_directed, assert_same_run
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SETTINGS = [
+    {"GC_HUB_T": "0"},                                        # every vertex with a neighbour is a hub
+    {"GC_HUB_T": "2"},
+    {"GC_HUB_T": "5", "GC_HUB_W": "1"},                       # bitmap of 32 colours: mex fallback
+    {"GC_HUB_T": "3"},
+    {"GC_HUB_T": "16", "GC_HUB_W": "2"},
+    {"GC_HUB_T": "64"},
+    {"GC_HUB_T": "1024"},                                     # the default
+    {"GC_HUB_T": "off"},
+]
+IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T1024", "off"]
+
+
+@pytest.fixture(params=SETTINGS, ids=IDS)
+def hubenv(request, monkeypatch):
+    for k in ("GC_HUB_T", "GC_HUB_W"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def _check(rp, col, symmetric=False, bounded=True):
+    with _dg().from_csr(rp, col, symmetric=symmetric) as dg:
+        o = oracle.c_color(rp, col, "A")
+        g = dg.color("A")
+        assert_same_run(g, o)
+        assert tuple(dg.validate()) == tuple(oracle.c_validate(rp, col, o["colors"]))
+        if bounded:
+            top = int(o["max_color"])
+            for k in sorted({1, max(1, top // 2), top}):
+                assert_same_run(dg.color("A", num_colors=k), oracle.c_color(rp, col, "A", k=k))
+        return g
+
+
+def test_reference_generator_graphs(hubenv):
+    from gcolor_amd.generators import reference_csr
+    for s in (0, 1, 4):
+        rp, col = reference_csr(3000, 8, random.Random(s))
+        _check(rp, col, symmetric=True)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_directed_multigraphs(hubenv, seed):
+    rp, col = _random_directed(2000, 12000, seed)
+    _check(rp, col)
+
+
+@pytest.mark.parametrize("scale", [9, 12])
+def test_rmat(hubenv, scale):
+    with _dg().rmat(scale, 16, seed=scale + 3) as dg:
+        rp, col = dg.export()
+    _check(rp, col, symmetric=True, bounded=scale < 12)
+
+
+def test_clique_and_star(hubenv):
+    """A 150-clique (mex up to 149, past a 1-word bitmap) joined to a degree-3000 star."""
+    n = 150 + 3000
+    adj = [[] for _ in range(n)]
+    for i in range(150):
+        adj[i] = [j for j in range(150) if j != i]
+    for leaf in range(150, n):
+        adj[0].append(leaf)
+        adj[leaf].append(0)
+    for leaf in range(151, n, 5):
+        adj[leaf].append(leaf - 1)
+        adj[leaf - 1].append(leaf)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    _check(rp, col, bounded=False)
+
+
+def test_uniform_dense(hubenv):
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(20000, 40, 5)
+    _check(rp, col, symmetric=True, bounded=False)
+
+
+def test_threshold_change_rebuilds(monkeypatch):
+    """The same handle re-derives its hubs when the threshold changes between calls."""
+    with _dg().rmat(11, 16, seed=2) as dg:
+        rp, col = dg.export()
+        o = oracle.c_color(rp, col, "A")
+        for t in ("64", "4", "off", "0", "64"):
+            monkeypatch.setenv("GC_HUB_T", t)
+            assert_same_run(dg.color("A"), o)
