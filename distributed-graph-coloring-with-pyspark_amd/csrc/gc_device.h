@@ -34,6 +34,29 @@ __device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, cons
     }
 }
 
+// Same walk, apply(o, u, val, slot) also gets the slot's offset inside owner o's range.
+template <typename Load, typename Apply>
+__device__ __forceinline__ void gc_chunk_edges_at(const int* __restrict__ col, const long long* s_start, int excl,
+                                                  int total, Load load, Apply apply) {
+    const int lane = gc_lane();
+    for (int base = 0; base < total; base += 2 * GC_WAVE) {
+        const int e0 = base + lane, e1 = e0 + GC_WAVE;
+        const int o0 = gc_owner(excl, e0);
+        const int o1 = gc_owner(excl, e1);
+        const int x0 = __shfl(excl, o0, GC_WAVE);
+        const int x1 = __shfl(excl, o1, GC_WAVE);
+        const bool v0 = e0 < total, v1 = e1 < total;
+        int u0 = 0, u1 = 0;
+        if (v0) u0 = col[s_start[o0] + (e0 - x0)];
+        if (v1) u1 = col[s_start[o1] + (e1 - x1)];
+        decltype(load(0)) g0{}, g1{};
+        if (v0) g0 = load(u0);
+        if (v1) g1 = load(u1);
+        if (v0) apply(o0, u0, g0, e0 - x0);
+        if (v1) apply(o1, u1, g1, e1 - x1);
+    }
+}
+
 // colour of u from the byte mirror (-1 uncoloured)
 __device__ __forceinline__ int gc_colour(const GDev& g, int u) {
     const unsigned b = g.c8[u];

@@ -34,10 +34,12 @@ struct gc_graph {
     int* undL[3] = {nullptr, nullptr, nullptr};
     int* undH[3] = {nullptr, nullptr, nullptr};
     int* seeds[2] = {nullptr, nullptr};
+    int* bigw = nullptr;
     int* ulist = nullptr;
     int* parent = nullptr;
     ull* best = nullptr;
     int* vcolors = nullptr;
+    int* lcur = nullptr;       // JP resume points (gc_jp_sweep)
     // hubs (gc_hubs.hip), built on the first variant-A colouring that wants them
     int hub_t = -1;            // threshold they were built for (-1: none)
     int hub_w = 0;             // bitmap words per hub

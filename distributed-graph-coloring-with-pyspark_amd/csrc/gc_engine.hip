@@ -61,6 +61,7 @@ GDev gc_view(const gc_graph* g) {
     d.inF = g->inF;
     d.mark = g->mark;
     d.ctl = g->ctl;
+    d.lcur = g->lcur;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hid = nullptr;
@@ -89,6 +90,7 @@ GLists gc_lists(const gc_graph* g) {
     }
     L.seeds[0] = g->seeds[0];
     L.seeds[1] = g->seeds[1];
+    L.bigw = g->bigw;
     L.rec = g->rec;
     L.delta = nullptr;
     return L;
@@ -115,6 +117,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->color, n);
     A(g->cround, n);
     A(g->cand, n);
+    A(g->lcur, n);
     A(g->c8, n);
     A(g->c4, n / 8 + 2);
     A(g->k8, n);
@@ -130,6 +133,7 @@ int gc_alloc_run_state(gc_graph* g) {
     }
     A(g->seeds[0], n);
     A(g->seeds[1], n);
+    A(g->bigw, n);
     A(g->ulist, n);
     A(g->parent, n);
     A(g->best, n);

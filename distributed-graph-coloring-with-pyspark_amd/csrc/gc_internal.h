@@ -34,7 +34,8 @@ typedef unsigned long long ull;
 #define GC_HUB_T 1024
 #define GC_HUB_W 128
 #define GC_HUB_NOT_STARTED (1ll << 40)
-#define GC_TAIL_HMAX_HUB 32  // tail sweeps may take this many hubs (their sweeps read short lists)
+#define GC_TAIL_HMAX_HUB 32
+#define GC_BIGROW 4096       // a winner with longer in-rows is walked by the whole grid (k_commit_big)  // tail sweeps may take this many hubs (their sweeps read short lists)
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
@@ -106,6 +107,7 @@ struct DevCtl {
     ull list_cnt;      // E1: compacted uncoloured list
     ull ticket;        // (unused)
     ull dcnt;          // sharded: deltas written this phase
+    ull bigw_cnt;      // winners deferred to k_commit_big this commit
     long long sweeps;  // JP sweeps that found work in the current round (first included)
     long long sweep_total;  // sum over rounds of sweeps beyond the first
     long long maxdepth;     // max JP passes of a round (first sweep included)

@@ -416,58 +416,65 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 }
 
 // JP step of hub x against the lower-rank hubs of its row (hlow), resumable across the
-// round's sweeps: hpend holds up to GC_BLOCK entries that were undecided with the hub's
-// candidate when last seen, hcur how far the row has been read (everything before it is
-// decided-not-IN or in hpend).  A sweep re-checks hpend, then reads on from hcur while
-// no winner turned up and the undecided entries still fit.  Returns 1 (OUT: a same-
-// candidate lower-rank hub is IN), 2 (undecided) or 0 (IN).  Whole workgroup, uniform.
+// round's sweeps: hpend holds the entries that were undecided with the hub's candidate
+// when last seen and hcur how far the row has been read (everything before it is decided
+// not-IN or in hpend); more than GC_BLOCK such entries overflow (hpc = GC_HPC_OVF) and the
+// next sweep reads the row again.  One strided pass, four gathers in flight per thread.
+// Returns 1 (OUT: a same-candidate lower-rank hub is IN), 2 (undecided) or 0 (IN).
+// Whole workgroup; the value is the same on every thread.
+#define GC_HPC_OVF 0x7FFFFFFF
 __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
-    __shared__ int s_n, s_add;
+    __shared__ int s_n, s_ovf;
     __shared__ unsigned s_out;
     const int t = threadIdx.x;
     const unsigned char* __restrict__ k8 = g.k8;
     int* pend = g.hpend + (long long)x * GC_BLOCK;
     const int cnt = g.hpc[x];
+    const long long base = g.hlow_rp[x];
+    const int len = (int)(g.hlow_rp[x + 1] - base);
+    const int start = cnt == GC_HPC_OVF ? 0 : g.hcur[x];
     if (t == 0) {
         s_n = 0;
+        s_ovf = 0;
         s_out = 0u;
     }
     __syncthreads();
-    {  // pending entries, compacted in place (all read before any is rewritten)
-        const int u = t < cnt ? pend[t] : -1;
-        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
-        if (fl & 1u) s_out = 1u;
-        __syncthreads();
-        if (fl == 2u) pend[atomicAdd(&s_n, 1)] = u;
-        __syncthreads();
+    const int u0 = (cnt != GC_HPC_OVF && t < cnt) ? pend[t] : -1;
+    const unsigned f0 = u0 >= 0 ? gc_jp_flag(g, u0, k8[u0], cv6, cv) : 0u;
+    if (f0 & 1u) s_out = 1u;
+    __syncthreads();  // every kept entry read before the list is rewritten
+    auto keep = [&](int u) {
+        const int p = atomicAdd(&s_n, 1);
+        if (p < GC_BLOCK) pend[p] = u;
+        else s_ovf = 1;
+    };
+    if (f0 == 2u) keep(u0);
+    const int* __restrict__ hc = g.hlow_col + base;
+    for (int e = start + t; e < len && !s_out; e += 4 * GC_BLOCK) {
+        int u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
+        unsigned ku[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (u[k] < 0) continue;
+            const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
+            if (fl & 1u) s_out = 1u;
+            if (fl == 2u) keep(u[k]);
+        }
     }
-    const long long base = g.hlow_rp[x];
-    const int len = (int)(g.hlow_rp[x + 1] - base);
-    int cur = g.hcur[x];
-    while (!s_out && cur < len) {
-        const int e = cur + t;
-        const int u = e < len ? g.hlow_col[base + e] : -1;
-        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
-        if (t == 0) s_add = 0;
-        __syncthreads();
-        if (fl & 1u) s_out = 1u;
-        if (fl == 2u) atomicAdd(&s_add, 1);
-        __syncthreads();
-        const int n = s_n, add = s_add;
-        if (s_out || n + add > GC_BLOCK) break;  // winner found / no room: stop here
-        __syncthreads();
-        if (fl == 2u) pend[n + atomicAdd(&s_n, 1) - n] = u;
-        cur = cur + GC_BLOCK < len ? cur + GC_BLOCK : len;
-        __syncthreads();
-    }
+    __syncthreads();
     const unsigned out = s_out;
     const int n = s_n;
+    const bool ovf = s_ovf != 0;
     __syncthreads();
     if (t == 0) {
-        g.hcur[x] = cur;
-        g.hpc[x] = n;
+        g.hcur[x] = len;
+        g.hpc[x] = ovf ? GC_HPC_OVF : n;
     }
-    return out ? 1u : ((n > 0 || cur < len) ? 2u : 0u);
+    return out ? 1u : (n > 0 ? 2u : 0u);
 }
 
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
@@ -476,6 +483,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                                             const int* hlist, long long hcnt, int* uo, ull* uo_cnt, int* ho,
                                             ull* ho_cnt, ull& lsum, ull& lnv, long long* dout, ull* dcnt) {
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_first[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -487,7 +495,9 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     // undecided appends staged in LDS: one atomic per 512 entries, not one per wave-chunk
     // (a single counter takes ~88 returning atomics/us; 86k chunks cost ~1 ms)
     GcStage st{s_stage[w], 0};
-    // hubs first: one workgroup per vertex
+    // hubs first: one workgroup per vertex; undecided ones staged by wave 0 (LDS of its own)
+    __shared__ int s_hstage[GC_STAGE_CAP];
+    GcStage hst{s_hstage, 0};
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
         const int v = hlist[i];
         const int d = g.deg[v];
@@ -511,11 +521,11 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         }
         if (f) atomicOr(&s_f, f);
         __syncthreads();
+        const unsigned ff = s_f;
+        if (w == 0) gc_stage_push(hst, lane == 0 && (ff & 3u) == 2u, v, ho, ho_cnt);  // undecided hub
         if (threadIdx.x == 0) {
-            const unsigned ff = s_f;
             if (ff & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
-            else if (ff & 2u) ho[atomicAdd(ho_cnt, 1ull)] = v;
-            else gc_set_state(g, v, kv, GC_JP_IN);
+            else if (!(ff & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
             if (dout && ((ff & 1u) || !(ff & 2u)))
                 dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (ff & 1u) ? GC_JP_OUT : GC_JP_IN);
             lsum += (ull)d;
@@ -523,6 +533,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         }
         __syncthreads();
     }
+    if (w == 0) gc_stage_flush(hst, ho, ho_cnt);
     const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -531,22 +542,27 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
-        const int dl = skip ? 0 : g.nlow[v];
+        // resumable: entries before lcur[v] were seen decided-not-IN or off-candidate in an
+        // earlier sweep of this round (states only move UND -> IN/OUT), so skip them
+        const int lc = (skip || skip_heavy) ? 0 : g.lcur[v];
+        const int dl = skip ? 0 : g.nlow[v] - lc;
         const unsigned kv = skip ? 0xFFu : (unsigned)k8[v];
         const unsigned cv6 = skip ? 0x100u : gc_k8_cand(kv);
         s_flag[w][lane] = 0;
-        s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
+        s_first[w][lane] = 0x7FFFFFFF;
+        s_start[w][lane] = v >= 0 ? g.rp[v] + lc : 0;
         s_c6[w][lane] = cv6;
         s_cv[w][lane] = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
         const int incl = gc_wave_incl_scan(dl);
         const int excl = incl - dl;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        gc_chunk_edges(
+        gc_chunk_edges_at(
             g.col, s_start[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
-            [&](int o, int u, unsigned ku) {
+            [&](int o, int u, unsigned ku, int slot) {
                 const unsigned f = gc_jp_flag(g, u, ku, s_c6[w][o], s_cv[w][o]);
                 if (f) atomicOr(&s_flag[w][o], f);
+                if (f == 2u) atomicMin(&s_first[w][o], slot);
             });
         gc_wave_sync();
         bool pend = false;
@@ -556,6 +572,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             if (f & 1u) nst = GC_JP_OUT;
             else if (f & 2u) pend = true;
             else nst = GC_JP_IN;
+            if (pend) g.lcur[v] = lc + s_first[w][lane];
             if (nst != GC_JP_UND) gc_set_state(g, v, kv, nst);
             lsum += (ull)d;
             lnv++;
@@ -777,6 +794,7 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
         gc_st(&c->undh_cnt[k], 0ull);
     }
     gc_st(&c->seed_cnt[0], 0ull);
+    gc_st(&c->bigw_cnt, 0ull);
     gc_st(&c->seed_cnt[1], 0ull);
     gc_st(&c->ticket, 0ull);
     gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
@@ -814,7 +832,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[GC_WAVES_PER_BLOCK];
-    __shared__ int s_acc, s_accc;
+    __shared__ int s_acc, s_accc, s_lose;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const long long last = mode == GC_CM_ROUND ? c->tail_last : nsweeps;  // k_sweep_tail ran before
@@ -858,12 +876,17 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 if (want_cround) g.cround[v] = round;
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
+                const long long rows = (g.trp[v + 1] - g.trp[v]) + (g.hub_w ? g.hin_rp[v + 1] - g.hin_rp[v] : 0);
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
-            } else if (js == GC_JP_OUT && !big) {
-                next[atomicAdd(next_cnt, 1ull)] = v;
+                if (rows > GC_BIGROW) {  // the whole grid walks it (k_commit_big)
+                    L.bigw[atomicAdd(&c->bigw_cnt, 1ull)] = v;
+                    s_acc = 0;
+                }
             }
+            s_lose = js == GC_JP_OUT && !big;
         }
         __syncthreads();
+        if (w == 0) gc_stage_push(st, lane == 0 && s_lose, v, next, next_cnt);  // losers stay
         if (s_acc && g.hub_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
         if (s_acc && (mark || !big)) {
             const long long ts = g.trp[v], te = g.trp[v + 1];
@@ -954,6 +977,51 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     gc_block_add(&c->accepted, lacc, scratch);
     gc_block_add(&c->sumdeg[GC_K_COMMIT], lsum, scratch);
     gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
+}
+
+// Winners whose in-rows exceed GC_BIGROW, deferred by k_commit: every workgroup takes a
+// share of every such row (colour pushes into the hubs listing the winner, then the
+// frontier claims / marks of its in-neighbours), instead of one workgroup walking it.
+__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big) {
+    DevCtl* c = g.ctl;
+    if (mode == GC_CM_ROUND && c->halt) return;
+    const long long nb = (long long)c->bigw_cnt;
+    if (nb == 0) return;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    const int w = threadIdx.x / GC_WAVE;
+    const bool rnd = mode == GC_CM_ROUND || mode == GC_CM_SHARD;
+    const int cur = c->cur;
+    const int nxt = rnd ? cur ^ 1 : cur;
+    int* next = L.F[nxt];
+    ull* next_cnt = &c->fcnt[nxt];
+    const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);
+    const bool mark = big && !gc_pull_on(c);
+    GcStage st{s_stage[w], 0};
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long j = 0; j < nb; ++j) {
+        const int v = L.bigw[j];
+        if (g.hub_w) {
+            const int cc = gc_colour(g, v);
+            const long long h0 = g.hin_rp[v], h1 = g.hin_rp[v + 1];
+            for (long long e = h0 + (long long)blockIdx.x * blockDim.x + threadIdx.x; e < h1; e += stride)
+                gc_hub_mark(g, g.hin_col[e], cc);
+        }
+        if (mark || !big) {
+            const long long ts = g.trp[v], te = g.trp[v + 1];
+            for (long long e0 = ts + (long long)blockIdx.x * blockDim.x; e0 < te; e0 += stride) {
+                const long long e = e0 + threadIdx.x;
+                bool claim = false;
+                int x = 0;
+                if (e < te) {
+                    x = g.tcol[e];
+                    if (mark) g.mark[x] = 1;
+                    else claim = gc_claim(g.inF, x);
+                }
+                gc_stage_push(st, claim, x, next, next_cnt);
+            }
+        }
+    }
+    gc_stage_flush(st, next, next_cnt);
 }
 
 // Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
@@ -1168,6 +1236,7 @@ __global__ void k_shard_reset(GDev g, long long round) {
     c->maxmex = -1;
     c->sweeps = 0;
     c->dcnt = 0;
+    c->bigw_cnt = 0;
     c->list_cnt = 0;
     c->seed_cnt[0] = 0;
     c->seed_cnt[1] = 0;
@@ -1514,6 +1583,7 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big) {
     hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+    hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

@@ -22,6 +22,7 @@ struct GDev {
     unsigned int* inF;
     unsigned char* mark;  // big rounds: in-neighbours of the winners (0/1), merged into inF
     DevCtl* ctl;
+    int* lcur;            // undecided light vertex: low-row entries a later JP sweep may skip
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
@@ -49,6 +50,7 @@ struct GLists {
     int* undL[3];
     int* undH[3];
     int* seeds[2];
+    int* bigw;  // winners with long in-rows (k_commit_big)
     RoundRec* rec;
     long long* delta;  // sharded engine: this phase's outgoing (vertex, value) deltas; else null
 };
