@@ -54,7 +54,7 @@ struct gc_graph {
     int* hlow_col = nullptr;
     int* hcur = nullptr;
     int* hpc = nullptr;
-    int* hpend = nullptr;
+    int* hpend[2] = {nullptr, nullptr};
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;

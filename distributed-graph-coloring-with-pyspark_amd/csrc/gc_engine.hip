@@ -74,7 +74,7 @@ GDev gc_view(const gc_graph* g) {
     d.hlow_col = nullptr;
     d.hcur = nullptr;
     d.hpc = nullptr;
-    d.hpend = nullptr;
+    d.hpend[0] = d.hpend[1] = nullptr;
     return d;
 }
 

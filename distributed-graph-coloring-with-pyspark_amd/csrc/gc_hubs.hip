@@ -145,7 +145,7 @@ int build(gc_graph* g, int T, int W) {
     // memory: hid/hub_v, the hub transpose (one entry per hub-row entry), bitmaps, blockers
     size_t freeb = 0, totalb = 0;
     hipMemGetInfo(&freeb, &totalb);
-    const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (20.0 + 4.0 * (W + GC_BLOCK)) * (double)H;
+    const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (20.0 + 4.0 * W) * (double)H;
     if (need > 0.5 * (double)freeb) {  // no room: row scans as before
         hipFree(pos);
         g->hub_t = T;
@@ -165,7 +165,7 @@ int build(gc_graph* g, int T, int W) {
     long long E = 0;
     GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
     hipMemGetInfo(&freeb, &totalb);
-    const double need2 = 4.0 * (double)E + (20.0 + 4.0 * (W + GC_BLOCK)) * (double)H;
+    const double need2 = 4.0 * (double)E + (20.0 + 4.0 * W) * (double)H;
     if (need2 > 0.6 * (double)freeb) {
         hipFree(pos);
         gc_hubs_free(g);
@@ -181,7 +181,7 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMalloc((void**)&g->hkill, sizeof(unsigned) * (size_t)H));
     GC_HIP(hipMalloc((void**)&g->hcur, sizeof(int) * (size_t)H));
     GC_HIP(hipMalloc((void**)&g->hpc, sizeof(int) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hpend, sizeof(int) * (size_t)H * GC_BLOCK));
+
     // lower-rank hubs of each hub row (pos reused: H + 1 counts)
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
     hipLaunchKernelGGL(k_hlow_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
@@ -191,6 +191,8 @@ int build(gc_graph* g, int T, int W) {
     long long EL = 0;
     GC_HIP(hipMemcpy(&EL, g->hlow_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
     GC_HIP(hipMalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(hipMalloc((void**)&g->hpend[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(hipMalloc((void**)&g->hpend[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
     hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
                        g->hlow_rp, g->hlow_col);
     GC_HIP(hipGetLastError());
@@ -205,10 +207,10 @@ int build(gc_graph* g, int T, int W) {
 
 void gc_hubs_free(gc_graph* g) {
     void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
-                    g->hcur, g->hpc, g->hpend};
+                    g->hcur, g->hpc, g->hpend[0], g->hpend[1]};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend = nullptr;
+    g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
     g->hin_rp = g->hlow_rp = nullptr;
     g->hbits = g->hkill = nullptr;
     g->nhub = 0;
@@ -241,7 +243,8 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hlow_col = g->hlow_col;
     d.hcur = g->hcur;
     d.hpc = g->hpc;
-    d.hpend = g->hpend;
+    d.hpend[0] = g->hpend[0];
+    d.hpend[1] = g->hpend[1];
     return GC_OK;
 }
 

@@ -416,41 +416,37 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 }
 
 // JP step of hub x against the lower-rank hubs of its row (hlow), resumable across the
-// round's sweeps: hpend holds the entries that were undecided with the hub's candidate
-// when last seen and hcur how far the row has been read (everything before it is decided
-// not-IN or in hpend); more than GC_BLOCK such entries overflow (hpc = GC_HPC_OVF) and the
-// next sweep reads the row again.  One strided pass, four gathers in flight per thread.
-// Returns 1 (OUT: a same-candidate lower-rank hub is IN), 2 (undecided) or 0 (IN).
-// Whole workgroup; the value is the same on every thread.
-#define GC_HPC_OVF 0x7FFFFFFF
+// round's sweeps: hcur says how far the row has been read; every entry before it is
+// decided not-IN, or still undecided with the hub's candidate and then kept in the hub's
+// pending list.  A sweep re-checks the pending list (ping-pong halves hpend[0|1], same
+// offsets as hlow, so it never overflows), then reads the rest of the row -- only the
+// first hub sweep of a round does -- with four gathers in flight per thread.
+// hpc[x] = pending count << 1 | current half.  Returns 1 (OUT: a same-candidate
+// lower-rank hub is IN), 2 (undecided) or 0 (IN); whole workgroup, same value everywhere.
 __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
-    __shared__ int s_n, s_ovf;
+    __shared__ int s_n;
     __shared__ unsigned s_out;
     const int t = threadIdx.x;
     const unsigned char* __restrict__ k8 = g.k8;
-    int* pend = g.hpend + (long long)x * GC_BLOCK;
-    const int cnt = g.hpc[x];
+    const int enc = g.hpc[x];
+    const int sel = enc & 1, cnt = enc >> 1;
     const long long base = g.hlow_rp[x];
     const int len = (int)(g.hlow_rp[x + 1] - base);
-    const int start = cnt == GC_HPC_OVF ? 0 : g.hcur[x];
+    const int* __restrict__ src = g.hpend[sel] + base;
+    int* dst = g.hpend[sel ^ 1] + base;
     if (t == 0) {
         s_n = 0;
-        s_ovf = 0;
         s_out = 0u;
     }
     __syncthreads();
-    const int u0 = (cnt != GC_HPC_OVF && t < cnt) ? pend[t] : -1;
-    const unsigned f0 = u0 >= 0 ? gc_jp_flag(g, u0, k8[u0], cv6, cv) : 0u;
-    if (f0 & 1u) s_out = 1u;
-    __syncthreads();  // every kept entry read before the list is rewritten
-    auto keep = [&](int u) {
-        const int p = atomicAdd(&s_n, 1);
-        if (p < GC_BLOCK) pend[p] = u;
-        else s_ovf = 1;
-    };
-    if (f0 == 2u) keep(u0);
+    for (int i = t; i < cnt && !s_out; i += GC_BLOCK) {
+        const int u = src[i];
+        const unsigned fl = gc_jp_flag(g, u, k8[u], cv6, cv);
+        if (fl & 1u) s_out = 1u;
+        if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u;
+    }
     const int* __restrict__ hc = g.hlow_col + base;
-    for (int e = start + t; e < len && !s_out; e += 4 * GC_BLOCK) {
+    for (int e = g.hcur[x] + t; e < len && !s_out; e += 4 * GC_BLOCK) {
         int u[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
@@ -462,17 +458,16 @@ __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
             if (u[k] < 0) continue;
             const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
             if (fl & 1u) s_out = 1u;
-            if (fl == 2u) keep(u[k]);
+            if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
         }
     }
     __syncthreads();
     const unsigned out = s_out;
     const int n = s_n;
-    const bool ovf = s_ovf != 0;
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && !out) {  // an OUT hub is final: its list is not read again this round
         g.hcur[x] = len;
-        g.hpc[x] = ovf ? GC_HPC_OVF : n;
+        g.hpc[x] = (n << 1) | (sel ^ 1);
     }
     return out ? 1u : (n > 0 ? 2u : 0u);
 }

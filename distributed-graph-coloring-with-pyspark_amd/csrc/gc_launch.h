@@ -38,8 +38,8 @@ struct GDev {
     const long long* hlow_rp; // hub x: the lower-rank HUBS its row lists (vertex ids)
     const int* hlow_col;
     int* hcur;                // hub x, this round: hlow entries read so far (gc_hub_jp)
-    int* hpc;                 //   undecided same-candidate entries kept in hpend
-    int* hpend;               //   GC_BLOCK slots per hub
+    int* hpc;                 //   undecided same-candidate entries kept in hpend (count << 1 | half)
+    int* hpend[2];            //   ping-pong halves, hlow's offsets
 };
 
 // Work lists of the round pipeline (counts live in DevCtl).
