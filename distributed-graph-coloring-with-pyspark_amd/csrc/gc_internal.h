@@ -39,7 +39,7 @@ typedef unsigned long long ull;
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
-#define GC_ROUND_GRID 2048
+#define GC_ROUND_GRID 1024
 #define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
 #define GC_BLOCK_GRID 1024

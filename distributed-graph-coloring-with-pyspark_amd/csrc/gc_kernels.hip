@@ -24,6 +24,8 @@
 // at a time (two slots in flight per lane), so consecutive lanes read consecutive col[]
 // entries and no lane idles on a short row.  All of it is HBM/L2-bound gather work; no
 // MFMA involved.
+#include <stdlib.h>
+
 #include "gcolor.h"
 #include "gc_internal.h"
 #include "gc_launch.h"
@@ -1534,20 +1536,32 @@ void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t
     hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 1);
     hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 1);
 }
+// Grids of the gather-heavy round kernels (workgroups; they grid-stride over device
+// counts).  Their waves spend ~80% of their cycles waiting on gathers (SQ_WAIT_ANY), so
+// the grid sets how many are in flight; GC_GRID_{P,R,C} override for measurements.
+static int round_grid(const char* env, int dflt) {
+    const char* e = getenv(env);
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : dflt;
+}
+static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
+static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
+static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
+
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
 }
 void gcl_propose(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
+    hipLaunchKernelGGL(k_propose, dim3(kGridP), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(GC_BLOCK_GRID), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
+    hipLaunchKernelGGL(k_resolve, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, i);
+    hipLaunchKernelGGL(k_sweep, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L, i);
 }
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
@@ -1577,7 +1591,7 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big) {
-    hipLaunchKernelGGL(k_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+    hipLaunchKernelGGL(k_commit, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
     hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
