@@ -62,6 +62,7 @@ GDev gc_view(const gc_graph* g) {
     d.mark = g->mark;
     d.ctl = g->ctl;
     d.lcur = g->lcur;
+    d.bstat = g->bstat;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hid = nullptr;
@@ -118,6 +119,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->cround, n);
     A(g->cand, n);
     A(g->lcur, n);
+    A(g->bstat, (size_t)GC_STAT_SLOTS * 16);
     A(g->c8, n);
     A(g->c4, n / 8 + 2);
     A(g->k8, n);
@@ -348,6 +350,7 @@ struct Run {
         h.want_cround = cround_out != nullptr;
         h.pull_off = getenv("GC_NO_PULL") ? 1 : 0;
         GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, s));
+        GC_HIP(hipMemsetAsync(g->bstat, 0, sizeof(ull) * GC_STAT_SLOTS * 16, s));
         GC_HIP(hipEventRecord(g->ev0, s));
         // init + seed (coloring.py:74-76)
         kt.begin(GC_K_INIT);
@@ -415,6 +418,7 @@ struct Run {
         }
         kt.begin(GC_K_OTHER);
         gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
+        gcl_stat_reduce(d, s);
         kt.end();
         GC_HIP(hipEventRecord(g->ev1, s));
         if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));

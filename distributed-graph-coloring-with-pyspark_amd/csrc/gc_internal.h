@@ -43,6 +43,7 @@ typedef unsigned long long ull;
 #define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
 #define GC_BLOCK_GRID 1024
+#define GC_STAT_SLOTS 256  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
 // dynamic LDS words of the workgroup-per-vertex mex bitmap (128 Ki colours per window)
 #define GC_MEX_WORDS 4096
 
@@ -255,6 +256,7 @@ __device__ __forceinline__ void gc_block_add(ull* dst, ull v, ull* lds_scratch) 
     __syncthreads();
 }
 
+// (reads first: the running max settles quickly, so most workgroups skip the atomic)
 __device__ __forceinline__ void gc_block_max(long long* dst, long long v, long long* lds_scratch) {
     v = gc_wave_max(v);
     const int w = threadIdx.x / GC_WAVE;
@@ -263,7 +265,7 @@ __device__ __forceinline__ void gc_block_max(long long* dst, long long v, long l
     if (threadIdx.x == 0) {
         long long t = lds_scratch[0];
         for (int i = 1; i < (int)(blockDim.x / GC_WAVE); ++i) t = lds_scratch[i] > t ? lds_scratch[i] : t;
-        if (t >= 0) atomicMax(dst, t);
+        if (t >= 0 && t > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(dst, t);
     }
     __syncthreads();
 }

@@ -39,7 +39,7 @@
 // Isolated vertices are coloured at init; when some OTHER vertex lists one of them
 // (asymmetric input) it must push like a committed vertex, so it joins the seed list.
 __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     ull best = 0, unc = 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_fsort_count(GDev g, unsigned* bsum
     const bool on = c->fsort_all ? true : (gc_resort_on(g, c) && !c->sorted);
     if (blockIdx.x == 0 && threadIdx.x == 0) c->resort = on ? 1 : 0;
     if (!on) return;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long words = ((long long)g.n + 31) / 32;
     const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
     ull cnt = w < words ? (ull)__popc(gc_front_word(g, w)) : 0ull;
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     if (c->halt) return;
     __shared__ ull s_mask[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int cur = c->cur;
@@ -321,8 +321,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     __syncthreads();
     gc_block_max(&c->maxmex, lmax, (long long*)scratch);
     gc_block_add(&c->failcnt, lfail, scratch);
-    gc_block_add(&c->sumdeg[GC_K_PROPOSE], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_PROPOSE], lnv, scratch);
+    gc_stat_add(g, GC_K_PROPOSE, lsum, lnv, scratch);
 }
 
 // One workgroup per vertex: hubs (deg > GC_HEAVY_T) and light vertices whose mex >= 64.
@@ -333,7 +332,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
     if (c->halt) return;
     extern __shared__ __attribute__((aligned(16))) unsigned s_bits[];
     __shared__ int s_first;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long na = (long long)c->heavy_cnt, nb = (long long)c->wide_cnt;
     if (na + nb == 0) return;
     const long long kbound = c->kbound;
@@ -393,8 +392,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
     __syncthreads();
     gc_block_max(&c->maxmex, lmax, (long long*)scratch);
     gc_block_add(&c->failcnt, lfail, scratch);
-    gc_block_add(&c->sumdeg[GC_K_PROPOSE], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_PROPOSE], lnv, scratch);
+    gc_stat_add(g, GC_K_PROPOSE, lsum, lnv, scratch);
 }
 
 // ------------------------------------------------------------------------------------
@@ -604,7 +602,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
 __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     if (c->kbound >= 0 && c->failcnt > 0) {  // coloring.py:104-108: fail with the round-start state
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             const long long r = c->round;
@@ -633,8 +631,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
     gc_jp_sweep(g, L.F[cur], (long long)c->fcnt[cur], 1, L.heavy, g.hub_w ? 0ll : (long long)c->heavy_cnt, L.undL[0],
                 &c->und_cnt[0], L.undH[0], &c->undh_cnt[0], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
-    gc_block_add(&c->sumdeg[GC_K_RESOLVE], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_RESOLVE], lnv, scratch);
+    gc_stat_add(g, GC_K_RESOLVE, lsum, lnv, scratch);
 }
 
 // Sweep i >= 1 reads slot (i-1)%3, appends to slot i%3 and clears slot (i+1)%3, which
@@ -642,7 +639,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
 __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int in = (i - 1) % 3, out = i % 3, z = (i + 1) % 3;
     const long long cl = (long long)c->und_cnt[in];
     long long ch = (long long)c->undh_cnt[in];
@@ -660,8 +657,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                 &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
     __syncthreads();
-    gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
+    gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
 }
 
 // The rest of a round's sweeps in ONE workgroup, after the host's S full-grid sweeps: the
@@ -675,7 +671,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
 __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ long long s_cl, s_ch;
     int j = S;
     ull lsum = 0, lnv = 0;
@@ -705,8 +701,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S
         __syncthreads();
     }
     if (threadIdx.x == 0) gc_st(&c->tail_last, (long long)j);
-    gc_block_add(&c->sumdeg[GC_K_SWEEP], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_SWEEP], lnv, scratch);
+    gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
 }
 
 // ------------------------------------------------------------------------------------
@@ -828,7 +823,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ int s_acc, s_accc, s_lose;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
@@ -972,8 +967,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     gc_block_add(&c->accepted, lacc, scratch);
-    gc_block_add(&c->sumdeg[GC_K_COMMIT], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
+    gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
 // Winners whose in-rows exceed GC_BIGROW, deferred by k_commit: every workgroup takes a
@@ -1055,7 +1049,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_pull(GDev g, int allow_big) {
 __global__ void __launch_bounds__(GC_BLOCK) k_front_count(GDev g, unsigned* bsum) {
     DevCtl* c = g.ctl;
     if (!gc_front_on(g, c, 1)) return;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long words = ((long long)g.n + 31) / 32;
     const long long w = (long long)blockIdx.x * GC_BLOCK + threadIdx.x;
     ull cnt = 0;
@@ -1153,7 +1147,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
     DevCtl* c = g.ctl;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int nxt = c->cur ^ 1;
@@ -1361,7 +1355,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_seeds(GDev g, const int* list, 
 __global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __restrict__ colors) {
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_c[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     ull unc = 0, conf = 0;
@@ -1547,6 +1541,20 @@ static int round_grid(const char* env, int dflt) {
 static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
 static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
+
+// per-slot stats -> DevCtl.sumdeg / nvert (one workgroup; before the host reads them)
+__global__ void k_stat_reduce(GDev g) {
+    const int t = threadIdx.x;
+    if (t < 16) {
+        ull a = 0;
+        for (int k = 0; k < GC_STAT_SLOTS; ++k) a += g.bstat[k * 16 + t];
+        if (t < 8) g.ctl->sumdeg[t] = a;
+        else g.ctl->nvert[t - 8] = a;
+    }
+}
+void gcl_stat_reduce(const GDev& g, hipStream_t s) {
+    hipLaunchKernelGGL(k_stat_reduce, dim3(1), dim3(64), 0, s, g);
+}
 
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);

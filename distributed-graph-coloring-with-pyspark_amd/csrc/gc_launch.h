@@ -23,6 +23,7 @@ struct GDev {
     unsigned char* mark;  // big rounds: in-neighbours of the winners (0/1), merged into inF
     DevCtl* ctl;
     int* lcur;            // undecided light vertex: low-row entries a later JP sweep may skip
+    ull* bstat;           // GC_STAT_SLOTS x 16 stats slots (gc_stat_add)
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
@@ -60,6 +61,7 @@ void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s);
 int gcl_fsort_blocks(long long n);
 void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);
 void gcl_pack_c4(const GDev& g, hipStream_t s);
+void gcl_stat_reduce(const GDev& g, hipStream_t s);
 void gcl_propose(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);

@@ -70,7 +70,7 @@ __global__ void k_b_reset(GDev g, long long round) {
 // (coloring_optimized.py:159-164); k_propose counted every proposer.
 __global__ void __launch_bounds__(GC_BLOCK) k_b_fail0(GDev g, GLists L) {
     DevCtl* c = g.ctl;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     ull lf = 0;
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, GLists L, int* ev) {
     __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int* __restrict__ list = L.F[c->cur];
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, GLists L, const int*
     __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int* __restrict__ list = L.F[c->cur];
@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, GLists L, const int*
 // winners: admitted and never evicted, coloured (coloring_optimized.py:129-140)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev) {
     DevCtl* c = g.ctl;
-    __shared__ ull scratch[GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     const int round = (int)(c->round + 1);
@@ -228,8 +228,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     gc_block_add(&c->accepted, lacc, scratch);
-    gc_block_add(&c->sumdeg[GC_K_COMMIT], lsum, scratch);
-    gc_block_add(&c->nvert[GC_K_COMMIT], lacc, scratch);
+    gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
 struct RunB {
@@ -265,6 +264,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     h.fail_round = -1;
     h.want_cround = cround_out != nullptr;
     GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, s));
+    GC_HIP(hipMemsetAsync(g->bstat, 0, sizeof(ull) * GC_STAT_SLOTS * 16, s));
     GC_HIP(hipEventRecord(g->ev0, s));
     // init + seed (coloring_optimized.py:70-80 == coloring.py:12-35)
     gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), s);
@@ -326,6 +326,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         sweeps_total += passes;
     }
     gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
+    gcl_stat_reduce(d, s);
     GC_HIP(hipEventRecord(g->ev1, s));
     if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
     if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
