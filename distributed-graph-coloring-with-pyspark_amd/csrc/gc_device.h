@@ -9,52 +9,42 @@
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ long long gc_nchunks(long long cnt, int vpw) { return (cnt + vpw - 1) / vpw; }
 
-// Iterate the edge slots [0, total) of a wave chunk, two 64-slot groups per step so each
-// lane has two independent col[] -> gather chains in flight.  load(u) returns the
-// gathered value; apply(o, u, val) consumes it for owner lane o.
-template <typename Load, typename Apply>
-__device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, const long long* s_start, int excl,
-                                               int total, Load load, Apply apply) {
-    const int lane = gc_lane();
-    for (int base = 0; base < total; base += 2 * GC_WAVE) {
-        const int e0 = base + lane, e1 = e0 + GC_WAVE;
-        const int o0 = gc_owner(excl, e0);
-        const int o1 = gc_owner(excl, e1);
-        const int x0 = __shfl(excl, o0, GC_WAVE);
-        const int x1 = __shfl(excl, o1, GC_WAVE);
-        const bool v0 = e0 < total, v1 = e1 < total;
-        int u0 = 0, u1 = 0;
-        if (v0) u0 = col[s_start[o0] + (e0 - x0)];
-        if (v1) u1 = col[s_start[o1] + (e1 - x1)];
-        decltype(load(0)) g0{}, g1{};
-        if (v0) g0 = load(u0);
-        if (v1) g1 = load(u1);
-        if (v0) apply(o0, u0, g0);
-        if (v1) apply(o1, u1, g1);
-    }
-}
-
-// Same walk, apply(o, u, val, slot) also gets the slot's offset inside owner o's range.
+// Iterate the edge slots [0, total) of a wave chunk, GC_SLOTS 64-slot groups per step so
+// each lane has GC_SLOTS independent col[] -> gather chains in flight (the waves spend most
+// of their cycles waiting on these gathers).  load(u) returns the gathered value;
+// apply(o, u, val, slot) consumes it for owner lane o (slot = offset in o's range).
+#ifndef GC_SLOTS
+#define GC_SLOTS 2
+#endif
 template <typename Load, typename Apply>
 __device__ __forceinline__ void gc_chunk_edges_at(const int* __restrict__ col, const long long* s_start, int excl,
                                                   int total, Load load, Apply apply) {
     const int lane = gc_lane();
-    for (int base = 0; base < total; base += 2 * GC_WAVE) {
-        const int e0 = base + lane, e1 = e0 + GC_WAVE;
-        const int o0 = gc_owner(excl, e0);
-        const int o1 = gc_owner(excl, e1);
-        const int x0 = __shfl(excl, o0, GC_WAVE);
-        const int x1 = __shfl(excl, o1, GC_WAVE);
-        const bool v0 = e0 < total, v1 = e1 < total;
-        int u0 = 0, u1 = 0;
-        if (v0) u0 = col[s_start[o0] + (e0 - x0)];
-        if (v1) u1 = col[s_start[o1] + (e1 - x1)];
-        decltype(load(0)) g0{}, g1{};
-        if (v0) g0 = load(u0);
-        if (v1) g1 = load(u1);
-        if (v0) apply(o0, u0, g0, e0 - x0);
-        if (v1) apply(o1, u1, g1, e1 - x1);
+    for (int base = 0; base < total; base += GC_SLOTS * GC_WAVE) {
+        int o[GC_SLOTS], x[GC_SLOTS], u[GC_SLOTS];
+        bool ok[GC_SLOTS];
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) {
+            const int e = base + k * GC_WAVE + lane;
+            o[k] = gc_owner(excl, e);
+            x[k] = e - __shfl(excl, o[k], GC_WAVE);
+            ok[k] = e < total;
+        }
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) u[k] = ok[k] ? col[s_start[o[k]] + x[k]] : 0;
+        decltype(load(0)) gv[GC_SLOTS];
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) gv[k] = ok[k] ? load(u[k]) : decltype(load(0)){};
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k)
+            if (ok[k]) apply(o[k], u[k], gv[k], x[k]);
     }
+}
+
+template <typename Load, typename Apply>
+__device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, const long long* s_start, int excl,
+                                               int total, Load load, Apply apply) {
+    gc_chunk_edges_at(col, s_start, excl, total, load, [&](int o, int u, decltype(load(0)) v, int) { apply(o, u, v); });
 }
 
 // colour of u from the byte mirror (-1 uncoloured)
