@@ -56,6 +56,9 @@ struct gc_graph {
     int* hcur = nullptr;
     int* hpc = nullptr;
     int* hpend[2] = {nullptr, nullptr};
+    int* hrow = nullptr;
+    int* hlen = nullptr;
+    int* hlow2[2] = {nullptr, nullptr};
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;

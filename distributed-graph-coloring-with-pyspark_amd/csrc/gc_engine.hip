@@ -76,6 +76,8 @@ GDev gc_view(const gc_graph* g) {
     d.hcur = nullptr;
     d.hpc = nullptr;
     d.hpend[0] = d.hpend[1] = nullptr;
+    d.hrow = d.hlen = nullptr;
+    d.hlowb[0] = d.hlowb[1] = d.hlowb[2] = nullptr;
     return d;
 }
 

@@ -145,7 +145,7 @@ int build(gc_graph* g, int T, int W) {
     // memory: hid/hub_v, the hub transpose (one entry per hub-row entry), bitmaps, blockers
     size_t freeb = 0, totalb = 0;
     hipMemGetInfo(&freeb, &totalb);
-    const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (20.0 + 4.0 * W) * (double)H;
+    const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (28.0 + 4.0 * W) * (double)H;
     if (need > 0.5 * (double)freeb) {  // no room: row scans as before
         hipFree(pos);
         g->hub_t = T;
@@ -165,7 +165,7 @@ int build(gc_graph* g, int T, int W) {
     long long E = 0;
     GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
     hipMemGetInfo(&freeb, &totalb);
-    const double need2 = 4.0 * (double)E + (20.0 + 4.0 * W) * (double)H;
+    const double need2 = 24.0 * (double)E + (28.0 + 4.0 * W) * (double)H;  // hin + hlow copies <= 5 E
     if (need2 > 0.6 * (double)freeb) {
         hipFree(pos);
         gc_hubs_free(g);
@@ -193,6 +193,10 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
     GC_HIP(hipMalloc((void**)&g->hpend[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
     GC_HIP(hipMalloc((void**)&g->hpend[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(hipMalloc((void**)&g->hlow2[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(hipMalloc((void**)&g->hlow2[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(hipMalloc((void**)&g->hrow, sizeof(int) * (size_t)H));
+    GC_HIP(hipMalloc((void**)&g->hlen, sizeof(int) * (size_t)H));
     hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
                        g->hlow_rp, g->hlow_col);
     GC_HIP(hipGetLastError());
@@ -207,10 +211,11 @@ int build(gc_graph* g, int T, int W) {
 
 void gc_hubs_free(gc_graph* g) {
     void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
-                    g->hcur, g->hpc, g->hpend[0], g->hpend[1]};
+                    g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen};
     for (void* p : ptrs)
         if (p) hipFree(p);
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
+    g->hlow2[0] = g->hlow2[1] = g->hrow = g->hlen = nullptr;
     g->hin_rp = g->hlow_rp = nullptr;
     g->hbits = g->hkill = nullptr;
     g->nhub = 0;
@@ -245,6 +250,12 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hpc = g->hpc;
     d.hpend[0] = g->hpend[0];
     d.hpend[1] = g->hpend[1];
+    d.hrow = g->hrow;
+    d.hlen = g->hlen;
+    d.hlowb[0] = g->hlow_col;
+    d.hlowb[1] = g->hlow2[0];
+    d.hlowb[2] = g->hlow2[1];
+    GC_HIP(hipMemsetAsync(g->hrow, 0, sizeof(int) * (size_t)g->nhub, g->stream));  // full rows again
     return GC_OK;
 }
 

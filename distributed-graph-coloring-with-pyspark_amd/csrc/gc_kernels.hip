@@ -415,27 +415,30 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
     g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
 
-// JP step of hub x against the lower-rank hubs of its row (hlow), resumable across the
-// round's sweeps: hcur says how far the row has been read; every entry before it is
-// decided not-IN, or still undecided with the hub's candidate and then kept in the hub's
-// pending list.  A sweep re-checks the pending list (ping-pong halves hpend[0|1], same
-// offsets as hlow, so it never overflows), then reads the rest of the row -- only the
-// first hub sweep of a round does -- with four gathers in flight per thread.
-// hpc[x] = pending count << 1 | current half.  Returns 1 (OUT: a same-candidate
-// lower-rank hub is IN), 2 (undecided) or 0 (IN); whole workgroup, same value everywhere.
+// JP step of hub x against the lower-rank hubs of its row (hlow).  The first evaluation
+// of a round reads the whole row: undecided entries with the hub's candidate go to its
+// pending list, and the entries not yet coloured are copied to the next working copy of
+// the row (colours are final, so a coloured entry never matters again: the rows of the
+// hubs that linger shrink round by round).  Later sweeps of the round re-check only the
+// pending list (ping-pong halves hpend[0|1], hlow's offsets, never overflow).
+// hpc[x] = pending count << 1 | current half; hcur[x] = 1 once the row was read this round;
+// hrow[x] = which copy holds the live row (0: the original hlow_col), hlen[x] its length.
+// Returns 1 (OUT: a same-candidate lower-rank hub is IN), 2 (undecided) or 0 (IN); whole
+// workgroup, same value everywhere.
 __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
-    __shared__ int s_n;
+    __shared__ int s_n, s_k;
     __shared__ unsigned s_out;
     const int t = threadIdx.x;
     const unsigned char* __restrict__ k8 = g.k8;
     const int enc = g.hpc[x];
     const int sel = enc & 1, cnt = enc >> 1;
     const long long base = g.hlow_rp[x];
-    const int len = (int)(g.hlow_rp[x + 1] - base);
     const int* __restrict__ src = g.hpend[sel] + base;
     int* dst = g.hpend[sel ^ 1] + base;
+    const bool first = g.hcur[x] == 0;
     if (t == 0) {
         s_n = 0;
+        s_k = 0;
         s_out = 0u;
     }
     __syncthreads();
@@ -445,29 +448,43 @@ __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
         if (fl & 1u) s_out = 1u;
         if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u;
     }
-    const int* __restrict__ hc = g.hlow_col + base;
-    for (int e = g.hcur[x] + t; e < len && !s_out; e += 4 * GC_BLOCK) {
-        int u[4];
+    const int hr = first ? g.hrow[x] : 0;
+    if (first) {
+        const int len = hr ? g.hlen[x] : (int)(g.hlow_rp[x + 1] - base);
+        const int* __restrict__ hc = g.hlowb[hr] + base;
+        int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
+        const unsigned char* __restrict__ c8 = g.c8;
+        for (int e = t; e < len; e += 4 * GC_BLOCK) {
+            int u[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
-        unsigned ku[4];
+            for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
+            unsigned ku[4], cu[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
+            for (int k = 0; k < 4; ++k) {
+                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
+                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
+            }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (u[k] < 0) continue;
-            const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
-            if (fl & 1u) s_out = 1u;
-            if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
+            for (int k = 0; k < 4; ++k) {
+                if (u[k] < 0 || cu[k] != GC_C8_NONE) continue;  // coloured: dropped for good
+                keep[atomicAdd(&s_k, 1)] = u[k];
+                const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
+                if (fl & 1u) s_out = 1u;
+                if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
+            }
         }
     }
     __syncthreads();
     const unsigned out = s_out;
     const int n = s_n;
     __syncthreads();
-    if (t == 0 && !out) {  // an OUT hub is final: its list is not read again this round
-        g.hcur[x] = len;
-        g.hpc[x] = (n << 1) | (sel ^ 1);
+    if (t == 0) {
+        if (first) {  // the kept copy is complete (the whole row was read)
+            g.hrow[x] = hr == 1 ? 2 : 1;
+            g.hlen[x] = s_k;
+            g.hcur[x] = 1;
+        }
+        if (!out) g.hpc[x] = (n << 1) | (sel ^ 1);
     }
     return out ? 1u : (n > 0 ? 2u : 0u);
 }

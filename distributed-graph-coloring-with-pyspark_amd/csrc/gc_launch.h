@@ -38,7 +38,10 @@ struct GDev {
     unsigned* hkill;          // hub x, this round: a lower-rank light neighbour it lists won its candidate
     const long long* hlow_rp; // hub x: the lower-rank HUBS its row lists (vertex ids)
     const int* hlow_col;
-    int* hcur;                // hub x, this round: hlow entries read so far (gc_hub_jp)
+    int* hcur;                // hub x, this round: 1 once its row was read (gc_hub_jp)
+    int* hrow;                // hub x: which copy holds its live row (0 = hlow_col)
+    int* hlen;                //   and its length (copies 1, 2)
+    int* hlowb[3];            // hlow_col and two working copies (hlow's offsets)
     int* hpc;                 //   undecided same-candidate entries kept in hpend (count << 1 | half)
     int* hpend[2];            //   ping-pong halves, hlow's offsets
 };
