@@ -507,7 +507,7 @@ extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolore
     }
     GC_HIP(hipMemsetAsync(&g->ctl->uncolored, 0, sizeof(ull), g->stream));
     GC_HIP(hipMemsetAsync(&g->ctl->conflicts, 0, sizeof(ull), g->stream));
-    gcl_validate(gc_view(g), src, gc_grid_for_waves(g->n), g->stream);
+    gcl_validate(gc_view(g), src, g->heavy, gc_grid_for_waves(g->n), g->stream);
     GC_HIP(hipGetLastError());
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));

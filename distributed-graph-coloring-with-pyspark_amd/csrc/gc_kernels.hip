@@ -1369,7 +1369,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_seeds(GDev g, const int* list, 
 // ------------------------------------------------------------------------------------
 // validate_graph_coloring counts (coloring.py:149-162)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __restrict__ colors) {
+// Rows longer than GC_HEAVY_T are left to k_validate_heavy (listed in `heavy`): one wave
+// walking a 10^5-entry hub row would hold the whole launch.
+__global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __restrict__ colors, int* heavy) {
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_c[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
@@ -1381,7 +1383,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __rest
          chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long v = chunk * GC_WAVE + lane;
         const bool valid = v < g.n;
-        const int d = valid ? g.deg[v] : 0;
+        const int dv = valid ? g.deg[v] : 0;
+        gc_wave_append(dv > GC_HEAVY_T, (int)v, heavy, &g.ctl->list_cnt);
+        const int d = dv > GC_HEAVY_T ? 0 : dv;
         const int cv = valid ? colors[v] : 0;
         if (valid && cv == -1) unc++;
         s_start[w][lane] = valid ? g.rp[v] : 0;
@@ -1399,6 +1403,23 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __rest
     }
     __syncthreads();
     gc_block_add(&g.ctl->uncolored, unc, scratch);
+    gc_block_add(&g.ctl->conflicts, conf, scratch);
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_validate_heavy(GDev g, const int* __restrict__ colors,
+                                                             const int* heavy) {
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    const long long nh = (long long)g.ctl->list_cnt;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    ull conf = 0;
+    for (long long j = 0; j < nh; ++j) {
+        const int v = heavy[j];
+        const int cv = colors[v];
+        const long long e1 = g.rp[v + 1];
+        for (long long e = g.rp[v] + (long long)blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += stride)
+            conf += colors[g.col[e]] == cv;
+    }
+    __syncthreads();
     gc_block_add(&g.ctl->conflicts, conf, scratch);
 }
 
@@ -1632,8 +1653,10 @@ void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, c
                   int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best, sl, sh);
 }
-void gcl_validate(const GDev& g, const int* colors, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors);
+void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStream_t s) {
+    hipMemsetAsync(&g.ctl->list_cnt, 0, sizeof(ull), s);
+    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, heavy);
+    hipLaunchKernelGGL(k_validate_heavy, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, colors, (const int*)heavy);
 }
 void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, deg, n, nlow);

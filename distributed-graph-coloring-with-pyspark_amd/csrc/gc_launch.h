@@ -89,5 +89,5 @@ void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, in
 void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, const ull* best, int* sl, int* sh,
                   int grid, hipStream_t s);
-void gcl_validate(const GDev& g, const int* colors, int grid, hipStream_t s);
+void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStream_t s);
 void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s);
