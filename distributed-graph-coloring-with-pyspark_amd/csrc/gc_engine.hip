@@ -297,9 +297,10 @@ struct Run {
     }
     // sweeps to enqueue per round from the depths seen so far: none while every round
     // was decided by the first sweep (meshes), else twice the last round's depth
-    static int pick_sweeps(const DevCtl& h) {
+    const int sweep_pad = getenv("GC_SWEEP_PAD") ? atoi(getenv("GC_SWEEP_PAD")) : 2;
+    int pick_sweeps(const DevCtl& h) const {
         if (h.maxdepth <= 1) return 0;
-        return (int)std::min<long long>(64, h.lastbig + 2);  // the small-list tail runs in k_sweep_tail
+        return (int)std::min<long long>(64, h.lastbig + sweep_pad);  // the small-list tail runs in k_sweep_tail
     }
     // rounds per batch: small while the frontier is tiny or the colouring is nearly done
     static int pick_batch(const DevCtl& h, long long n, int prev) {
