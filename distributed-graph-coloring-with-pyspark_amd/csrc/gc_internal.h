@@ -206,6 +206,31 @@ __device__ __forceinline__ void gc_stage_flush(GcStage& s, int* out, ull* out_cn
     s.cnt = 0;
 }
 
+// End-of-kernel flush for the whole workgroup (every thread calls): one global atomic per
+// workgroup instead of one per wave -- thousands of waves each returning a handful of
+// entries on one counter cost ~10 us per 1000 atomics.
+__device__ __forceinline__ void gc_stage_flush_block(GcStage& s, int* out, ull* out_cnt) {
+    __shared__ int s_cnt[GC_WAVES_PER_BLOCK];
+    __shared__ ull s_base;
+    const int w = threadIdx.x / GC_WAVE;
+    gc_wave_sync();
+    if (gc_lane() == 0) s_cnt[w] = s.cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += s_cnt[i];
+        s_base = t ? atomicAdd(out_cnt, (ull)t) : 0ull;
+    }
+    __syncthreads();
+    ull base = s_base;
+    for (int i = 0; i < w; ++i) base += (ull)s_cnt[i];
+#pragma unroll 1
+    for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+    gc_wave_sync();
+    s.cnt = 0;
+    __syncthreads();
+}
+
 // All 64 lanes must call; pred per lane.
 __device__ __forceinline__ void gc_stage_push(GcStage& s, bool pred, int val, int* out, ull* out_cnt) {
     const ull m = __ballot(pred);

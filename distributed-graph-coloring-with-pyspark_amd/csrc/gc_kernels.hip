@@ -613,7 +613,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                 });
         }
     }
-    gc_stage_flush(st, uo, uo_cnt);
+    gc_stage_flush_block(st, uo, uo_cnt);
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
@@ -980,7 +980,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         }
         gc_wave_sync();
     }
-    gc_stage_flush(st, next, next_cnt);
+    gc_stage_flush_block(st, next, next_cnt);
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     gc_block_add(&c->accepted, lacc, scratch);
@@ -1029,7 +1029,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
             }
         }
     }
-    gc_stage_flush(st, next, next_cnt);
+    gc_stage_flush_block(st, next, next_cnt);
 }
 
 // Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
@@ -1225,7 +1225,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
             gc_wave_sync();
         }
     }
-    gc_stage_flush(st, next, next_cnt);
+    gc_stage_flush_block(st, next, next_cnt);
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     gc_block_add(&c->accepted, lacc, scratch);
