@@ -41,6 +41,7 @@ struct gc_graph {
     int* vcolors = nullptr;
     int* lcur = nullptr;       // JP resume points (gc_jp_sweep)
     ull* bstat = nullptr;      // stats slots (gc_stat_add)
+    ull* accs = nullptr;       // winner-count slots (k_commit -> k_close)
     // hubs (gc_hubs.hip), built on the first variant-A colouring that wants them
     int hub_t = -1;            // threshold they were built for (-1: none)
     int hub_w = 0;             // bitmap words per hub

@@ -63,6 +63,7 @@ GDev gc_view(const gc_graph* g) {
     d.ctl = g->ctl;
     d.lcur = g->lcur;
     d.bstat = g->bstat;
+    d.accs = nullptr;  // the single-GPU variant-A engine turns it on (Run)
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hid = nullptr;
@@ -122,6 +123,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->cand, n);
     A(g->lcur, n);
     A(g->bstat, (size_t)GC_STAT_SLOTS * 16);
+    A(g->accs, (size_t)GC_ACC_SLOTS);
     A(g->c8, n);
     A(g->c4, n / 8 + 2);
     A(g->k8, n);
@@ -486,6 +488,8 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
     if ((rc = gc_hubs_prepare(g, run.d))) return rc;
+    run.d.accs = g->accs;
+    GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
     rc = run.go(colors_out, cround_out);
     if (rc < 0) return rc;
     if (stats && stats->round_cap < (long long)run.recs.size() && (stats->round_U || stats->round_F)) {

@@ -43,7 +43,8 @@ typedef unsigned long long ull;
 #define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
 #define GC_BLOCK_GRID 1024
-#define GC_STAT_SLOTS 256  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
+#define GC_STAT_SLOTS 256
+#define GC_ACC_SLOTS 256   // commit's winner count, summed by k_close  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
 // dynamic LDS words of the workgroup-per-vertex mex bitmap (128 Ki colours per window)
 #define GC_MEX_WORDS 4096
 

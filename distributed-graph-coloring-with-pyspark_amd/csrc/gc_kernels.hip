@@ -983,7 +983,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     gc_stage_flush_block(st, next, next_cnt);
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
-    gc_block_add(&c->accepted, lacc, scratch);
+    if (g.accs) {  // slotted (k_close sums them): 1024 workgroups on one counter cost ~10 us
+        const ull wacc = gc_wave_sum(lacc);
+        if (gc_lane() == 0 && wacc) atomicAdd(&g.accs[(blockIdx.x * GC_WAVES_PER_BLOCK + w) % GC_ACC_SLOTS], wacc);
+    } else {
+        gc_block_add(&c->accepted, lacc, scratch);
+    }
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
@@ -1106,6 +1111,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_front_count(GDev g, unsigned* bsum
 __global__ void k_close(GDev g, GLists L, int mode, int allow_big) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
+    if (g.accs && blockIdx.x == 0 && threadIdx.x < GC_WAVE) {  // the commit's slotted winner counts
+        ull a = 0;
+        for (int k = threadIdx.x; k < GC_ACC_SLOTS; k += GC_WAVE) {
+            a += g.accs[k];
+            g.accs[k] = 0ull;
+        }
+        a = gc_wave_sum(a);
+        if (threadIdx.x == 0 && a) atomicAdd(&c->accepted, a);
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
         gc_close_round(L, c, mode);

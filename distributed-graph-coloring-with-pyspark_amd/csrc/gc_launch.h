@@ -24,6 +24,7 @@ struct GDev {
     DevCtl* ctl;
     int* lcur;            // undecided light vertex: low-row entries a later JP sweep may skip
     ull* bstat;           // GC_STAT_SLOTS x 16 stats slots (gc_stat_add)
+    ull* accs;            // GC_ACC_SLOTS winner-count slots (single-GPU engine), else null
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
