@@ -64,6 +64,7 @@ GDev gc_view(const gc_graph* g) {
     d.lcur = g->lcur;
     d.bstat = g->bstat;
     d.accs = nullptr;  // the single-GPU variant-A engine turns it on (Run)
+    d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= GC_BIGROW);
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hid = nullptr;
@@ -205,6 +206,8 @@ struct Run {
     long long drained = 0;       // absolute index of the first record not yet drained
     bool debug = getenv("GC_DEBUG") != nullptr;
     bool resort_hint = false;    // enqueue the frontier re-sort kernels (last snapshot's frontier >= n/256)
+    bool c4_hint = true;         // enqueue k_pack_c4 (last snapshot's frontier >= n/64, colours < 14)
+    const int batch_max = getenv("GC_BATCH_MAX") ? atoi(getenv("GC_BATCH_MAX")) : 4;
 
     int sync_ctl() {
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
@@ -275,9 +278,11 @@ struct Run {
             gcl_fsort(d, L, g->fsum, s);
             kt.end();
         }
-        kt.begin(GC_K_OTHER);
-        gcl_pack_c4(d, s);
-        kt.end();
+        if (c4_hint) {  // the nibble mirror can only pay in a big round (k_pack_c4 decides)
+            kt.begin(GC_K_OTHER);
+            gcl_pack_c4(d, s);
+            kt.end();
+        }
         kt.begin(GC_K_PROPOSE);
         gcl_propose(d, L, s);
         kt.end();
@@ -305,10 +310,11 @@ struct Run {
         return (int)std::min<long long>(64, h.lastbig + sweep_pad);  // the small-list tail runs in k_sweep_tail
     }
     // rounds per batch: small while the frontier is tiny or the colouring is nearly done
-    static int pick_batch(const DevCtl& h, long long n, int prev) {
+    int pick_batch(const DevCtl& h, long long n, int prev) const {
         if (h.U * 64 < n) return 1;
-        return std::min(prev * 2, 4);
+        return std::min(prev * 2, std::max(1, batch_max));
     }
+    static bool pick_c4(const DevCtl& h, long long n) { return (long long)h.fcnt[h.cur] * 64 >= n && h.maxcolor < 14; }
 
     // E1: every component of the uncoloured-induced subgraph gets its
     // argmax-(deg, pos) vertex as a colour-0 seed; committed like a round's winners.
@@ -381,6 +387,7 @@ struct Run {
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
                 S = pick_sweeps(sn);
                 resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
+                c4_hint = pick_c4(sn, g->n);
                 batch = pick_batch(sn, g->n, batch);
                 slot ^= 1;
             }
@@ -400,6 +407,7 @@ struct Run {
             }
             S = pick_sweeps(h);
             resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
+            c4_hint = pick_c4(h, g->n);
             batch = pick_batch(h, g->n, 1);
             if (halt == GC_RUN) continue;
             if (halt == GC_H_DONE || halt == GC_H_FAILED || halt == GC_H_STALLED) break;

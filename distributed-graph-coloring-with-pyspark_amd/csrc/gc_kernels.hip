@@ -804,6 +804,7 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     }
     gc_st(&c->seed_cnt[0], 0ull);
     gc_st(&c->bigw_cnt, 0ull);
+    gc_st(&c->use_c4, 0);  // k_pack_c4 (when the host enqueues it) turns it on for its round
     gc_st(&c->seed_cnt[1], 0ull);
     gc_st(&c->ticket, 0ull);
     gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
@@ -1652,7 +1653,8 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big) {
     hipLaunchKernelGGL(k_commit, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
-    hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
+    if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
+        hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

@@ -25,6 +25,7 @@ struct GDev {
     int* lcur;            // undecided light vertex: low-row entries a later JP sweep may skip
     ull* bstat;           // GC_STAT_SLOTS x 16 stats slots (gc_stat_add)
     ull* accs;            // GC_ACC_SLOTS winner-count slots (single-GPU engine), else null
+    int big_rows;         // some in-row (+ hub row) may exceed GC_BIGROW: k_commit_big is needed
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
