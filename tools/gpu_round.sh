@@ -1,7 +1,8 @@
 set -euo pipefail
-bash tools/gpu_profile.sh r01_v5
-mkdir -p gpurun_out/r01_v5/wl
+TAG=${1:-r01_v6}
+bash tools/gpu_profile.sh $TAG
+mkdir -p gpurun_out/$TAG/wl
 for w in rmat24 rmat26 mesh512 mesh256; do
-  timeout -k 10 280 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --json-out gpurun_out/r01_v5/wl/bench_$w.json > gpurun_out/r01_v5/wl/bench_$w.log 2>&1
-  tail -1 gpurun_out/r01_v5/wl/bench_$w.log | cut -c1-250
+  timeout -k 10 280 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --json-out gpurun_out/$TAG/wl/bench_$w.json > gpurun_out/$TAG/wl/bench_$w.log 2>&1
+  tail -1 gpurun_out/$TAG/wl/bench_$w.log | cut -c1-250
 done
