@@ -64,7 +64,8 @@ GDev gc_view(const gc_graph* g) {
     d.lcur = g->lcur;
     d.bstat = g->bstat;
     d.accs = nullptr;  // the single-GPU variant-A engine turns it on (Run)
-    d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= GC_BIGROW);
+    d.bigrow = getenv("GC_BIGROW") ? atoi(getenv("GC_BIGROW")) : GC_BIGROW;  // env: tests / tuning
+    d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= d.bigrow);
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hid = nullptr;

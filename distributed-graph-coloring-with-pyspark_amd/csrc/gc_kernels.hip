@@ -415,6 +415,17 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
     g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
 
+// Wave-aggregated append through an LDS counter (all 64 lanes call; pred per lane).
+__device__ __forceinline__ void gc_lds_append(bool pred, int val, int* out, int* lds_cnt) {
+    const ull m = __ballot(pred);
+    if (m == 0) return;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (gc_lane() == leader) base = atomicAdd(lds_cnt, __popcll(m));
+    base = __shfl(base, leader, GC_WAVE);
+    if (pred) out[base + __popcll(m & gc_lanemask_lt())] = val;
+}
+
 // JP step of hub x against the lower-rank hubs of its row (hlow).  The first evaluation
 // of a round reads the whole row: undecided entries with the hub's candidate go to its
 // pending list, and the entries not yet coloured are copied to the next working copy of
@@ -454,23 +465,28 @@ __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
         const int* __restrict__ hc = g.hlowb[hr] + base;
         int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
         const unsigned char* __restrict__ c8 = g.c8;
-        for (int e = t; e < len; e += 4 * GC_BLOCK) {
-            int u[4];
+        // 8 entries per thread in flight (one workgroup walks a row of up to ~10^6 hubs, so the
+        // walk is latency-bound); appends are wave-aggregated (one LDS atomic per wave)
+        for (int e0 = 0; e0 < len; e0 += 8 * GC_BLOCK) {
+            int u[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
-            unsigned ku[4], cu[4];
+            for (int k = 0; k < 8; ++k) {
+                const int e = e0 + t + k * GC_BLOCK;
+                u[k] = e < len ? hc[e] : -1;
+            }
+            unsigned ku[8], cu[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 8; ++k) {
                 ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
                 cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (u[k] < 0 || cu[k] != GC_C8_NONE) continue;  // coloured: dropped for good
-                keep[atomicAdd(&s_k, 1)] = u[k];
-                const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
+            for (int k = 0; k < 8; ++k) {
+                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
+                const unsigned fl = live ? gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;
                 if (fl & 1u) s_out = 1u;
-                if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
+                gc_lds_append(live, u[k], keep, &s_k);
+                gc_lds_append(fl == 2u, u[k], dst, &s_n);
             }
         }
     }
@@ -888,7 +904,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 lacc++;
                 const long long rows = (g.trp[v + 1] - g.trp[v]) + (g.hub_w ? g.hin_rp[v + 1] - g.hin_rp[v] : 0);
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
-                if (rows > GC_BIGROW) {  // the whole grid walks it (k_commit_big)
+                if (rows > g.bigrow) {  // the whole grid walks it (k_commit_big)
                     L.bigw[atomicAdd(&c->bigw_cnt, 1ull)] = v;
                     s_acc = 0;
                 }
@@ -993,16 +1009,25 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
-// Winners whose in-rows exceed GC_BIGROW, deferred by k_commit: every workgroup takes a
-// share of every such row (colour pushes into the hubs listing the winner, then the
-// frontier claims / marks of its in-neighbours), instead of one workgroup walking it.
+// Winners whose in-rows exceed bigrow (GC_BIGROW), deferred by k_commit: the grid walks the
+// concatenation of every such winner's rows (colour pushes into the hubs listing the
+// winner, then the frontier claims / marks of its in-neighbours) as one flat index space,
+// 256 winners per tile (their row offsets prefix-summed in LDS, owner by binary search).
+// Walking the winners one after another cost ~5 dependent memory round trips per winner
+// on every workgroup: 1.8 ms for the ~400 hub winners of an R-MAT-26 round.
 __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
     const long long nb = (long long)c->bigw_cnt;
     if (nb == 0) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
-    const int w = threadIdx.x / GC_WAVE;
+    __shared__ long long s_off[GC_BLOCK + 1];  // exclusive prefix of the tile's per-winner work
+    __shared__ long long s_hs[GC_BLOCK], s_ts[GC_BLOCK];
+    __shared__ int s_hl[GC_BLOCK], s_cc[GC_BLOCK];
+    __shared__ long long s_wsum[GC_WAVES_PER_BLOCK];
+    const int t = threadIdx.x;
+    const int lane = gc_lane();
+    const int w = t / GC_WAVE;
     const bool rnd = mode == GC_CM_ROUND || mode == GC_CM_SHARD;
     const int cur = c->cur;
     const int nxt = rnd ? cur ^ 1 : cur;
@@ -1010,30 +1035,59 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
     ull* next_cnt = &c->fcnt[nxt];
     const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);
     const bool mark = big && !gc_pull_on(c);
+    const bool walk_t = mark || !big;
     GcStage st{s_stage[w], 0};
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long j = 0; j < nb; ++j) {
-        const int v = L.bigw[j];
-        if (g.hub_w) {
-            const int cc = gc_colour(g, v);
-            const long long h0 = g.hin_rp[v], h1 = g.hin_rp[v + 1];
-            for (long long e = h0 + (long long)blockIdx.x * blockDim.x + threadIdx.x; e < h1; e += stride)
-                gc_hub_mark(g, g.hin_col[e], cc);
-        }
-        if (mark || !big) {
-            const long long ts = g.trp[v], te = g.trp[v + 1];
-            for (long long e0 = ts + (long long)blockIdx.x * blockDim.x; e0 < te; e0 += stride) {
-                const long long e = e0 + threadIdx.x;
-                bool claim = false;
-                int x = 0;
-                if (e < te) {
-                    x = g.tcol[e];
-                    if (mark) g.mark[x] = 1;
-                    else claim = gc_claim(g.inF, x);
-                }
-                gc_stage_push(st, claim, x, next, next_cnt);
+    for (long long j0 = 0; j0 < nb; j0 += GC_BLOCK) {
+        const int tn = (int)(nb - j0 < GC_BLOCK ? nb - j0 : GC_BLOCK);
+        long long len = 0;
+        if (t < tn) {
+            const int v = L.bigw[j0 + t];
+            int hl = 0;
+            if (g.hub_w) {
+                s_hs[t] = g.hin_rp[v];
+                hl = (int)(g.hin_rp[v + 1] - s_hs[t]);
+                s_cc[t] = gc_colour(g, v);
             }
+            s_hl[t] = hl;
+            s_ts[t] = g.trp[v];
+            len = hl + (walk_t ? g.trp[v + 1] - s_ts[t] : 0ll);
         }
+        // workgroup inclusive scan of len
+        long long x = len;
+#pragma unroll
+        for (int o = 1; o < GC_WAVE; o <<= 1) {
+            const long long y = __shfl_up(x, o, GC_WAVE);
+            if (lane >= o) x += y;
+        }
+        if (lane == GC_WAVE - 1) s_wsum[w] = x;
+        __syncthreads();
+        for (int k = 0; k < w; ++k) x += s_wsum[k];
+        s_off[t + 1] = x;
+        if (t == 0) s_off[0] = 0;
+        __syncthreads();
+        const long long total = s_off[tn];
+        for (long long f0 = (long long)blockIdx.x * blockDim.x; f0 < total; f0 += stride) {
+            const long long f = f0 + t;
+            bool claim = false;
+            int xv = 0;
+            if (f < total) {
+                int k = 0;  // max k < tn with s_off[k] <= f
+#pragma unroll
+                for (int step = GC_BLOCK / 2; step > 0; step >>= 1)
+                    if (k + step < tn && s_off[k + step] <= f) k += step;
+                const long long off = f - s_off[k];
+                if (off < s_hl[k]) {
+                    gc_hub_mark(g, g.hin_col[s_hs[k] + off], s_cc[k]);
+                } else {
+                    xv = g.tcol[s_ts[k] + (off - s_hl[k])];
+                    if (mark) g.mark[xv] = 1;
+                    else claim = gc_claim(g.inF, xv);
+                }
+            }
+            gc_stage_push(st, claim, xv, next, next_cnt);
+        }
+        __syncthreads();  // the tile's LDS is rewritten next
     }
     gc_stage_flush_block(st, next, next_cnt);
 }

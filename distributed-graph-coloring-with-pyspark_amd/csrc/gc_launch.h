@@ -25,7 +25,8 @@ struct GDev {
     int* lcur;            // undecided light vertex: low-row entries a later JP sweep may skip
     ull* bstat;           // GC_STAT_SLOTS x 16 stats slots (gc_stat_add)
     ull* accs;            // GC_ACC_SLOTS winner-count slots (single-GPU engine), else null
-    int big_rows;         // some in-row (+ hub row) may exceed GC_BIGROW: k_commit_big is needed
+    int big_rows;         // some in-row (+ hub row) may exceed bigrow: k_commit_big is needed
+    int bigrow;           // heavy winners with longer in-rows (+ hub rows) go to k_commit_big (GC_BIGROW)
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a

@@ -109,3 +109,17 @@ def test_threshold_change_rebuilds(monkeypatch):
         for t in ("64", "4", "off", "0", "64"):
             monkeypatch.setenv("GC_HUB_T", t)
             assert_same_run(dg.color("A"), o)
+
+
+@pytest.mark.parametrize("bigrow", ["0", "8", "64"])
+@pytest.mark.parametrize("hub_t", ["0", "4", "1024"])
+def test_commit_big_tiles(monkeypatch, bigrow, hub_t):
+    """Winners deferred to k_commit_big (in-rows past GC_BIGROW): with a tiny threshold
+    hundreds of hub winners per round go through its flat walk, several 256-winner tiles."""
+    monkeypatch.setenv("GC_HUB_T", hub_t)
+    monkeypatch.setenv("GC_BIGROW", bigrow)
+    with _dg().rmat(12, 16, seed=7) as dg:
+        rp, col = dg.export()
+    _check(rp, col, symmetric=True, bounded=False)
+    rp, col = _random_directed(3000, 30000, 11)
+    _check(rp, col)
