@@ -415,17 +415,6 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
     g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
 
-// Wave-aggregated append through an LDS counter (all 64 lanes call; pred per lane).
-__device__ __forceinline__ void gc_lds_append(bool pred, int val, int* out, int* lds_cnt) {
-    const ull m = __ballot(pred);
-    if (m == 0) return;
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (gc_lane() == leader) base = atomicAdd(lds_cnt, __popcll(m));
-    base = __shfl(base, leader, GC_WAVE);
-    if (pred) out[base + __popcll(m & gc_lanemask_lt())] = val;
-}
-
 // JP step of hub x against the lower-rank hubs of its row (hlow).  The first evaluation
 // of a round reads the whole row: undecided entries with the hub's candidate go to its
 // pending list, and the entries not yet coloured are copied to the next working copy of
@@ -465,28 +454,23 @@ __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
         const int* __restrict__ hc = g.hlowb[hr] + base;
         int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
         const unsigned char* __restrict__ c8 = g.c8;
-        // 8 entries per thread in flight (one workgroup walks a row of up to ~10^6 hubs, so the
-        // walk is latency-bound); appends are wave-aggregated (one LDS atomic per wave)
-        for (int e0 = 0; e0 < len; e0 += 8 * GC_BLOCK) {
-            int u[8];
+        for (int e = t; e < len; e += 4 * GC_BLOCK) {
+            int u[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int e = e0 + t + k * GC_BLOCK;
-                u[k] = e < len ? hc[e] : -1;
-            }
-            unsigned ku[8], cu[8];
+            for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
+            unsigned ku[4], cu[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < 4; ++k) {
                 ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
                 cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
-                const unsigned fl = live ? gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;
+            for (int k = 0; k < 4; ++k) {
+                if (u[k] < 0 || cu[k] != GC_C8_NONE) continue;  // coloured: dropped for good
+                keep[atomicAdd(&s_k, 1)] = u[k];
+                const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
                 if (fl & 1u) s_out = 1u;
-                gc_lds_append(live, u[k], keep, &s_k);
-                gc_lds_append(fl == 2u, u[k], dst, &s_n);
+                if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
             }
         }
     }
@@ -503,6 +487,75 @@ __device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
         if (!out) g.hpc[x] = (n << 1) | (sel ^ 1);
     }
     return out ? 1u : (n > 0 ? 2u : 0u);
+}
+
+// gc_hub_jp for ONE wave (all 64 lanes call with the same x; returns the same value on
+// every lane).  Hub rows of lower-rank hubs are short (R-MAT-24: at most ~1.7k entries),
+// while a hub's evaluation is a chain of ~10 dependent loads: a wave per hub keeps 4x as
+// many hubs in flight as a workgroup per hub, and its appends are counted in registers.
+__device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
+    const int lane = gc_lane();
+    const ull lt = gc_lanemask_lt();
+    const unsigned char* __restrict__ k8 = g.k8;
+    const int enc = g.hpc[x];
+    const int sel = enc & 1, cnt = enc >> 1;
+    const long long base = g.hlow_rp[x];
+    const int* __restrict__ src = g.hpend[sel] + base;
+    int* dst = g.hpend[sel ^ 1] + base;
+    const bool first = g.hcur[x] == 0;
+    int nn = 0, nk = 0;  // wave-uniform append counts
+    bool out = false;    // wave-uniform
+    for (int i0 = 0; i0 < cnt && !out; i0 += GC_WAVE) {
+        const int i = i0 + lane;
+        const int u = i < cnt ? src[i] : -1;
+        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
+        out = __ballot((fl & 1u) != 0u) != 0ull;
+        const ull m = __ballot(fl == 2u);
+        if (fl == 2u) dst[nn + __popcll(m & lt)] = u;
+        nn += __popcll(m);
+    }
+    const int hr = first ? g.hrow[x] : 0;
+    if (first) {
+        const int len = hr ? g.hlen[x] : (int)(g.hlow_rp[x + 1] - base);
+        const int* __restrict__ hc = g.hlowb[hr] + base;
+        int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
+        const unsigned char* __restrict__ c8 = g.c8;
+        for (int e0 = 0; e0 < len; e0 += 4 * GC_WAVE) {
+            int u[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = e0 + k * GC_WAVE + lane;
+                u[k] = e < len ? hc[e] : -1;
+            }
+            unsigned ku[4], cu[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
+                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
+                const unsigned fl = live ? gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;
+                if (__ballot((fl & 1u) != 0u)) out = true;
+                const ull mk = __ballot(live);
+                if (live) keep[nk + __popcll(mk & lt)] = u[k];
+                nk += __popcll(mk);
+                const ull mp = __ballot(fl == 2u);
+                if (fl == 2u) dst[nn + __popcll(mp & lt)] = u[k];
+                nn += __popcll(mp);
+            }
+        }
+    }
+    if (lane == 0) {
+        if (first) {  // the kept copy is complete (the whole row was read)
+            g.hrow[x] = hr == 1 ? 2 : 1;
+            g.hlen[x] = nk;
+            g.hcur[x] = 1;
+        }
+        if (!out) g.hpc[x] = (nn << 1) | (sel ^ 1);
+    }
+    return out ? 1u : (nn > 0 ? 2u : 0u);
 }
 
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
@@ -526,6 +579,40 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     // hubs first: one workgroup per vertex; undecided ones staged by wave 0 (LDS of its own)
     __shared__ int s_hstage[GC_STAGE_CAP];
     GcStage hst{s_hstage, 0};
+    if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
+        for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
+             i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+            const int v = hlist[i];
+            const unsigned kv = k8[v];
+            const unsigned cv6 = gc_k8_cand(kv);
+            const int cv = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
+            const int x = g.hid[v];
+            unsigned f = 0;
+            if (x >= 0) {
+                f = g.hkill[x] ? 1u : gc_hub_jp_wave(g, x, cv6, cv);
+            } else {  // not a hub (cannot happen while heavy_t is the hub threshold): row scan
+                const int dl = g.nlow[v];
+                const long long start = g.rp[v];
+                unsigned lf = 0;
+                for (int e = lane; e < dl; e += GC_WAVE) {
+                    const int u = g.col[start + e];
+                    lf |= gc_jp_flag(g, u, k8[u], cv6, cv);
+                }
+                f = (__ballot((lf & 1u) != 0u) ? 1u : 0u) | (__ballot((lf & 2u) != 0u) ? 2u : 0u);
+            }
+            gc_stage_push(st, lane == 0 && (f & 3u) == 2u, v, ho, ho_cnt);  // undecided hub
+            if (lane == 0) {
+                if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
+                else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
+                if (dout && ((f & 1u) || !(f & 2u)))
+                    dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
+                lsum += (ull)g.deg[v];
+                lnv++;
+            }
+        }
+        gc_stage_flush(st, ho, ho_cnt);  // st is the light list's stage from here on
+        hcnt = 0;
+    }
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
         const int v = hlist[i];
         const int d = g.deg[v];
