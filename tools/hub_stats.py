@@ -28,11 +28,11 @@ src = np.repeat(np.arange(n, dtype=np.int32), deg)
 m = hub[src] & hub[col]
 hs, hd = src[m], col[m]
 print(f"hub-hub entries={m.sum()} ({m.sum()/len(col):.2%} of nnz)")
-# rank: (deg, pos) -- higher rank decides first (coloring.py:64); 'low' = higher-priority
+# rank: (deg, pos) ascending decides first (coloring.py:64); hlow(x) = hubs of smaller rank
 key = deg.astype(np.int64) * (n + 1) + np.arange(n)
-low = key[hd] > key[hs]
+low = key[hd] < key[hs]
 hl = np.bincount(hs[low], minlength=n)[hub]
-print(f"hlow entries={low.sum()} max row={hl.max()} top rows={np.sort(hl)[-5:]}")
+print(f"hlow entries={low.sum()} max row={hl.max()} top rows={np.sort(hl)[-5:]} rows>4096: {(hl > 4096).sum()} entries in them {hl[hl > 4096].sum()}")
 cr = np.asarray(res.colored_round)
 if cr is not None and cr.size == n:
     R = int(cr.max()) + 1
