@@ -425,71 +425,7 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 // hrow[x] = which copy holds the live row (0: the original hlow_col), hlen[x] its length.
 // Returns 1 (OUT: a same-candidate lower-rank hub is IN), 2 (undecided) or 0 (IN); whole
 // workgroup, same value everywhere.
-__device__ unsigned gc_hub_jp(const GDev& g, int x, unsigned cv6, int cv) {
-    __shared__ int s_n, s_k;
-    __shared__ unsigned s_out;
-    const int t = threadIdx.x;
-    const unsigned char* __restrict__ k8 = g.k8;
-    const int enc = g.hpc[x];
-    const int sel = enc & 1, cnt = enc >> 1;
-    const long long base = g.hlow_rp[x];
-    const int* __restrict__ src = g.hpend[sel] + base;
-    int* dst = g.hpend[sel ^ 1] + base;
-    const bool first = g.hcur[x] == 0;
-    if (t == 0) {
-        s_n = 0;
-        s_k = 0;
-        s_out = 0u;
-    }
-    __syncthreads();
-    for (int i = t; i < cnt && !s_out; i += GC_BLOCK) {
-        const int u = src[i];
-        const unsigned fl = gc_jp_flag(g, u, k8[u], cv6, cv);
-        if (fl & 1u) s_out = 1u;
-        if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u;
-    }
-    const int hr = first ? g.hrow[x] : 0;
-    if (first) {
-        const int len = hr ? g.hlen[x] : (int)(g.hlow_rp[x + 1] - base);
-        const int* __restrict__ hc = g.hlowb[hr] + base;
-        int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
-        const unsigned char* __restrict__ c8 = g.c8;
-        for (int e = t; e < len; e += 4 * GC_BLOCK) {
-            int u[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) u[k] = e + k * GC_BLOCK < len ? hc[e + k * GC_BLOCK] : -1;
-            unsigned ku[4], cu[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
-                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (u[k] < 0 || cu[k] != GC_C8_NONE) continue;  // coloured: dropped for good
-                keep[atomicAdd(&s_k, 1)] = u[k];
-                const unsigned fl = gc_jp_flag(g, u[k], ku[k], cv6, cv);
-                if (fl & 1u) s_out = 1u;
-                if (fl == 2u) dst[atomicAdd(&s_n, 1)] = u[k];
-            }
-        }
-    }
-    __syncthreads();
-    const unsigned out = s_out;
-    const int n = s_n;
-    __syncthreads();
-    if (t == 0) {
-        if (first) {  // the kept copy is complete (the whole row was read)
-            g.hrow[x] = hr == 1 ? 2 : 1;
-            g.hlen[x] = s_k;
-            g.hcur[x] = 1;
-        }
-        if (!out) g.hpc[x] = (n << 1) | (sel ^ 1);
-    }
-    return out ? 1u : (n > 0 ? 2u : 0u);
-}
-
-// gc_hub_jp for ONE wave (all 64 lanes call with the same x; returns the same value on
+// ... evaluated by ONE wave (all 64 lanes call with the same x; returns the same value on
 // every lane).  Hub rows of lower-rank hubs are short (R-MAT-24: at most ~1.7k entries),
 // while a hub's evaluation is a chain of ~10 dependent loads: a wave per hub keeps 4x as
 // many hubs in flight as a workgroup per hub, and its appends are counted in registers.
@@ -576,7 +512,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     // undecided appends staged in LDS: one atomic per 512 entries, not one per wave-chunk
     // (a single counter takes ~88 returning atomics/us; 86k chunks cost ~1 ms)
     GcStage st{s_stage[w], 0};
-    // hubs first: one workgroup per vertex; undecided ones staged by wave 0 (LDS of its own)
+    // heavy vertices first.  Hubs off: a workgroup each, undecided ones staged by wave 0
     __shared__ int s_hstage[GC_STAGE_CAP];
     GcStage hst{s_hstage, 0};
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
@@ -623,16 +559,10 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         const int cv = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
         if (threadIdx.x == 0) s_f = 0;
         __syncthreads();
-        unsigned f = 0;
-        const int x = g.hub_w ? g.hid[v] : -1;
-        if (x >= 0) {  // hub (gc_hubs.hip): every light entry is decided; flagged = one won cv
-            if (g.hkill[x]) f = 1u;
-            else f = gc_hub_jp(g, x, cv6, cv);  // whole workgroup, same value on every thread
-        } else {
-            for (long long e = threadIdx.x; e < dl; e += blockDim.x) {
-                const int u = g.col[start + e];
-                f |= gc_jp_flag(g, u, k8[u], cv6, cv);
-            }
+        unsigned f = 0;  // hubs off here (hubs on: evaluated by waves above, hcnt = 0)
+        for (long long e = threadIdx.x; e < dl; e += blockDim.x) {
+            const int u = g.col[start + e];
+            f |= gc_jp_flag(g, u, k8[u], cv6, cv);
         }
         if (f) atomicOr(&s_f, f);
         __syncthreads();
