@@ -249,13 +249,17 @@ struct Run {
     // device then decides per round (gc_big_on) whether the commit pushes or marks.
     void launch_commit(int mode, int nsweeps) {
         const int big = mode == GC_CM_ROUND && resort_hint;
-        if (mode == GC_CM_ROUND) {
+        // no sweeps enqueued and >= 16 rounds so far all decided by their first sweep (meshes):
+        // no tail kernel either; a round that needs more makes the commit ask for sweeps
+        // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
+        const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
+        if (tail) {
             kt.begin(GC_K_SWEEP);
             gcl_sweep_tail(d, L, nsweeps, s);
             kt.end();
         }
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
-        gcl_commit(d, L, mode, nsweeps, s, big);
+        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big);
         kt.end();
         if (big) {
             kt.begin(GC_K_COMMIT);
@@ -311,7 +315,9 @@ struct Run {
     // sweeps to enqueue per round from the depths seen so far: none while every round
     // was decided by the first sweep (meshes), else twice the last round's depth
     const int sweep_pad = getenv("GC_SWEEP_PAD") ? atoi(getenv("GC_SWEEP_PAD")) : 2;
-    int pick_sweeps(const DevCtl& h) const {
+    bool skip_tail = false;  // set with S = 0 once 16 rounds ran without a second sweep
+    int pick_sweeps(const DevCtl& h) {
+        skip_tail = h.maxdepth <= 1 && h.round >= 16;
         if (h.maxdepth <= 1) return 0;
         return (int)std::min<long long>(64, h.lastbig + sweep_pad);  // the small-list tail runs in k_sweep_tail
     }

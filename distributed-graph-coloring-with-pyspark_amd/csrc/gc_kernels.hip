@@ -878,7 +878,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ int s_acc, s_accc, s_lose;
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const long long last = mode == GC_CM_ROUND ? c->tail_last : nsweeps;  // k_sweep_tail ran before
+    // k_sweep_tail ran before (nsweeps >= 0), else only the first sweep (k_resolve, slot 0) did
+    const long long last = mode == GC_CM_ROUND ? (nsweeps < 0 ? 0ll : c->tail_last) : nsweeps;
     const int last_slot = (int)(last % 3);
     if (mode == GC_CM_ROUND &&
         ((c->und_cnt[last_slot] | c->undh_cnt[last_slot]) || (g.hub_w && c->heavy_cnt && c->hub_start > last))) {
