@@ -441,14 +441,25 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
     const bool first = g.hcur[x] == 0;
     int nn = 0, nk = 0;  // wave-uniform append counts
     bool out = false;    // wave-uniform
-    for (int i0 = 0; i0 < cnt && !out; i0 += GC_WAVE) {
-        const int i = i0 + lane;
-        const int u = i < cnt ? src[i] : -1;
-        const unsigned fl = u >= 0 ? gc_jp_flag(g, u, k8[u], cv6, cv) : 0u;
-        out = __ballot((fl & 1u) != 0u) != 0ull;
-        const ull m = __ballot(fl == 2u);
-        if (fl == 2u) dst[nn + __popcll(m & lt)] = u;
-        nn += __popcll(m);
+    for (int i0 = 0; i0 < cnt && !out; i0 += 4 * GC_WAVE) {  // 4 per lane, flags before stores
+        int u[4];
+        unsigned fl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * GC_WAVE + lane;
+            u[k] = i < cnt ? src[i] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? gc_jp_flag(g, u[k], fl[k], cv6, cv) : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (__ballot((fl[k] & 1u) != 0u)) out = true;
+            const ull m = __ballot(fl[k] == 2u);
+            if (fl[k] == 2u) dst[nn + __popcll(m & lt)] = u[k];
+            nn += __popcll(m);
+        }
     }
     const int hr = first ? g.hrow[x] : 0;
     if (first) {
@@ -456,29 +467,35 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
         const int* __restrict__ hc = g.hlowb[hr] + base;
         int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
         const unsigned char* __restrict__ c8 = g.c8;
-        for (int e0 = 0; e0 < len; e0 += 4 * GC_WAVE) {
-            int u[4];
+        // GC_HUB_UNR entries per lane in flight; every flag (and its cand[] gather, for
+        // candidates >= 62) is computed before the first store, which could alias cand[]
+        for (int e0 = 0; e0 < len; e0 += GC_HUB_UNR * GC_WAVE) {
+            int u[GC_HUB_UNR];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
                 const int e = e0 + k * GC_WAVE + lane;
                 u[k] = e < len ? hc[e] : -1;
             }
-            unsigned ku[4], cu[4];
+            unsigned ku[GC_HUB_UNR], cu[GC_HUB_UNR];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
                 ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
                 cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
             }
+            unsigned fl[GC_HUB_UNR];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
                 const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
-                const unsigned fl = live ? gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;
-                if (__ballot((fl & 1u) != 0u)) out = true;
-                const ull mk = __ballot(live);
-                if (live) keep[nk + __popcll(mk & lt)] = u[k];
+                fl[k] = live ? 4u | gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;  // bit 2: live
+            }
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                if (__ballot((fl[k] & 1u) != 0u)) out = true;
+                const ull mk = __ballot(fl[k] != 0u);
+                if (fl[k]) keep[nk + __popcll(mk & lt)] = u[k];
                 nk += __popcll(mk);
-                const ull mp = __ballot(fl == 2u);
-                if (fl == 2u) dst[nn + __popcll(mp & lt)] = u[k];
+                const ull mp = __ballot((fl[k] & 3u) == 2u);
+                if ((fl[k] & 3u) == 2u) dst[nn + __popcll(mp & lt)] = u[k];
                 nn += __popcll(mp);
             }
         }
