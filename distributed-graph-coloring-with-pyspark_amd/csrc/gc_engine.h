@@ -60,6 +60,10 @@ struct gc_graph {
     int* hrow = nullptr;
     int* hlen = nullptr;
     int* hlow2[2] = {nullptr, nullptr};
+    long long* hch_rp = nullptr;  // hub x: first static GC_HCH-entry chunk of its hlow row
+    int* hch_own = nullptr;       // static chunk -> hub
+    int* hkcnt = nullptr;         // hub x: kept-row entries written by the long-row first pass this round
+    long long nhch = 0;           // static chunks
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;

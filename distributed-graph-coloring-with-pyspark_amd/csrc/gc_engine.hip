@@ -68,6 +68,13 @@ GDev gc_view(const gc_graph* g) {
     d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= d.bigrow);
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
+    d.hub_long = 0;
+    d.hch_rp = nullptr;
+    d.hch_own = nullptr;
+    d.hkcnt = nullptr;
+    d.nhch = 0;
+    d.hch_mul = 1;
+    d.hprep = 0;
     d.hid = nullptr;
     d.hub_v = nullptr;
     d.hin_rp = nullptr;

@@ -24,6 +24,7 @@
 // results stay bit-identical to the row-scan engine (and to the oracle).  The cost moves
 // to the low-degree side -- one walk of a vertex's hin row when it is coloured (bitmaps)
 // and one when it wins (flags) -- instead of every hub re-reading its row every round.
+#include <numeric>
 #include <stdlib.h>
 #include <string.h>
 
@@ -98,6 +99,18 @@ __global__ void k_hlow_fill(const long long* rp, const int* col, const int* nlow
             o += __popcll(m);
         }
     }
+}
+
+// static chunks of the hlow rows: ceil(len / GC_HCH) per hub, then chunk -> hub
+__global__ void k_hch_count(const long long* hlow_rp, long long H, long long* cnt) {
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < H) cnt[x] = (hlow_rp[x + 1] - hlow_rp[x] + GC_HCH - 1) / GC_HCH;
+    else if (x == H) cnt[x] = 0;
+}
+__global__ void k_hch_fill(const long long* hch_rp, long long H, int* own) {
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < H)
+        for (long long j = hch_rp[x]; j < hch_rp[x + 1]; ++j) own[j] = (int)x;
 }
 
 int scan_ll(const long long* in, long long* out, long long count, hipStream_t s) {
@@ -199,6 +212,14 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMalloc((void**)&g->hlen, sizeof(int) * (size_t)H));
     hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
                        g->hlow_rp, g->hlow_col);
+    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
+    hipLaunchKernelGGL(k_hch_count, dim3(grid_of(H + 1)), dim3(GC_BLOCK), 0, s, g->hlow_rp, H, pos);
+    GC_HIP(hipMalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
+    if ((rc = scan_ll(pos, g->hch_rp, H + 1, s))) { hipFree(pos); return rc; }
+    GC_HIP(hipMemcpy(&g->nhch, g->hch_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_HIP(hipMalloc((void**)&g->hch_own, sizeof(int) * (size_t)std::max<long long>(g->nhch, 1)));
+    GC_HIP(hipMalloc((void**)&g->hkcnt, sizeof(int) * (size_t)H));
+    hipLaunchKernelGGL(k_hch_fill, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, g->hch_rp, H, g->hch_own);
     GC_HIP(hipGetLastError());
     GC_HIP(hipStreamSynchronize(s));
     hipFree(pos);
@@ -211,12 +232,15 @@ int build(gc_graph* g, int T, int W) {
 
 void gc_hubs_free(gc_graph* g) {
     void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
-                    g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen};
+                    g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen,
+                    g->hch_rp, g->hch_own, g->hkcnt};
     for (void* p : ptrs)
         if (p) hipFree(p);
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
     g->hlow2[0] = g->hlow2[1] = g->hrow = g->hlen = nullptr;
-    g->hin_rp = g->hlow_rp = nullptr;
+    g->hin_rp = g->hlow_rp = g->hch_rp = nullptr;
+    g->hch_own = g->hkcnt = nullptr;
+    g->nhch = 0;
     g->hbits = g->hkill = nullptr;
     g->nhub = 0;
     g->hub_t = -1;
@@ -255,6 +279,15 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hlowb[0] = g->hlow_col;
     d.hlowb[1] = g->hlow2[0];
     d.hlowb[2] = g->hlow2[1];
+    d.hub_long = env_int("GC_HUB_LONG", GC_HUB_LONG);
+    d.hch_rp = g->hch_rp;
+    d.hch_own = g->hch_own;
+    d.hkcnt = g->hkcnt;
+    d.nhch = g->nhch;
+    d.hprep = env_int("GC_HUB_PREP", 1) > 0 && g->nhch > 0 && d.hub_long >= 0;
+    long long m = std::max<long long>(1, (long long)(0.6180339887 * (double)g->nhch));
+    while (std::gcd(m, std::max<long long>(g->nhch, 1ll)) != 1) ++m;
+    d.hch_mul = m;
     GC_HIP(hipMemsetAsync(g->hrow, 0, sizeof(int) * (size_t)g->nhub, g->stream));  // full rows again
     return GC_OK;
 }

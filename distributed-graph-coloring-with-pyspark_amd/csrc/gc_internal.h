@@ -33,6 +33,8 @@ typedef unsigned long long ull;
 // hubs (gc_hubs.hip): default threshold, bitmap words (4096 colours)
 #define GC_HUB_T 1024
 #define GC_HUB_W 128
+#define GC_HUB_LONG 16384   // hub-start sweep: longer hlow rows are first-read by the whole grid
+#define GC_HCH 1024         // entries per static chunk of an hlow row (one wave each)
 #ifndef GC_HUB_UNR
 #define GC_HUB_UNR 8        // hub row walk (gc_hub_jp_wave): entries per lane in flight
 #endif

@@ -354,6 +354,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
                 g.hkill[x] = 0u;
                 g.hcur[x] = 0;
                 g.hpc[x] = 0;
+                if (g.hprep) g.hkcnt[x] = 0;
                 s_first = 0x7FFFFFFF;
             }
             __syncthreads();
@@ -433,12 +434,21 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
     const int lane = gc_lane();
     const ull lt = gc_lanemask_lt();
     const unsigned char* __restrict__ k8 = g.k8;
-    const int enc = g.hpc[x];
+    int enc = g.hpc[x];
+    const int hc0 = g.hcur[x];
+    const bool first = hc0 == 0;
+    if (hc0 == 2) {  // the grid read this long row in the hub-start sweep (gc_hub_first_long): adopt its
+        enc |= 1;    // kept copy and its pending list (half 1)
+        if (lane == 0) {
+            g.hrow[x] = g.hrow[x] == 1 ? 2 : 1;
+            g.hlen[x] = g.hkcnt[x];
+            g.hcur[x] = 1;
+        }
+    }
     const int sel = enc & 1, cnt = enc >> 1;
     const long long base = g.hlow_rp[x];
     const int* __restrict__ src = g.hpend[sel] + base;
     int* dst = g.hpend[sel ^ 1] + base;
-    const bool first = g.hcur[x] == 0;
     int nn = 0, nk = 0;  // wave-uniform append counts
     bool out = false;    // wave-uniform
     for (int i0 = 0; i0 < cnt && !out; i0 += 4 * GC_WAVE) {  // 4 per lane, flags before stores
@@ -511,11 +521,103 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
     return out ? 1u : (nn > 0 ? 2u : 0u);
 }
 
+// First read of the LONG hub rows (static length > hub_long) in the sweep that starts the
+// hubs, by the whole grid: one wave per GC_HCH-entry chunk (static chunk index hch_rp /
+// hch_own, scanned in a scattered order so a long row's chunks land on many waves).  It
+// writes what the hub's first evaluation would: the kept copy of the row (uncoloured
+// entries; hkcnt counts them) and the pending list (entries with the hub's candidate that
+// are not OUT, in hpend[1]; hpc counts them, x2).  The hub itself was listed undecided with
+// hcur = 2 by the same sweep and adopts both at its first evaluation (next sweep).  No hub
+// is IN before this sweep's evaluations; an entry that is IN by the time the hub reads its
+// pending list makes it OUT there, as in the row walk.  One wave walking a 2.5e5-entry row
+// (R-MAT-26) was the hub-start sweep's long pole.
+__device__ void gc_hub_first_long(GDev& g) {
+    constexpr int K = GC_HCH / GC_WAVE;
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const ull lt = gc_lanemask_lt();
+    const unsigned char* __restrict__ k8 = g.k8;
+    const unsigned char* __restrict__ c8 = g.c8;
+    const long long NC = g.nhch;
+    const long long wstride = (long long)gridDim.x * GC_WAVES_PER_BLOCK * GC_WAVE;
+    for (long long j0 = ((long long)blockIdx.x * GC_WAVES_PER_BLOCK + w) * GC_WAVE; j0 < NC; j0 += wstride) {
+        const long long j = j0 + lane;
+        int x = -1, part = 0, len = 0, hr = 0;
+        unsigned kx = 0;
+        if (j < NC) {
+            const long long jj = (long long)(((ull)j * (ull)g.hch_mul) % (ull)NC);
+            x = g.hch_own[jj];
+            part = (int)(jj - g.hch_rp[x]);
+            const long long full = g.hlow_rp[x + 1] - g.hlow_rp[x];
+            if (full > g.hub_long) {
+                kx = k8[g.hub_v[x]];
+                hr = g.hrow[x];
+                len = hr ? g.hlen[x] : (int)full;
+            }
+            // short row / no proposer / past the live row / flagged (OUT without a read)
+            if (full <= g.hub_long || gc_k8_cand(kx) == GC_K8_NONE || (long long)part * GC_HCH >= len || g.hkill[x])
+                x = -1;
+        }
+        ull act = __ballot(x >= 0);
+        while (act) {
+            const int sl = __ffsll((long long)act) - 1;
+            act &= act - 1;
+            const int hx = __shfl(x, sl, GC_WAVE);
+            const int e0 = __shfl(part, sl, GC_WAVE) * GC_HCH;
+            const int hl = __shfl(len, sl, GC_WAVE);
+            const int hhr = __shfl(hr, sl, GC_WAVE);
+            const unsigned cv6 = gc_k8_cand(__shfl(kx, sl, GC_WAVE));
+            const int cv = cv6 == GC_K8_BIG ? g.cand[g.hub_v[hx]] : (int)cv6;
+            const long long base = g.hlow_rp[hx];
+            const int* __restrict__ hc = g.hlowb[hhr] + base;
+            int u[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int e = e0 + k * GC_WAVE + lane;
+                u[k] = e < hl ? hc[e] : -1;
+            }
+            unsigned ku[K], cu[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
+                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
+            }
+            ull mk[K], mp[K];  // wave masks per slot: live (kept) / pending
+            int tk = 0, tp = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
+                mk[k] = __ballot(live);
+                mp[k] = __ballot(live && gc_jp_flag(g, u[k], ku[k], cv6, cv) != 0u);
+                tk += __popcll(mk[k]);
+                tp += __popcll(mp[k]);
+            }
+            int kb = 0, pb = 0;
+            if (lane == 0) {
+                if (tk) kb = atomicAdd(&g.hkcnt[hx], tk);
+                if (tp) pb = atomicAdd(&g.hpc[hx], 2 * tp) >> 1;
+            }
+            kb = __shfl(kb, 0, GC_WAVE);
+            pb = __shfl(pb, 0, GC_WAVE);
+            int* keep = g.hlowb[hhr == 1 ? 2 : 1] + base;
+            int* pend = g.hpend[1] + base;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if ((mk[k] >> lane) & 1ull) keep[kb + __popcll(mk[k] & lt)] = u[k];
+                if ((mp[k] >> lane) & 1ull) pend[pb + __popcll(mp[k] & lt)] = u[k];
+                kb += __popcll(mk[k]);
+                pb += __popcll(mp[k]);
+            }
+        }
+    }
+}
+
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
 // undecided vertices are appended to (uo, uo_cnt) / (ho, ho_cnt).
 __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ list, long long cnt, int skip_heavy,
                                             const int* hlist, long long hcnt, int* uo, ull* uo_cnt, int* ho,
-                                            ull* ho_cnt, ull& lsum, ull& lnv, long long* dout, ull* dcnt) {
+                                            ull* ho_cnt, ull& lsum, ull& lnv, long long* dout, ull* dcnt,
+                                            bool hub_first = false) {
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_first[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -542,7 +644,14 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             const int x = g.hid[v];
             unsigned f = 0;
             if (x >= 0) {
-                f = g.hkill[x] ? 1u : gc_hub_jp_wave(g, x, cv6, cv);
+                if (g.hkill[x]) {
+                    f = 1u;
+                } else if (hub_first && g.hlow_rp[x + 1] - g.hlow_rp[x] > g.hub_long) {
+                    f = 2u;  // long row: read by the grid below (gc_hub_first_long), evaluated next sweep
+                    if (lane == 0) g.hcur[x] = 2;
+                } else {
+                    f = gc_hub_jp_wave(g, x, cv6, cv);
+                }
             } else {  // not a hub (cannot happen while heavy_t is the hub threshold): row scan
                 const int dl = g.nlow[v];
                 const long long start = g.rp[v];
@@ -564,6 +673,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             }
         }
         gc_stage_flush(st, ho, ho_cnt);  // st is the light list's stage from here on
+        if (hub_first) gc_hub_first_long(g);
         hcnt = 0;
     }
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
@@ -722,7 +832,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     if (cl + ch == 0) return;
     ull lsum = 0, lnv = 0;
     gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
-                &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
+                &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt, hub_start && g.hprep);
     __syncthreads();
     gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
 }

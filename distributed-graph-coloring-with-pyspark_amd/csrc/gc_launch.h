@@ -33,6 +33,13 @@ struct GDev {
     // list, both pushed to it, instead of re-reading its whole row every round / sweep.
     int heavy_t;
     int hub_w;                // words per hub bitmap (0 = hubs off)
+    long long hub_long;       // hub-start sweep: hubs whose hlow row exceeds this are first-read by the whole grid
+    const long long* hch_rp;  // static GC_HCH-entry chunks of the hlow rows (hub x: [hch_rp[x], hch_rp[x+1]))
+    const int* hch_own;       //   chunk -> hub
+    int* hkcnt;               //   kept-row entries written by the grid this round
+    long long nhch;
+    long long hch_mul;        //   coprime to nhch, ~0.618 nhch: chunk scan order (a long row's chunks spread out)
+    int hprep;                // long-row first pass on (GC_HUB_PREP)
     const int* hid;           // hub index of v, -1 if v is no hub
     const int* hub_v;         // vertex of hub index x
     const long long* hin_rp;  // for every u: the hubs (indices) whose rows list u

@@ -32,13 +32,16 @@ SETTINGS = [
     {"GC_HUB_T": "64"},
     {"GC_HUB_T": "1024"},                                     # the default
     {"GC_HUB_T": "off"},
+    {"GC_HUB_T": "0", "GC_HUB_LONG": "4"},                    # long rows first-read by the whole grid
+    {"GC_HUB_T": "2", "GC_HUB_LONG": "0"},                    # ... every row
+    {"GC_HUB_T": "0", "GC_HUB_LONG": "0", "GC_HUB_PREP": "off"},  # every row walked by its wave
 ]
-IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T1024", "off"]
+IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T1024", "off", "T0long4", "T2long0", "T0noprep"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
-    for k in ("GC_HUB_T", "GC_HUB_W"):
+    for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
