@@ -75,6 +75,8 @@ GDev gc_view(const gc_graph* g) {
     d.nhch = 0;
     d.hch_mul = 1;
     d.hprep = 0;
+    d.hk = nullptr;
+    d.hcand = nullptr;
     d.hid = nullptr;
     d.hub_v = nullptr;
     d.hin_rp = nullptr;

@@ -309,6 +309,7 @@ __device__ __forceinline__ unsigned char gc_c8_of(long long c) {
 // the candidate is in cand[]) or GC_K8_NONE (not proposing this round)
 #define GC_K8_BIG 62u
 #define GC_K8_NONE 63u
+#define GC_HK_COLOURED 0xFFu  // hub mirror hk: coloured (cand NONE, state 3)
 __device__ __forceinline__ unsigned char gc_k8(unsigned c6, unsigned st) { return (unsigned char)((c6 << 2) | st); }
 __device__ __forceinline__ unsigned gc_c6_of(long long c) { return c >= 62 ? GC_K8_BIG : (unsigned)c; }
 __device__ __forceinline__ unsigned gc_k8_cand(unsigned k) { return k >> 2; }

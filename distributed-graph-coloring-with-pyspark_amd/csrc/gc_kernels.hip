@@ -53,6 +53,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
             g.cround[v] = iso ? 0 : -1;
             g.c8[v] = iso ? 0 : (unsigned char)GC_C8_NONE;
             g.k8[v] = push0 ? gc_k8(0u, GC_JP_IN) : gc_k8(GC_K8_NONE, GC_JP_UND);
+            if (g.hub_w && g.hid[v] >= 0)  // hub mirror (never isolated)
+                g.hk[g.hid[v]] = gc_k8(GC_K8_NONE, GC_JP_UND);
             g.mark[v] = 0;
             if (!iso) {
                 unc++;
@@ -91,6 +93,7 @@ __global__ void k_seed_prep(GDev g, int* seed_light, int* seed_heavy) {
     const int s = (int)(sk & 0xFFFFFFFFull);
     const int d = g.deg[s];
     g.k8[s] = gc_k8(0u, GC_JP_IN);
+    if (g.hub_w && g.hid[s] >= 0) g.hk[g.hid[s]] = gc_k8(0u, GC_JP_IN);
     atomicOr(&g.inF[s >> 5], 1u << (s & 31));
     if (d > GC_HEAVY_T) seed_heavy[atomicAdd(&g.ctl->seed_cnt[1], 1ull)] = s;
     else seed_light[atomicAdd(&g.ctl->seed_cnt[0], 1ull)] = s;
@@ -384,6 +387,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
         }
         if (threadIdx.x == 0) {
             gc_set_cand(g, v, mex);
+            if (x >= 0) {  // hub mirror
+                g.hk[x] = gc_k8(gc_c6_of(mex), GC_JP_UND);
+                g.hcand[x] = (int)mex;
+            }
             lmax = mex > lmax ? mex : lmax;
             if (kbound >= 0 && mex >= kbound) lfail++;
             lsum += (ull)d;
@@ -412,6 +419,15 @@ __device__ __forceinline__ unsigned gc_jp_flag(const GDev& g, int u, unsigned ku
     return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
 }
 
+// gc_jp_flag for a hub entry hx (hub index) from the hub mirrors: hk = k8 of the hub, or
+// GC_HK_COLOURED (cand NONE: never a proposer's candidate)
+__device__ __forceinline__ unsigned gc_jp_flag_h(const GDev& g, int hx, unsigned hk, unsigned cv6, int cv) {
+    if (gc_k8_cand(hk) != cv6) return 0u;
+    if (cv6 == GC_K8_BIG && g.hcand[hx] != cv) return 0u;
+    const unsigned st = gc_k8_state(hk);
+    return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
+}
+
 __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsigned st) {
     g.k8[v] = (unsigned char)((kv & ~3u) | st);
 }
@@ -433,7 +449,7 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
     const int lane = gc_lane();
     const ull lt = gc_lanemask_lt();
-    const unsigned char* __restrict__ k8 = g.k8;
+    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
     int enc = g.hpc[x];
     const int hc0 = g.hcur[x];
     const bool first = hc0 == 0;
@@ -460,9 +476,9 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
             u[k] = i < cnt ? src[i] : -1;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0u;
+        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? (unsigned)hk[u[k]] : 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? gc_jp_flag(g, u[k], fl[k], cv6, cv) : 0u;
+        for (int k = 0; k < 4; ++k) fl[k] = u[k] >= 0 ? gc_jp_flag_h(g, u[k], fl[k], cv6, cv) : 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (__ballot((fl[k] & 1u) != 0u)) out = true;
@@ -476,7 +492,6 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
         const int len = hr ? g.hlen[x] : (int)(g.hlow_rp[x + 1] - base);
         const int* __restrict__ hc = g.hlowb[hr] + base;
         int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
-        const unsigned char* __restrict__ c8 = g.c8;
         // GC_HUB_UNR entries per lane in flight; every flag (and its cand[] gather, for
         // candidates >= 62) is computed before the first store, which could alias cand[]
         for (int e0 = 0; e0 < len; e0 += GC_HUB_UNR * GC_WAVE) {
@@ -486,17 +501,14 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
                 const int e = e0 + k * GC_WAVE + lane;
                 u[k] = e < len ? hc[e] : -1;
             }
-            unsigned ku[GC_HUB_UNR], cu[GC_HUB_UNR];
+            unsigned ku[GC_HUB_UNR];
 #pragma unroll
-            for (int k = 0; k < GC_HUB_UNR; ++k) {
-                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
-                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
-            }
+            for (int k = 0; k < GC_HUB_UNR; ++k) ku[k] = u[k] >= 0 ? (unsigned)hk[u[k]] : GC_HK_COLOURED;
             unsigned fl[GC_HUB_UNR];
 #pragma unroll
             for (int k = 0; k < GC_HUB_UNR; ++k) {
-                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
-                fl[k] = live ? 4u | gc_jp_flag(g, u[k], ku[k], cv6, cv) : 0u;  // bit 2: live
+                const bool live = ku[k] != GC_HK_COLOURED;  // coloured (or no entry): dropped for good
+                fl[k] = live ? 4u | gc_jp_flag_h(g, u[k], ku[k], cv6, cv) : 0u;  // bit 2: live
             }
 #pragma unroll
             for (int k = 0; k < GC_HUB_UNR; ++k) {
@@ -536,8 +548,7 @@ __device__ void gc_hub_first_long(GDev& g) {
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const ull lt = gc_lanemask_lt();
-    const unsigned char* __restrict__ k8 = g.k8;
-    const unsigned char* __restrict__ c8 = g.c8;
+    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
     const long long NC = g.nhch;
     const long long wstride = (long long)gridDim.x * GC_WAVES_PER_BLOCK * GC_WAVE;
     for (long long j0 = ((long long)blockIdx.x * GC_WAVES_PER_BLOCK + w) * GC_WAVE; j0 < NC; j0 += wstride) {
@@ -550,7 +561,7 @@ __device__ void gc_hub_first_long(GDev& g) {
             part = (int)(jj - g.hch_rp[x]);
             const long long full = g.hlow_rp[x + 1] - g.hlow_rp[x];
             if (full > g.hub_long) {
-                kx = k8[g.hub_v[x]];
+                kx = hk[x];
                 hr = g.hrow[x];
                 len = hr ? g.hlen[x] : (int)full;
             }
@@ -567,7 +578,7 @@ __device__ void gc_hub_first_long(GDev& g) {
             const int hl = __shfl(len, sl, GC_WAVE);
             const int hhr = __shfl(hr, sl, GC_WAVE);
             const unsigned cv6 = gc_k8_cand(__shfl(kx, sl, GC_WAVE));
-            const int cv = cv6 == GC_K8_BIG ? g.cand[g.hub_v[hx]] : (int)cv6;
+            const int cv = cv6 == GC_K8_BIG ? g.hcand[hx] : (int)cv6;
             const long long base = g.hlow_rp[hx];
             const int* __restrict__ hc = g.hlowb[hhr] + base;
             int u[K];
@@ -576,19 +587,16 @@ __device__ void gc_hub_first_long(GDev& g) {
                 const int e = e0 + k * GC_WAVE + lane;
                 u[k] = e < hl ? hc[e] : -1;
             }
-            unsigned ku[K], cu[K];
+            unsigned ku[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                ku[k] = u[k] >= 0 ? (unsigned)k8[u[k]] : 0xFFu;
-                cu[k] = u[k] >= 0 ? (unsigned)c8[u[k]] : 0u;
-            }
+            for (int k = 0; k < K; ++k) ku[k] = u[k] >= 0 ? (unsigned)hk[u[k]] : GC_HK_COLOURED;
             ull mk[K], mp[K];  // wave masks per slot: live (kept) / pending
             int tk = 0, tp = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const bool live = u[k] >= 0 && cu[k] == GC_C8_NONE;  // coloured: dropped for good
+                const bool live = ku[k] != GC_HK_COLOURED;  // coloured (or no entry): dropped for good
                 mk[k] = __ballot(live);
-                mp[k] = __ballot(live && gc_jp_flag(g, u[k], ku[k], cv6, cv) != 0u);
+                mp[k] = __ballot(live && gc_jp_flag_h(g, u[k], ku[k], cv6, cv) != 0u);
                 tk += __popcll(mk[k]);
                 tp += __popcll(mp[k]);
             }
@@ -666,6 +674,8 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             if (lane == 0) {
                 if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
                 else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
+                if (x >= 0 && ((f & 1u) || !(f & 2u)))  // hub mirror
+                    g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
                 if (dout && ((f & 1u) || !(f & 2u)))
                     dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
                 lsum += (ull)g.deg[v];

@@ -40,6 +40,8 @@ struct GDev {
     long long nhch;
     long long hch_mul;        //   coprime to nhch, ~0.618 nhch: chunk scan order (a long row's chunks spread out)
     int hprep;                // long-row first pass on (GC_HUB_PREP)
+    unsigned char* hk;        // hub x: k8 of hub_v[x], or GC_HK_COLOURED; the hlow rows and pending lists hold
+    int* hcand;               //   hub indices, so hub JP gathers these L2-resident mirrors, not k8 / c8 / cand
     const int* hid;           // hub index of v, -1 if v is no hub
     const int* hub_v;         // vertex of hub index x
     const long long* hin_rp;  // for every u: the hubs (indices) whose rows list u
