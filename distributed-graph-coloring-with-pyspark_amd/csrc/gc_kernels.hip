@@ -344,7 +344,44 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
     words = words < 1 ? 1 : (words > GC_MEX_WORDS ? GC_MEX_WORDS : words);
     long long lmax = -1;
     ull lfail = 0, lsum = 0, lnv = 0;
-    for (long long i = blockIdx.x; i < na + nb; i += gridDim.x) {
+    // Hubs whose bitmap covers every colour in use: a wave each (first zero bit of a
+    // <= 4096-bit bitmap), not a workgroup with its barriers.  Heavy == hub while hubs are on.
+    const bool hub_waves = g.hub_w && maxc + 2 <= 32ll * g.hub_w;
+    if (hub_waves) {
+        const int lane = gc_lane();
+        const int w = threadIdx.x / GC_WAVE;
+        for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < na;
+             i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+            const int v = L.heavy[i];
+            const int x = g.hid[v];
+            const unsigned* hb = g.hbits + (long long)x * g.hub_w;
+            long long mex = -1;
+            for (int t0 = 0; t0 < words && mex < 0; t0 += GC_WAVE) {  // a zero bit lies in range
+                const int t = t0 + lane;
+                const unsigned wd = t < words ? hb[t] : 0xFFFFFFFFu;
+                const ull m = __ballot(wd != 0xFFFFFFFFu);
+                if (m) {
+                    const int l = __ffsll((long long)m) - 1;
+                    const unsigned zw = __shfl(wd, l, GC_WAVE);
+                    mex = 32ll * (t0 + l) + __builtin_ctz(~zw);
+                }
+            }
+            if (lane == 0) {
+                g.hkill[x] = 0u;  // this round's conflict flag and JP state (gc_hubs.hip)
+                g.hcur[x] = 0;
+                g.hpc[x] = 0;
+                if (g.hprep) g.hkcnt[x] = 0;
+                gc_set_cand(g, v, mex);
+                g.hk[x] = gc_k8(gc_c6_of(mex), GC_JP_UND);  // hub mirror
+                g.hcand[x] = (int)mex;
+                lmax = mex > lmax ? mex : lmax;
+                if (kbound >= 0 && mex >= kbound) lfail++;
+                lsum += (ull)g.deg[v];
+                lnv++;
+            }
+        }
+    }
+    for (long long i = (hub_waves ? na : 0) + blockIdx.x; i < na + nb; i += gridDim.x) {
         const int v = i < na ? L.heavy[i] : L.wide[i - na];
         const int d = g.deg[v];
         const long long start = g.rp[v];
