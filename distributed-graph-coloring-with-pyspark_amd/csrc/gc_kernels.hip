@@ -1080,8 +1080,50 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     GcStage st{s_stage[w], 0};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
-    // hubs: one workgroup per vertex
-    for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
+    // hubs on: a wave per hub (in-rows past bigrow are deferred to k_commit_big)
+    if (g.hub_w) {
+        for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
+             i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+            const int v = hlist[i];
+            const unsigned kv = g.k8[v];
+            const unsigned js = gc_k8_state(kv);
+            bool walk = js == GC_JP_IN;
+            int cc = 0;
+            if (walk) {
+                cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+                const long long tl = g.trp[v + 1] - g.trp[v];
+                walk = tl + (g.hin_rp[v + 1] - g.hin_rp[v]) <= g.bigrow;
+                if (lane == 0) {
+                    gc_commit_colour(g, v, cc);
+                    if (want_cround) g.cround[v] = round;
+                    lmaxc = cc > lmaxc ? cc : lmaxc;
+                    lacc++;
+                    lsum += (ull)tl;
+                    if (!walk) L.bigw[atomicAdd(&c->bigw_cnt, 1ull)] = v;  // the whole grid walks it
+                }
+            }
+            gc_stage_push(st, lane == 0 && js == GC_JP_OUT && !big, v, next, next_cnt);  // losers stay
+            if (walk) {
+                gc_hub_mark_row(g, v, cc, lane, GC_WAVE);  // gc_hubs.hip
+                if (mark || !big) {
+                    const long long ts = g.trp[v], te = g.trp[v + 1];
+                    for (long long e0 = ts; e0 < te; e0 += GC_WAVE) {
+                        const long long e = e0 + lane;
+                        bool claim = false;
+                        int x = 0;
+                        if (e < te) {
+                            x = g.tcol[e];
+                            if (mark) g.mark[x] = 1;
+                            else claim = gc_claim(g.inF, x);
+                        }
+                        gc_stage_push(st, claim, x, next, next_cnt);
+                    }
+                }
+            }
+        }
+    }
+    // hubs off: a workgroup per heavy vertex
+    for (long long i = blockIdx.x; i < (g.hub_w ? 0ll : hcnt); i += gridDim.x) {
         const int v = hlist[i];
         if (threadIdx.x == 0) {
             const unsigned kv = g.k8[v];
