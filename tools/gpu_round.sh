@@ -1,5 +1,5 @@
 set -euo pipefail
-TAG=${1:-r01_v6}
+TAG=${1:-r01}
 bash tools/gpu_profile.sh $TAG
 mkdir -p gpurun_out/$TAG/wl
 for w in rmat24 rmat26 mesh512 mesh256; do
