@@ -87,7 +87,7 @@ __device__ __forceinline__ void gc_hub_mark_row(const GDev& g, int v, int cc, in
     for (long long e = g.hin_rp[v] + t0; e < e1; e += step) gc_hub_mark(g, g.hin_col[e], cc);
 }
 // heavy entries the one-workgroup tail sweeps may take
-__device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.hub_w ? GC_TAIL_HMAX_HUB : GC_TAIL_HMAX; }
+__device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.tail_hmax; }
 
 // Which hubs sweep i (>= 1) takes, from values fixed before the kernel (gc_hubs.hip): hubs
 // off -- the undecided heavy list; hubs already started (hub_start < i) -- likewise; not

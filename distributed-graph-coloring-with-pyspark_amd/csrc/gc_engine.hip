@@ -69,6 +69,7 @@ GDev gc_view(const gc_graph* g) {
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hub_long = 0;
+    d.tail_hmax = GC_TAIL_HMAX;
     d.hch_rp = nullptr;
     d.hch_own = nullptr;
     d.hkcnt = nullptr;

@@ -284,6 +284,7 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hlowb[1] = g->hlow2[0];
     d.hlowb[2] = g->hlow2[1];
     d.hub_long = env_int("GC_HUB_LONG", GC_HUB_LONG);
+    d.tail_hmax = std::max(0, env_int("GC_TAIL_HMAX_HUB", GC_TAIL_HMAX_HUB));
     d.hch_rp = g->hch_rp;
     d.hch_own = g->hch_own;
     d.hkcnt = g->hkcnt;

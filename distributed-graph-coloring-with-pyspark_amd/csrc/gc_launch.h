@@ -33,6 +33,7 @@ struct GDev {
     // list, both pushed to it, instead of re-reading its whole row every round / sweep.
     int heavy_t;
     int hub_w;                // words per hub bitmap (0 = hubs off)
+    int tail_hmax;            // heavy entries the one-workgroup tail sweeps may take (GC_TAIL_HMAX[_HUB])
     long long hub_long;       // hub-start sweep: hubs whose hlow row exceeds this are first-read by the whole grid
     const long long* hch_rp;  // static GC_HCH-entry chunks of the hlow rows (hub x: [hch_rp[x], hch_rp[x+1]))
     const int* hch_own;       //   chunk -> hub
