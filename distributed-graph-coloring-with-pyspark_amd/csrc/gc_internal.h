@@ -31,7 +31,7 @@ typedef unsigned long long ull;
 // Vertices with deg > GC_HEAVY_T take the workgroup-per-vertex path.
 #define GC_HEAVY_T 2048
 // hubs (gc_hubs.hip): default threshold, bitmap words (4096 colours)
-#define GC_HUB_T 1024
+#define GC_HUB_T 512
 #define GC_HUB_W 128
 #define GC_HUB_LONG 16384   // hub-start sweep: longer hlow rows are first-read by the whole grid
 #define GC_HCH 1024         // entries per static chunk of an hlow row (one wave each)

@@ -30,13 +30,14 @@ SETTINGS = [
     {"GC_HUB_T": "3"},
     {"GC_HUB_T": "16", "GC_HUB_W": "2"},
     {"GC_HUB_T": "64"},
-    {"GC_HUB_T": "1024"},                                     # the default
+    {"GC_HUB_T": "512"},                                      # the default
+    {"GC_HUB_T": "1024"},
     {"GC_HUB_T": "off"},
     {"GC_HUB_T": "0", "GC_HUB_LONG": "4"},                    # long rows first-read by the whole grid
     {"GC_HUB_T": "2", "GC_HUB_LONG": "0"},                    # ... every row
     {"GC_HUB_T": "0", "GC_HUB_LONG": "0", "GC_HUB_PREP": "off"},  # every row walked by its wave
 ]
-IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T1024", "off", "T0long4", "T2long0", "T0noprep"]
+IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
