@@ -168,12 +168,17 @@ int gc_alloc_run_state(gc_graph* g) {
 
 namespace {
 
-// Optional per-launch event bracketing (gc_options.kernel_timing).
+// Optional event timing of kernel classes (gc_options.kernel_timing).  A RUN of
+// consecutive launches of one timed class (a round's JP sweeps, say) is bracketed by ONE
+// event pair: bracketing every launch cost ~5 us per launch in gaps (R-MAT-24: ~10k sweep
+// launches per colouring).  The run's time includes the launch gaps inside it, so the
+// class time is an upper bound of its kernels' busy time.  Runs are closed at every host
+// synchronisation and at the end of every round, so no host wait is ever inside one.
 struct KTimer {
     gc_graph* g;
-    unsigned mask;  // kernel classes to bracket with events (bit GC_K_*)
+    unsigned mask;  // kernel classes to time (bit GC_K_*)
     gc_stats* st;
-    bool on_now = false;
+    int run_cls = -1;  // class of the open run (-1: none)
     std::vector<std::pair<int, size_t>> recs;  // (class, event index of start)
     size_t used = 0;
     hipEvent_t ev() {
@@ -186,16 +191,21 @@ struct KTimer {
     }
     void begin(int cls) {
         if (st) st->k_launches[cls]++;
-        on_now = (mask >> cls) & 1u;
-        if (!on_now) return;
+        if (cls == run_cls) return;  // the open run goes on
+        close();
+        if (!((mask >> cls) & 1u)) return;
+        run_cls = cls;
         recs.push_back({cls, used});
         hipEventRecord(ev(), g->stream);
     }
-    void end() {
-        if (!on_now) return;
+    void end() {}
+    void close() {
+        if (run_cls < 0) return;
         hipEventRecord(ev(), g->stream);
+        run_cls = -1;
     }
     void collect() {
+        close();
         if (!mask || !st) return;
         for (auto& r : recs) {
             float ms = 0.f;
@@ -224,6 +234,7 @@ struct Run {
     bool need_pblock() const { return g->maxdeg > d.heavy_t || g->maxdeg >= 64; }  // heavy_t is final once hubs are set
 
     int sync_ctl() {
+        kt.close();
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipStreamSynchronize(s));
         if (debug) {
@@ -241,6 +252,7 @@ struct Run {
     }
     // copy the device records [drained, round) out and restart the device buffer
     int drain_records() {
+        kt.close();
         const long long r = g->hctl->round;
         const long long cnt = r - drained;
         if (cnt > 0) {
@@ -282,6 +294,7 @@ struct Run {
         kt.begin(GC_K_OTHER);
         gcl_close(d, L, mode, s, big);
         kt.end();
+        kt.close();  // a round's runs end with it
     }
     void launch_sweeps(int from, int to) {  // sweeps from..to inclusive
         for (int i = from; i <= to; ++i) {
@@ -318,6 +331,7 @@ struct Run {
     // a batch of rounds followed by an async snapshot of the control block
     int enqueue_batch(int B, int S, int slot) {
         for (int b = 0; b < B; ++b) enqueue_round(S);
+        kt.close();
         GC_HIP(hipMemcpyAsync(&g->hsnap[slot], g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipEventRecord(g->evsnap[slot], s));
         return GC_OK;

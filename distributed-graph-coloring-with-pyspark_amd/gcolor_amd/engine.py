@@ -132,11 +132,13 @@ class DeviceGraph:
     def symmetric(self):
         return bool(self.flags & nat.GC_GRAPH_SYMMETRIC)
 
-    def export(self):
+    def export(self, col=True):
+        """Host copy of the device CSR (rows as the engine stores them); col=False copies
+        only the row offsets (returns (rp, None))."""
         rp = np.empty(self.n + 1, np.int64)
-        col = np.empty(max(self.nnz, 1), np.int32)
-        nat.check("gc_graph_export", self._lib.gc_graph_export(self._h, _ptr(rp), _ptr(col)))
-        return rp, col[: self.nnz]
+        c = np.empty(max(self.nnz, 1), np.int32) if col else None
+        nat.check("gc_graph_export", self._lib.gc_graph_export(self._h, _ptr(rp), _ptr(c)))
+        return rp, (c[: self.nnz] if col else None)
 
     def lower_counts(self):
         """nlow[v]: entries at the head of exported row v that rank below v (deg, pos)."""

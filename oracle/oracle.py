@@ -91,6 +91,51 @@ def c_color(rp, col, variant="A", k=None, e1=True, max_rounds=1 << 16):
     return out
 
 
+_omp = None
+OMP_LIB_PATH = os.path.join(HERE, "build", "libgcolor_omp.so")
+
+
+def load_omp():
+    global _omp
+    if _omp is None:
+        if not os.path.exists(OMP_LIB_PATH):
+            build()
+        lib = ctypes.CDLL(OMP_LIB_PATH)
+        P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        lib.omp_color.argtypes = [P, P, I64, I32, I32, P, P, P, P, P, P, P, I64, ctypes.POINTER(I64),
+                                  ctypes.POINTER(I64)]
+        lib.omp_color.restype = ctypes.c_int
+        _omp = lib
+    return _omp
+
+
+def omp_color(rp, col, symmetric=False, threads=0, want_rounds=True, max_rounds=1 << 17):
+    """The multi-core C restatement (gcolor_omp.c, variant A, unbounded, E1 on): the CPU
+    baseline of bench.py.  threads=0: OpenMP's default (OMP_NUM_THREADS / all cores)."""
+    lib = load_omp()
+    rp = np.ascontiguousarray(rp, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    n = rp.shape[0] - 1
+    color = np.empty(max(n, 1), np.int32)
+    cround = np.empty(max(n, 1), np.int32) if want_rounds else None
+    cap = max_rounds if want_rounds else 0
+    per = {key: np.zeros(max(cap, 1), np.int64) for key in ("U", "F", "maxmex", "accepted", "seeds")}
+    rounds, reseeds = ctypes.c_int64(), ctypes.c_int64()
+    pp = (lambda a: _ptr(a)) if want_rounds else (lambda a: None)
+    st = lib.omp_color(_ptr(rp), _ptr(col), n, 1 if symmetric else 0, int(threads), _ptr(color),
+                       None if cround is None else _ptr(cround), pp(per["U"]), pp(per["F"]), pp(per["maxmex"]),
+                       pp(per["accepted"]), pp(per["seeds"]), cap, ctypes.byref(rounds), ctypes.byref(reseeds))
+    if st < 0:
+        raise RuntimeError(f"omp_color failed with status {st}")
+    r = rounds.value
+    out = {"status": st, "colors": color[:n], "colored_round": None if cround is None else cround[:n],
+           "rounds": r, "reseeds": reseeds.value, "max_color": int(color[:n].max()) if n else -1}
+    if want_rounds:
+        for key, arr in per.items():
+            out["round_" + key] = arr[:r].copy()
+    return out
+
+
 def c_validate(rp, col, colors):
     lib = load()
     rp = np.ascontiguousarray(rp, dtype=np.int64)

@@ -1,0 +1,98 @@
+"""Full-size parity on the BASELINE.json single-GPU configs (coloring.py:73-132 semantics).
+
+* C2 (uniform 10M / max-degree 16, seed 42): bit-exact against the single-thread oracle
+  (oracle/gcolor_oracle.c) -- colours and every per-round record.
+* C3 (R-MAT scale 24): the hub engine (default) bit-exact against the row-scan engine
+  (GC_HUB_T=off) and against the multi-core restatement oracle/gcolor_omp.c (itself
+  bit-exact with the oracle, tests/test_oracle_omp.py), per-round records included;
+  valid; rounds and colours pinned to the numbers measured in round 1.
+* C4 on one GPU (mesh 512^3): valid, 2 colours (the wavefront 2-colours the bipartite
+  mesh), 1531 rounds (3 * (512 - 2) + 1, the last one empty), bit-exact
+  against the multi-core restatement.
+* north star (R-MAT scale 26): valid, rounds / colours pinned.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds")
+
+
+def _same_records(g, o):
+    assert g.status == o["status"] == 0
+    assert np.array_equal(g.colors, o["colors"])
+    for k in KEYS:
+        assert np.array_equal(np.asarray(getattr(g, k)), np.asarray(o[k])), k
+    assert g.reseeds == o["reseeds"]
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+
+
+def test_c2_uniform_10M_against_oracle():
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    rp, col = uniform_csr(10_000_000, 16, 42)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("A")
+        assert dg.validate() == (0, 0)
+    o = oracle.c_color(rp, col, "A")
+    _same_records(g, o)
+    assert np.array_equal(g.colored_round, o["colored_round"])
+    assert (g.rounds, g.max_color + 1) == (15, 10)
+
+
+@pytest.fixture(scope="module")
+def rmat24():
+    from gcolor_amd.engine import DeviceGraph
+    dg = DeviceGraph.rmat(24, 16, seed=1)
+    yield dg
+    dg.close()
+
+
+def test_c3_rmat24_hubs_match_row_scan_engine(rmat24, monkeypatch):
+    g = rmat24.color("A")
+    assert rmat24.validate() == (0, 0)
+    assert (g.rounds, g.max_color + 1) == (903, 899)
+    monkeypatch.setenv("GC_HUB_T", "off")
+    r = rmat24.color("A")
+    monkeypatch.delenv("GC_HUB_T")
+    _same_records(g, {"status": r.status, "colors": r.colors, "reseeds": r.reseeds,
+                      **{k: getattr(r, k) for k in KEYS}})
+    assert np.array_equal(g.colored_round, r.colored_round)
+
+
+def test_c3_rmat24_against_multicore_restatement(rmat24):
+    g = rmat24.color("A")
+    rp, col = rmat24.export()
+    o = oracle.omp_color(rp, col, symmetric=True, threads=_threads())
+    _same_records(g, o)
+    assert np.array_equal(g.colored_round, o["colored_round"])
+
+
+def test_c4_mesh512():
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.mesh(512, 512, 512) as dg:
+        assert (dg.n, dg.nnz) == (134_217_728, 803_733_504)
+        g = dg.color("A")
+        assert dg.validate() == (0, 0)
+        assert g.max_color + 1 == 2 and g.rounds == 1531
+        rp, col = dg.export()
+    o = oracle.omp_color(rp, col, symmetric=True, threads=_threads())
+    del rp, col
+    _same_records(g, o)
+
+
+def test_north_star_rmat26_valid():
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(26, 16, seed=1) as dg:
+        g = dg.color("A", want_rounds=False, want_colors=False)
+        assert dg.validate() == (0, 0)
+        assert (g.rounds, g.max_color + 1) == (1355, 1350)

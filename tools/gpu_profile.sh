@@ -1,32 +1,31 @@
 #!/bin/bash
-# One GPU session on the MI355X box (run through gpurun from the repo root):
-#   1. the GPU parity suite, 2. the default bench line, 3. rocprofv3 kernel-trace stats of
-#   the same bench command, 4./5. FETCH_SIZE and WRITE_SIZE PMC passes (separate runs,
-#   counters only -- never combined with other tracing).
+# One profiling session of one bench workload on the MI355X box (run through gpurun from
+# the repo root):
+#   1. the bench line, 2. rocprofv3 kernel-trace stats of the same bench command,
+#   3./4. FETCH_SIZE and WRITE_SIZE PMC passes (separate runs, counters only -- never
+#   combined with other tracing), 5. the per-kernel summary profiles/pmc/<workload>.json
+#   that bench.py reads for `traffic` (copied into the tree; commit it).
 # Every GPU step has its own time limit and the steps are chained: the first failure ends
-# the script.  Output lands in gpurun_out/ (merged back by gpurun).
-# Usage: bash tools/gpu_profile.sh [TAG] [extra bench args...]
+# the script.  Output lands in gpurun_out/<tag>/<workload> (merged back by gpurun).
+# Usage: bash tools/gpu_profile.sh TAG WORKLOAD [extra bench args...]
 set -euo pipefail
-TAG=${1:-r01}
-shift || true
+TAG=$1; WL=$2
+shift 2
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/$TAG
+OUT=$ROOT/gpurun_out/$TAG/$WL
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-SKIP_TESTS=${SKIP_TESTS:-0}
-if [ "$SKIP_TESTS" != "1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-    > "$OUT/pytest_gpu.log" 2>&1
-  tail -3 "$OUT/pytest_gpu.log"
-fi
-timeout -k 10 300 python -u bench.py --json-out "$OUT/bench.json" "$@" > "$OUT/bench.log" 2>&1
-tail -1 "$OUT/bench.log"
+timeout -k 10 400 python -u bench.py --workload $WL --json-out "$OUT/bench.json" "$@" > "$OUT/bench.log" 2>&1
+tail -1 "$OUT/bench.log" | cut -c1-600
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/trace" -o run -- \
-  python "$ROOT/bench.py" --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1
+  python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$OUT/trace.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -T -f csv -d "$OUT/pmc_fetch" -o run -- \
-  python "$ROOT/bench.py" --no-cpu-baseline --steps 2 --warmup 0 "$@" > "$OUT/pmc_fetch.log" 2>&1
+  python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --steps 2 --warmup 0 "$@" > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -T -f csv -d "$OUT/pmc_write" -o run -- \
-  python "$ROOT/bench.py" --no-cpu-baseline --steps 2 --warmup 0 "$@" > "$OUT/pmc_write.log" 2>&1
+  python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --steps 2 --warmup 0 "$@" > "$OUT/pmc_write.log" 2>&1
+cd "$ROOT"
+python tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.json"
+head -c 1500 "$OUT/pmc_summary.json"
 echo "gpu_profile done: $OUT"
