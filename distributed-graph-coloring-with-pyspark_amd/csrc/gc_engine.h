@@ -78,6 +78,8 @@ struct gc_graph {
     std::vector<hipEvent_t> evpool;
     bool has_run_state = false;
     bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
+    int part_prio = 0;         // rank the rows are partitioned for (gc_set_priority)
+    uint64_t part_seed = 0;
 };
 
 void gc_set_error(const char* fmt, ...);
@@ -99,6 +101,9 @@ void gc_hubs_free(gc_graph* g);
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
                        gc_stats* st);  // gc_variant_b.hip
 void gc_free_all(gc_graph* g);
+int gc_set_priority(gc_graph* g, int prio, uint64_t seed);  // gc_priority.hip: rows partitioned for the rank
+int gc_color_speculative(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
+                         gc_stats* st);  // gc_priority.hip
 GDev gc_view(const gc_graph* g);
 GLists gc_lists(const gc_graph* g);
 static inline int gc_grid_for_waves(long long items, int cap = 2048) {

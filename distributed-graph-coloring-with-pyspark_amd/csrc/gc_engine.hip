@@ -76,6 +76,7 @@ GDev gc_view(const gc_graph* g) {
     d.nhch = 0;
     d.hch_mul = 1;
     d.hprep = 0;
+    d.hub_scan = 0;
     d.hk = nullptr;
     d.hcand = nullptr;
     d.hid = nullptr;
@@ -528,10 +529,18 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         stats->round_seeds = keep.round_seeds;
         stats->max_color = -1;
     }
+    if (opt->variant == GC_VARIANT_B && (opt->priority != GC_PRIORITY_REF || opt->speculative)) {
+        gc_set_error("gc_color: seeded priorities and the speculative mode are variant A only");
+        return GC_EINVAL;
+    }
+    // the rows are partitioned for the rank of this colouring (re-partitioned when it changes)
+    if ((rc = gc_set_priority(g, opt->priority, opt->seed))) return rc;
     if (opt->variant == GC_VARIANT_B) return gc_color_variant_b(g, opt, colors_out, cround_out, stats);
+    if (opt->speculative) return gc_color_speculative(g, opt, colors_out, cround_out, stats);
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
-    if ((rc = gc_hubs_prepare(g, run.d))) return rc;
+    // hubs rank above every light vertex only under (deg, pos): seeded ranks use row scans
+    if (opt->priority == GC_PRIORITY_REF && (rc = gc_hubs_prepare(g, run.d))) return rc;
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
     rc = run.go(colors_out, cround_out);

@@ -213,7 +213,7 @@ static int partition_rows(gc_graph* g) {
     int* out = nullptr;
     GC_HIP(hipMalloc((void**)&out, sizeof(int) * (size_t)g->nnz));
     const int grid = gc_grid_for_waves(g->n, 8192);
-    gcl_rank_flags(g->rp, g->col, g->deg, (int)g->n, g->nlow, grid, s);
+    gcl_rank_flags(g->rp, g->col, reinterpret_cast<const unsigned*>(g->deg), (int)g->n, g->nlow, grid, s);
     gcl_partition_rows(g->rp, g->col, g->deg, g->nlow, (int)g->n, out, grid, s);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
         hipFree(out);

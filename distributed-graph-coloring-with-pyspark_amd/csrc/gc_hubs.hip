@@ -49,6 +49,22 @@ __global__ void k_hub_ids(const int* deg, long long n, int T, const long long* p
     }
 }
 
+// hub indices in rank order (deg, pos) -- the rank of coloring.py:64 -- so that an hlow
+// row sorted by hub index lists its lower-rank hubs lowest rank first (gc_hub_scan_wave)
+__global__ void k_hub_keys(const int* deg, const int* hub_v, long long H, ull* keys) {
+    for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < H; x += (long long)gridDim.x * blockDim.x) {
+        const int v = hub_v[x];
+        keys[x] = ((ull)(unsigned)deg[v] << 32) | (ull)(unsigned)v;
+    }
+}
+__global__ void k_hub_reindex(const ull* keys, long long H, int* hid, int* hub_v) {
+    for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < H; x += (long long)gridDim.x * blockDim.x) {
+        const int v = (int)(keys[x] & 0xFFFFFFFFull);
+        hub_v[x] = v;
+        hid[v] = (int)x;
+    }
+}
+
 // one wave per hub row
 __global__ void k_hub_count(const long long* rp, const int* col, const int* hub_v, long long H, ull* cnt) {
     const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
@@ -170,6 +186,24 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMalloc((void**)&g->hid, sizeof(int) * (size_t)std::max<long long>(n, 1)));
     GC_HIP(hipMalloc((void**)&g->hub_v, sizeof(int) * (size_t)H));
     hipLaunchKernelGGL(k_hub_ids, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, g->deg, n, T, pos, g->hid, g->hub_v);
+    {  // re-index the hubs in rank order
+        ull *k0 = nullptr, *k1 = nullptr;
+        GC_HIP(hipMalloc((void**)&k0, sizeof(ull) * (size_t)H));
+        GC_HIP(hipMalloc((void**)&k1, sizeof(ull) * (size_t)H));
+        hipLaunchKernelGGL(k_hub_keys, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, g->deg, g->hub_v, H, k0);
+        size_t bytes = 0;
+        GC_HIP(rocprim::radix_sort_keys(nullptr, bytes, k0, k1, (size_t)H, 0, 64, s));
+        void* tmp = nullptr;
+        GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+        const hipError_t e = rocprim::radix_sort_keys(tmp, bytes, k0, k1, (size_t)H, 0, 64, s);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL(k_hub_reindex, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const ull*)k1, H, g->hid, g->hub_v);
+        hipStreamSynchronize(s);
+        hipFree(tmp);
+        hipFree(k0);
+        hipFree(k1);
+        GC_HIP(e);
+    }
     // hub transpose: reuse pos as the per-target counter
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
     const int hgrid = (int)std::max<long long>(1, std::min<long long>((H + 3) / 4, 8192));
@@ -213,6 +247,19 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMalloc((void**)&g->hlen, sizeof(int) * (size_t)H));
     hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
                        g->hlow_rp, g->hlow_col);
+    if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
+        size_t bytes = 0;
+        GC_HIP(rocprim::segmented_radix_sort_keys(nullptr, bytes, g->hlow_col, g->hpend[0], (unsigned)EL, (unsigned)H,
+                                                  g->hlow_rp, g->hlow_rp + 1, 0, 32, s));
+        void* tmp = nullptr;
+        GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+        const hipError_t e = rocprim::segmented_radix_sort_keys(tmp, bytes, g->hlow_col, g->hpend[0], (unsigned)EL,
+                                                                (unsigned)H, g->hlow_rp, g->hlow_rp + 1, 0, 32, s);
+        hipStreamSynchronize(s);
+        hipFree(tmp);
+        GC_HIP(e);
+        std::swap(g->hlow_col, g->hpend[0]);  // the unsorted copy becomes working memory
+    }
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
     hipLaunchKernelGGL(k_hch_count, dim3(grid_of(H + 1)), dim3(GC_BLOCK), 0, s, g->hlow_rp, H, pos);
     GC_HIP(hipMalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
@@ -291,11 +338,13 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hk = g->hk;
     d.hcand = g->hcand;
     d.nhch = g->nhch;
-    d.hprep = env_int("GC_HUB_PREP", 1) > 0 && g->nhch > 0 && d.hub_long >= 0;
+    d.hub_scan = env_int("GC_HUB_SCAN", 1) > 0;
+    d.hprep = !d.hub_scan && env_int("GC_HUB_PREP", 1) > 0 && g->nhch > 0 && d.hub_long >= 0;
     long long m = std::max<long long>(1, (long long)(0.6180339887 * (double)g->nhch));
     while (std::gcd(m, std::max<long long>(g->nhch, 1ll)) != 1) ++m;
     d.hch_mul = m;
     GC_HIP(hipMemsetAsync(g->hrow, 0, sizeof(int) * (size_t)g->nhub, g->stream));  // full rows again
+    GC_HIP(hipMemsetAsync(g->hlen, 0, sizeof(int) * (size_t)g->nhub, g->stream));  // scan: no coloured prefix yet
     return GC_OK;
 }
 

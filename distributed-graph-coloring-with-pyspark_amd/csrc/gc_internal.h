@@ -319,3 +319,7 @@ __device__ __forceinline__ unsigned gc_k8_state(unsigned k) { return k & 3u; }
 __device__ __forceinline__ bool gc_rank_lt(int du, int u, int dv, int v) {
     return du < dv || (du == dv && u < v);
 }
+// the same order over a 32-bit key (deg, or a seeded priority: gc_priority.hip)
+__device__ __forceinline__ bool gc_rank_lt_key(unsigned ku, int u, unsigned kv, int v) {
+    return ku < kv || (ku == kv && u < v);
+}

@@ -483,23 +483,33 @@ __device__ __forceinline__ void gc_set_state(GDev& g, int v, unsigned kv, unsign
 // every lane).  Hub rows of lower-rank hubs are short (R-MAT-24: at most ~1.7k entries),
 // while a hub's evaluation is a chain of ~10 dependent loads: a wave per hub keeps 4x as
 // many hubs in flight as a workgroup per hub, and its appends are counted in registers.
-__device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
+// The hub's state words (hpc, hcur, hrow, hlen, hkcnt, hlow_rp) come in prefetched: the
+// sweep loads them for 64 hubs at once, one per lane (gc_jp_sweep), instead of as the
+// first links of every hub's own chain of dependent loads.
+struct GcHubPre {
+    long long base, full;  // hlow_rp[x], its static row length
+    int enc, hc0, hrow, hlen, hkcnt;
+};
+__device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv, GcHubPre p) {
     const int lane = gc_lane();
     const ull lt = gc_lanemask_lt();
     const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
-    int enc = g.hpc[x];
-    const int hc0 = g.hcur[x];
+    int enc = p.enc;
+    const int hc0 = p.hc0;
     const bool first = hc0 == 0;
+    int hrow = p.hrow, hlen = p.hlen;
     if (hc0 == 2) {  // the grid read this long row in the hub-start sweep (gc_hub_first_long): adopt its
         enc |= 1;    // kept copy and its pending list (half 1)
+        hrow = hrow == 1 ? 2 : 1;
+        hlen = p.hkcnt;
         if (lane == 0) {
-            g.hrow[x] = g.hrow[x] == 1 ? 2 : 1;
-            g.hlen[x] = g.hkcnt[x];
+            g.hrow[x] = hrow;
+            g.hlen[x] = hlen;
             g.hcur[x] = 1;
         }
     }
     const int sel = enc & 1, cnt = enc >> 1;
-    const long long base = g.hlow_rp[x];
+    const long long base = p.base;
     const int* __restrict__ src = g.hpend[sel] + base;
     int* dst = g.hpend[sel ^ 1] + base;
     int nn = 0, nk = 0;  // wave-uniform append counts
@@ -524,9 +534,9 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
             nn += __popcll(m);
         }
     }
-    const int hr = first ? g.hrow[x] : 0;
+    const int hr = first ? hrow : 0;
     if (first) {
-        const int len = hr ? g.hlen[x] : (int)(g.hlow_rp[x + 1] - base);
+        const int len = hr ? hlen : (int)p.full;
         const int* __restrict__ hc = g.hlowb[hr] + base;
         int* keep = g.hlowb[hr == 1 ? 2 : 1] + base;
         // GC_HUB_UNR entries per lane in flight; every flag (and its cand[] gather, for
@@ -568,6 +578,65 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv) {
         if (!out) g.hpc[x] = (nn << 1) | (sel ^ 1);
     }
     return out ? 1u : (nn > 0 ? 2u : 0u);
+}
+
+// JP step of hub x by a resumable scan of its row (hubs on, GC_HUB_SCAN; the default).
+// Hub indices are assigned in rank order (gc_hubs.hip) and every hlow row is sorted by
+// them, so the row lists the hub's lower-rank hubs lowest rank first.  The hub walks it
+// from where it stopped: an entry coloured, OUT or of another candidate can never block
+// it again this round (states only move UND -> IN / OUT inside a round, candidates are
+// fixed), so the walk stops at the first same-candidate UNDECIDED entry (the cursor, hpc),
+// and the hub is OUT as soon as a same-candidate entry is IN, IN once the end is reached.
+// Exactly the JP rule over the row, with no per-round copies: the kept-row and
+// pending-list rewrites of gc_hub_jp_wave wrote ~2x the live rows every round (R-MAT-24:
+// 60 GB of writes per colouring in the sweeps), and lower-rank winners sit near the row
+// start, so an OUT hub usually stops early.  Colours are final, so the coloured prefix of
+// the row is skipped for good: hlen holds its length (reset per colouring).
+// p.hc0 = hcur (0: first evaluation this round), p.enc = cursor, p.hlen = coloured prefix.
+__device__ unsigned gc_hub_scan_wave(const GDev& g, int x, unsigned cv6, int cv, GcHubPre p) {
+    const int lane = gc_lane();
+    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
+    const bool first = p.hc0 == 0;
+    const int full = (int)p.full;
+    const int* __restrict__ row = g.hlow_col + p.base;
+    int pos = first ? p.hlen : p.enc;
+    bool out = false, prefix = first;
+    int block = -1, nstart = full;
+    for (int e0 = pos; e0 < full && !out && block < 0; e0 += GC_HUB_UNR * GC_WAVE) {
+        int u[GC_HUB_UNR];
+#pragma unroll
+        for (int k = 0; k < GC_HUB_UNR; ++k) {
+            const int e = e0 + k * GC_WAVE + lane;
+            u[k] = e < full ? row[e] : -1;
+        }
+        unsigned ku[GC_HUB_UNR];
+#pragma unroll
+        for (int k = 0; k < GC_HUB_UNR; ++k) ku[k] = u[k] >= 0 ? (unsigned)hk[u[k]] : GC_HK_COLOURED;
+        unsigned fl[GC_HUB_UNR];
+#pragma unroll
+        for (int k = 0; k < GC_HUB_UNR; ++k) fl[k] = ku[k] != GC_HK_COLOURED ? gc_jp_flag_h(g, u[k], ku[k], cv6, cv) : 0u;
+#pragma unroll
+        for (int k = 0; k < GC_HUB_UNR; ++k) {
+            if (__ballot(fl[k] == 1u)) out = true;
+            const ull mb = __ballot(fl[k] == 2u);
+            if (mb && block < 0) block = e0 + k * GC_WAVE + __builtin_ctzll(mb);
+            if (prefix) {  // first non-coloured entry: the end of the coloured prefix
+                const ull ml = __ballot(u[k] >= 0 && ku[k] != GC_HK_COLOURED);
+                if (ml) {
+                    nstart = e0 + k * GC_WAVE + __builtin_ctzll(ml);
+                    prefix = false;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        if (first) {
+            g.hcur[x] = 1;
+            if (nstart > p.hlen) g.hlen[x] = nstart;
+        }
+        if (!out && block >= 0) g.hpc[x] = block;
+    }
+    return out ? 1u : (block >= 0 ? 2u : 0u);
 }
 
 // First read of the LONG hub rows (static length > hub_long) in the sweep that starts the
@@ -680,47 +749,84 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     __shared__ int s_hstage[GC_STAGE_CAP];
     GcStage hst{s_hstage, 0};
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
-        for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
-             i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-            const int v = hlist[i];
-            const unsigned kv = k8[v];
-            const unsigned cv6 = gc_k8_cand(kv);
-            const int cv = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
-            const int x = g.hid[v];
-            unsigned f = 0;
-            if (x >= 0) {
-                if (g.hkill[x]) {
-                    f = 1u;
-                } else if (hub_first && g.hlow_rp[x + 1] - g.hlow_rp[x] > g.hub_long) {
-                    f = 2u;  // long row: read by the grid below (gc_hub_first_long), evaluated next sweep
-                    if (lane == 0) g.hcur[x] = 2;
-                } else {
-                    f = gc_hub_jp_wave(g, x, cv6, cv);
-                }
-            } else {  // not a hub (cannot happen while heavy_t is the hub threshold): row scan
-                const int dl = g.nlow[v];
-                const long long start = g.rp[v];
-                unsigned lf = 0;
-                for (int e = lane; e < dl; e += GC_WAVE) {
-                    const int u = g.col[start + e];
-                    lf |= gc_jp_flag(g, u, k8[u], cv6, cv);
-                }
-                f = (__ballot((lf & 1u) != 0u) ? 1u : 0u) | (__ballot((lf & 2u) != 0u) ? 2u : 0u);
+        // a wave's hubs are i = wid + j * waves; lane l loads the state of hub j0 + l, so a
+        // hub's evaluation starts at its row read
+        const long long waves = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
+        const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+        for (long long i0 = wid; i0 < hcnt; i0 += waves * GC_WAVE) {
+            const long long il = i0 + (long long)lane * waves;
+            int pv = -1, px = -1, pcv = 0;
+            unsigned pkv = 0, pkill = 0;
+            GcHubPre pp{0, 0, 0, 0, 0, 0, 0};
+            if (il < hcnt) {
+                pv = hlist[il];
+                pkv = k8[pv];
+                pcv = gc_k8_cand(pkv) == GC_K8_BIG ? g.cand[pv] : (int)gc_k8_cand(pkv);
+                px = g.hid[pv];
             }
-            gc_stage_push(st, lane == 0 && (f & 3u) == 2u, v, ho, ho_cnt);  // undecided hub
-            if (lane == 0) {
-                if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
-                else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
-                if (x >= 0 && ((f & 1u) || !(f & 2u)))  // hub mirror
-                    g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
-                if (dout && ((f & 1u) || !(f & 2u)))
-                    dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
-                lsum += (ull)g.deg[v];
-                lnv++;
+            if (px >= 0) {
+                pkill = g.hkill[px];
+                pp.base = g.hlow_rp[px];
+                pp.full = g.hlow_rp[px + 1] - pp.base;
+                pp.enc = g.hpc[px];
+                pp.hc0 = g.hcur[px];
+                pp.hrow = g.hrow[px];
+                pp.hlen = g.hlen[px];
+                pp.hkcnt = g.hkcnt[px];
+            }
+            const long long left = (hcnt - i0 + waves - 1) / waves;
+            const int nj = left < GC_WAVE ? (int)left : GC_WAVE;
+            for (int j = 0; j < nj; ++j) {
+                const int v = __shfl(pv, j, GC_WAVE);
+                const unsigned kv = (unsigned)__shfl((int)pkv, j, GC_WAVE);
+                const unsigned cv6 = gc_k8_cand(kv);
+                const int cv = __shfl(pcv, j, GC_WAVE);
+                const int x = __shfl(px, j, GC_WAVE);
+                unsigned f = 0;
+                if (x >= 0) {
+                    GcHubPre q;
+                    q.base = __shfl(pp.base, j, GC_WAVE);
+                    q.full = __shfl(pp.full, j, GC_WAVE);
+                    q.enc = __shfl(pp.enc, j, GC_WAVE);
+                    q.hc0 = __shfl(pp.hc0, j, GC_WAVE);
+                    q.hrow = __shfl(pp.hrow, j, GC_WAVE);
+                    q.hlen = __shfl(pp.hlen, j, GC_WAVE);
+                    q.hkcnt = __shfl(pp.hkcnt, j, GC_WAVE);
+                    if (__shfl((int)pkill, j, GC_WAVE)) {
+                        f = 1u;
+                    } else if (g.hub_scan) {
+                        f = gc_hub_scan_wave(g, x, cv6, cv, q);
+                    } else if (hub_first && q.full > g.hub_long) {
+                        f = 2u;  // long row: read by the grid below (gc_hub_first_long), evaluated next sweep
+                        if (lane == 0) g.hcur[x] = 2;
+                    } else {
+                        f = gc_hub_jp_wave(g, x, cv6, cv, q);
+                    }
+                } else {  // not a hub (cannot happen while heavy_t is the hub threshold): row scan
+                    const int dl = g.nlow[v];
+                    const long long start = g.rp[v];
+                    unsigned lf = 0;
+                    for (int e = lane; e < dl; e += GC_WAVE) {
+                        const int u = g.col[start + e];
+                        lf |= gc_jp_flag(g, u, k8[u], cv6, cv);
+                    }
+                    f = (__ballot((lf & 1u) != 0u) ? 1u : 0u) | (__ballot((lf & 2u) != 0u) ? 2u : 0u);
+                }
+                gc_stage_push(st, lane == 0 && (f & 3u) == 2u, v, ho, ho_cnt);  // undecided hub
+                if (lane == 0) {
+                    if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
+                    else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
+                    if (x >= 0 && ((f & 1u) || !(f & 2u)))  // hub mirror
+                        g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
+                    if (dout && ((f & 1u) || !(f & 2u)))
+                        dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
+                    lsum += (ull)g.deg[v];
+                    lnv++;
+                }
             }
         }
         gc_stage_flush(st, ho, ho_cnt);  // st is the light list's stage from here on
-        if (hub_first) gc_hub_first_long(g);
+        if (hub_first && !g.hub_scan) gc_hub_first_long(g);
         hcnt = 0;
     }
     for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
@@ -1739,14 +1845,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_finalize(GDev g) {
 // graph helpers
 // ------------------------------------------------------------------------------------
 // Mark every adjacency entry whose neighbour does NOT rank below the row's vertex
-// (bit 31 of col; rank = (deg, pos), coloring.py:64) and count the lower ones.  A
-// segmented radix sort on bit 31 then lists lower-rank neighbours first (gc_graph.hip).
-__global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, int* col, const int* deg, int n,
+// (bit 31 of col; rank = (key, pos): key = deg for the reference's coloring.py:64, or a
+// seeded priority, gc_priority.hip) and count the lower ones; k_partition_rows then lists
+// lower-rank neighbours first (gc_graph.hip).
+__global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, int* col, const unsigned* key, int n,
                                                          int* nlow) {
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cnt[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ unsigned s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
@@ -1754,11 +1861,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, in
          chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long v = chunk * GC_WAVE + lane;
         const bool valid = v < n;
-        const int d = valid ? deg[v] : 0;
+        const int d = valid ? (int)(rp[v + 1] - rp[v]) : 0;
         s_start[w][lane] = valid ? rp[v] : 0;
         s_cnt[w][lane] = 0;
         s_v[w][lane] = (int)v;
-        s_d[w][lane] = d;
+        s_d[w][lane] = valid ? key[v] : 0u;
         const int incl = gc_wave_incl_scan(d);
         const int excl = incl - d;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -1770,7 +1877,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, in
             if (e < total) {
                 const long long ei = s_start[w][o] + (e - eo);
                 const int u = col[ei];
-                const bool lower = gc_rank_lt(deg[u], u, s_d[w][o], s_v[w][o]);
+                const bool lower = gc_rank_lt_key(key[u], u, s_d[w][o], s_v[w][o]);
                 if (lower) atomicAdd(&s_cnt[w][o], 1);
                 else col[ei] = (int)((unsigned)u | 0x80000000u);
             }
@@ -1962,8 +2069,8 @@ void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStr
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, heavy);
     hipLaunchKernelGGL(k_validate_heavy, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, colors, (const int*)heavy);
 }
-void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, deg, n, nlow);
+void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, key, n, nlow);
 }
 void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
                         int grid, hipStream_t s) {

@@ -41,6 +41,7 @@ struct GDev {
     long long nhch;
     long long hch_mul;        //   coprime to nhch, ~0.618 nhch: chunk scan order (a long row's chunks spread out)
     int hprep;                // long-row first pass on (GC_HUB_PREP)
+    int hub_scan;             // hub JP by a resumable scan of the rank-sorted row (GC_HUB_SCAN, default on)
     unsigned char* hk;        // hub x: k8 of hub_v[x], or GC_HK_COLOURED; the hlow rows and pending lists hold
     int* hcand;               //   hub indices, so hub JP gathers these L2-resident mirrors, not k8 / c8 / cand
     const int* hid;           // hub index of v, -1 if v is no hub
@@ -94,7 +95,7 @@ void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long lo
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
 void gcl_shard_flip(const GDev& g, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
-void gcl_rank_flags(const long long* rp, int* col, const int* deg, int n, int* nlow, int grid, hipStream_t s);
+void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s);
 void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
                         int grid, hipStream_t s);
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);

@@ -45,6 +45,8 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     if (!g || !out) { gc_set_error("gc_shard_create: null argument"); return GC_EINVAL; }
     if (lo < 0 || hi < lo || hi > g->n) { gc_set_error("gc_shard_create: bad range [%lld, %lld)", (long long)lo, (long long)hi); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
+    int rc0 = gc_set_priority(g, GC_PRIORITY_REF, 0);  // shards run the reference's (deg, pos) rank
+    if (rc0) return rc0;
     gc_shard* sh = new gc_shard();
     gc_graph& v = sh->v;
     v.device = g->device;

@@ -32,9 +32,13 @@ EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", 
            "gc_csr_free"]
 
 
+GC_PRIORITY_REF, GC_PRIORITY_SEEDED = 0, 1
+
+
 class GcOptions(ctypes.Structure):
     _fields_ = [("variant", ctypes.c_int32), ("e1", ctypes.c_int32), ("num_colors", ctypes.c_int64),
-                ("kernel_timing", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("kernel_timing", ctypes.c_int32), ("priority", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("speculative", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _I64P = ctypes.POINTER(ctypes.c_int64)

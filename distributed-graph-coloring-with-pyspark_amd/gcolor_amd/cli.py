@@ -88,6 +88,12 @@ def build_parser():
                    help="write the reference's failed-attempt snapshot instead of the valid colouring")
     p.add_argument("--no-e1", action="store_true", help="disable the stall re-seed extension (E1)")
     p.add_argument("--device", type=int, default=None, help="GPU ordinal")
+    p.add_argument("--priority-seed", type=int, default=None,
+                   help="variant A: order each colour's conflict resolution by the seeded priority "
+                        "prio_hash(seed, v) instead of the reference's (deg, pos)")
+    p.add_argument("--speculative", action="store_true",
+                   help="variant A: speculative first-fit rounds with one-shot resolution (not the reference's "
+                        "semantics; valid colourings)")
     return p
 
 
@@ -131,7 +137,10 @@ def main(argv=None, out=None):
 
     total_start = time.time()
     t0 = time.time()
-    full = dg.color(args.variant, e1=e1)
+    if args.variant == "B" and (args.priority_seed is not None or args.speculative):
+        parser.error("--priority-seed and --speculative apply to variant A")
+    mode = dict(priority=args.priority_seed, speculative=args.speculative)
+    full = dg.color(args.variant, e1=e1, **mode)
     full_ms = (time.time() - t0) * 1000.0
     if full.status == 2:
         # E1 disabled and the reference would spin forever here (coloring.py:93-95)
@@ -144,7 +153,7 @@ def main(argv=None, out=None):
     bounded, bounded_ms, bounded_val = None, 0.0, None
     if fail_k is not None:
         t0 = time.time()
-        bounded = dg.color(args.variant, num_colors=fail_k, e1=e1)
+        bounded = dg.color(args.variant, num_colors=fail_k, e1=e1, **mode)
         bounded_ms = (time.time() - t0) * 1000.0
         bounded_val = dg.validate(bounded.colors)
     lines, fail_k, minimal = transcript(K0, full, full_ms, full_val, bounded, bounded_ms, bounded_val)

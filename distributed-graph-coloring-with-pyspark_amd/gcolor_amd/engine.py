@@ -148,12 +148,19 @@ class DeviceGraph:
 
     # ---- hot path -------------------------------------------------------------------------
     def color(self, variant="A", num_colors=None, e1=True, kernel_timing=False, want_rounds=True,
-              want_colors=True):
+              want_colors=True, priority=None, speculative=False):
         """graph_coloring(graph, numOfColors): returns ColorResult.  ``num_colors=None``
-        is unbounded; on a bounded failure ``colors`` is the round-start snapshot."""
+        is unbounded; on a bounded failure ``colors`` is the round-start snapshot.
+        ``priority=None`` keeps the reference's (deg, pos) tie-break (coloring.py:64); an
+        int seed ranks each colour's conflict resolution by the seeded priority
+        prio_hash(seed, v) instead (variant A).  ``speculative=True``: speculative
+        first-fit rounds with one-shot resolution under that rank (variant A)."""
         opt = nat.GcOptions(variant=nat.GC_VARIANT_A if variant == "A" else nat.GC_VARIANT_B,
                             e1=1 if e1 else 0, num_colors=-1 if num_colors is None else int(num_colors),
-                            kernel_timing=_timing_mask(kernel_timing), reserved=0)
+                            kernel_timing=_timing_mask(kernel_timing),
+                            priority=nat.GC_PRIORITY_REF if priority is None else nat.GC_PRIORITY_SEEDED,
+                            seed=0 if priority is None else int(priority) & (2**64 - 1),
+                            speculative=1 if speculative else 0, reserved=0)
         st = nat.GcStats()
         cap = ROUND_CAP if want_rounds else 0
         rb = {k: np.zeros(max(cap, 1), np.int64) for k in ("U", "F", "maxmex", "accepted", "seeds")}

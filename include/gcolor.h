@@ -74,12 +74,22 @@ int gc_graph_lower_counts(const gc_graph* g, int32_t* nlow_out);
 #define GC_VARIANT_A 0 /* coloring.py (default)           */
 #define GC_VARIANT_B 1 /* coloring_optimized.py           */
 
+#define GC_PRIORITY_REF 0    /* rank (deg, pos): the reference's tie-break, coloring.py:64     */
+#define GC_PRIORITY_SEEDED 1 /* rank (prio_hash(seed, v), pos): seeded priorities (north_star) */
+
 typedef struct gc_options {
     int32_t variant;       /* GC_VARIANT_A / GC_VARIANT_B                                  */
     int32_t e1;            /* 1: re-seed on a zero-proposer round (extension E1)           */
     int64_t num_colors;    /* k of graph_coloring(graph, k); < 0 = unbounded               */
-    int32_t kernel_timing; /* bit GC_K_x set: bracket that class's launches with HIP events
+    int32_t kernel_timing; /* bit GC_K_x set: time that class's launches with HIP events
                               (gc_stats.k_ms); 0xFF = every class, 0 = none             */
+    int32_t priority;      /* GC_PRIORITY_REF / GC_PRIORITY_SEEDED (variant A only): the rank
+                              that orders each colour's conflict resolution             */
+    uint64_t seed;         /* seed of GC_PRIORITY_SEEDED                                    */
+    int32_t speculative;   /* 1: speculative first-fit rounds -- every uncoloured vertex
+                              proposes, one-shot resolution under the rank (variant A
+                              only; not the reference's semantics: valid colourings,
+                              colour count reported against the reference)              */
     int32_t reserved;
 } gc_options;
 

@@ -60,13 +60,33 @@ typedef struct {
 
 static inline int64_t deg_of(const int64_t* rp, int64_t v) { return rp[v + 1] - rp[v]; }
 
-/* rank order (deg asc, pos asc): coloring.py:64 stable sort of a file-ordered group */
+/* rank order (deg asc, pos asc): coloring.py:64 stable sort of a file-ordered group.
+   With seeded priorities (g_key != NULL) the sort key is key[v] = prio_hash(seed, v)
+   instead of deg(v): rank (key asc, pos asc). */
 static const int64_t* g_rp;
+static const uint32_t* g_key;
+static inline uint64_t rank_key(int64_t v) { return g_key ? (uint64_t)g_key[v] : (uint64_t)deg_of(g_rp, v); }
 static int cmp_rank(const void* a, const void* b) {
     int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
-    int64_t dx = deg_of(g_rp, x), dy = deg_of(g_rp, y);
+    uint64_t dx = rank_key(x), dy = rank_key(y);
     if (dx != dy) return dx < dy ? -1 : 1;
     return x < y ? -1 : (x > y);
+}
+static inline int rank_lt(int64_t u, int64_t v) {
+    uint64_t ku = rank_key(u), kv = rank_key(v);
+    return ku < kv || (ku == kv && u < v);
+}
+
+/* Seeded 32-bit priority of vertex v (SURVEY.md §8b priority = 1; BASELINE north_star
+   "Jones-Plassmann/Luby priority rounds on seeded hash priorities"): the top half of
+   splitmix64(seed + (v + 1) * golden gamma).  The GPU computes the same function
+   (csrc/gc_priority.hip, k_prio_hash). */
+uint32_t prio_hash(uint64_t seed, int64_t v) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(v + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
 }
 
 static int64_t uf_find(int64_t* p, int64_t x) {
@@ -126,10 +146,10 @@ static int64_t e1_reseed(const int64_t* rp, const int32_t* col, int64_t n, int32
  * On a bounded failure the colours are the state at the start of the failing round
  * (coloring.py:108 returns graph_rdd before the join).
  */
-int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t variant, int64_t k,
-                 int32_t e1, int32_t* color, int32_t* colored_round,
-                 int64_t* r_U, int64_t* r_F, int64_t* r_maxmex, int64_t* r_acc, int64_t* r_seeds,
-                 int64_t cap, orc_summary* sum) {
+static int color_impl(const int64_t* rp, const int32_t* col, int64_t n, int32_t variant, int64_t k,
+                      int32_t e1, const uint32_t* key, int32_t speculative, int32_t* color, int32_t* colored_round,
+                      int64_t* r_U, int64_t* r_F, int64_t* r_maxmex, int64_t* r_acc, int64_t* r_seeds,
+                      int64_t cap, orc_summary* sum) {
     memset(sum, 0, sizeof(*sum));
     sum->fail_round = -1;
     int status = ORC_OK;
@@ -173,6 +193,7 @@ int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t varia
 
     int64_t stampc = 0;
     g_rp = rp;
+    g_key = key;
     for (int64_t r = 0;; ++r) {
         if (r >= cap && (r_U || r_F || r_maxmex || r_acc || r_seeds)) { status = ORC_EROUNDS; break; }
         /* compact the uncoloured list (the reference filters color == -1, coloring.py:86) */
@@ -199,8 +220,10 @@ int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t varia
             }
             int64_t mex;
             if (ncol == 0) {
-                if (variant == 0) continue;          /* (-2, node): coloring.py:48-49          */
-                mex = 0;                             /* (0, info): coloring_optimized.py:159-160 */
+                if (variant == 0 && !speculative) continue;  /* (-2, node): coloring.py:48-49  */
+                mex = 0;                             /* (0, info): coloring_optimized.py:159-160;
+                                                        speculative first-fit: everyone proposes */
+                if (speculative && k >= 0 && mex >= k) fails++;
             } else {
                 mex = 0;
                 while (stamp[mex] == stampc) ++mex;
@@ -234,7 +257,22 @@ int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t varia
         }
 
         int64_t nacc = 0;
-        if (variant == 0) {
+        if (speculative) {
+            /* speculative first-fit, one-shot resolution (Luby / Jones-Plassmann depth 1):
+               v keeps its proposal iff no LISTED neighbour of lower rank proposed the same
+               colour this round; every other proposer retries next round */
+            for (int64_t i = 0; i < nprop; ++i) acc_stamp[props[i]] = -3 - r;  /* proposer mark */
+            for (int64_t i = 0; i < nprop; ++i) {
+                int64_t v = props[i];
+                int ok = 1;
+                for (int64_t e = rp[v]; e < rp[v + 1] && ok; ++e) {
+                    int64_t u = col[e];
+                    if (u != v && (acc_stamp[u] == -3 - r || acc_stamp[u] == r) && cand[u] == cand[v] && rank_lt(u, v))
+                        ok = 0;
+                }
+                if (ok) acc_stamp[v] = r;
+            }
+        } else if (variant == 0) {
             /* LFMIS per candidate colour under rank (deg asc, pos asc).  Groups are
                independent, so one pass in global rank order is the same computation. */
             qsort(props, (size_t)nprop, sizeof(int64_t), cmp_rank);
@@ -243,7 +281,7 @@ int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t varia
                 int ok = 1;
                 for (int64_t e = rp[v]; e < rp[v + 1]; ++e) {
                     int64_t u = col[e];
-                    if (acc_stamp[u] == r && cand[u] == cand[v]) { ok = 0; break; }
+                    if (acc_stamp[u] == r && cand[u] == cand[v]) { ok = 0; break; }  /* LFMIS */
                 }
                 if (ok) acc_stamp[v] = r;
             }
@@ -290,6 +328,34 @@ out:
     free(cand); free(stamp); free(acc_stamp); free(props); free(unc); free(parent); free(best);
     free(trp); free(tcol);
     return status;
+}
+
+int oracle_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t variant, int64_t k,
+                 int32_t e1, int32_t* color, int32_t* colored_round,
+                 int64_t* r_U, int64_t* r_F, int64_t* r_maxmex, int64_t* r_acc, int64_t* r_seeds,
+                 int64_t cap, orc_summary* sum) {
+    return color_impl(rp, col, n, variant, k, e1, NULL, 0, color, colored_round, r_U, r_F, r_maxmex, r_acc,
+                      r_seeds, cap, sum);
+}
+
+/* Variant A with seeded priorities (priority = 1: rank = (prio_hash(seed, v), pos) replaces
+   (deg, pos) in the per-colour LFMIS of coloring.py:56-70; the seed / E1 rule stays
+   argmax (deg, pos)) and/or speculative first-fit rounds (speculative = 1: every
+   uncoloured vertex proposes, one-shot resolution under the same rank). */
+int oracle_color_prio(const int64_t* rp, const int32_t* col, int64_t n, int64_t k, int32_t e1, int32_t priority,
+                      uint64_t seed, int32_t speculative, int32_t* color, int32_t* colored_round, int64_t* r_U,
+                      int64_t* r_F, int64_t* r_maxmex, int64_t* r_acc, int64_t* r_seeds, int64_t cap,
+                      orc_summary* sum) {
+    uint32_t* key = NULL;
+    if (priority) {
+        key = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+        if (!key) return ORC_ENOMEM;
+        for (int64_t v = 0; v < n; ++v) key[v] = prio_hash(seed, v);
+    }
+    int st = color_impl(rp, col, n, 0, k, e1, key, speculative, color, colored_round, r_U, r_F, r_maxmex, r_acc,
+                        r_seeds, cap, sum);
+    free(key);
+    return st;
 }
 
 /* validate_graph_coloring (coloring.py:149-162): uncoloured count and the directed

@@ -53,6 +53,12 @@ def load():
         lib.oracle_color.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                      P, P, P, P, P, P, P, ctypes.c_int64, ctypes.POINTER(_Summary)]
         lib.oracle_color.restype = ctypes.c_int
+        lib.oracle_color_prio.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_uint64, ctypes.c_int32, P, P, P, P, P, P, P, ctypes.c_int64,
+                                          ctypes.POINTER(_Summary)]
+        lib.oracle_color_prio.restype = ctypes.c_int
+        lib.prio_hash.argtypes = [ctypes.c_uint64, ctypes.c_int64]
+        lib.prio_hash.restype = ctypes.c_uint32
         lib.oracle_validate.argtypes = [P, P, ctypes.c_int64, P, ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]
         lib.oracle_validate.restype = None
@@ -136,6 +142,36 @@ def omp_color(rp, col, symmetric=False, threads=0, want_rounds=True, max_rounds=
     return out
 
 
+def c_color_prio(rp, col, k=None, e1=True, priority=1, seed=0, speculative=False, max_rounds=1 << 16):
+    """Variant A with seeded priorities (priority=1: rank (prio_hash(seed, v), pos) in the
+    per-colour LFMIS) and/or speculative first-fit rounds with one-shot resolution."""
+    lib = load()
+    rp = np.ascontiguousarray(rp, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    n = rp.shape[0] - 1
+    color = np.empty(max(n, 1), np.int32)
+    cround = np.empty(max(n, 1), np.int32)
+    per = {key: np.zeros(max_rounds, np.int64) for key in ("U", "F", "maxmex", "accepted", "seeds")}
+    s = _Summary()
+    st = lib.oracle_color_prio(_ptr(rp), _ptr(col), n, -1 if k is None else int(k), 1 if e1 else 0, int(priority),
+                               int(seed) & (2**64 - 1), 1 if speculative else 0, _ptr(color), _ptr(cround),
+                               _ptr(per["U"]), _ptr(per["F"]), _ptr(per["maxmex"]), _ptr(per["accepted"]),
+                               _ptr(per["seeds"]), max_rounds, ctypes.byref(s))
+    if st < 0:
+        raise RuntimeError(f"oracle_color_prio failed with status {st}")
+    r = s.rounds
+    out = {"status": st, "colors": color[:n], "colored_round": cround[:n], "rounds": r,
+           "fail_round": s.fail_round, "fail_count": s.fail_count, "reseeds": s.reseeds,
+           "max_color": s.max_color}
+    for key, arr in per.items():
+        out["round_" + key] = arr[:r].copy()
+    return out
+
+
+def prio_hash(seed, v):
+    return load().prio_hash(int(seed) & (2**64 - 1), int(v))
+
+
 def c_validate(rp, col, colors):
     lib = load()
     rp = np.ascontiguousarray(rp, dtype=np.int64)
@@ -178,10 +214,24 @@ def _components_argmax(adj, deg, color):
     return sorted(best.values())
 
 
-def py_color(adj, variant="A", k=None, e1=True):
-    """Pure-Python restatement. ``adj`` = list of neighbour-position lists (file order)."""
+def py_prio_hash(seed, v):
+    """Pure-Python prio_hash (splitmix64 finaliser, top 32 bits) -- checks the C one."""
+    M = (1 << 64) - 1
+    z = (int(seed) + 0x9E3779B97F4A7C15 * (v + 1)) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    z ^= z >> 31
+    return z >> 32
+
+
+def py_color(adj, variant="A", k=None, e1=True, priority_seed=None, speculative=False):
+    """Pure-Python restatement. ``adj`` = list of neighbour-position lists (file order).
+    ``priority_seed``: sort each candidate group by py_prio_hash(seed, v) instead of deg
+    (coloring.py:64's key); ``speculative``: every uncoloured vertex proposes and keeps its
+    proposal iff no listed lower-rank neighbour proposed the same colour (variant A)."""
     n = len(adj)
     deg = [len(a) for a in adj]
+    rkey = deg if priority_seed is None else [py_prio_hash(priority_seed, v) for v in range(n)]
     kk = None if k is None else int(k)
     # coloring.py:12-17
     color = [0 if deg[v] == 0 else -1 for v in range(n)]
@@ -209,8 +259,10 @@ def py_color(adj, variant="A", k=None, e1=True):
         for v in U:                                           # coloring.py:98-102
             used = set(color[u] for u in adj[v] if color[u] != -1)
             if not used:
-                if variant == "A":
+                if variant == "A" and not speculative:
                     continue                                  # -2
+                if speculative and kk is not None and kk <= 0:
+                    fails += 1
                 props.append((0, v))                          # coloring_optimized.py:159-160
                 continue
             c = 0
@@ -239,9 +291,14 @@ def py_color(adj, variant="A", k=None, e1=True):
             groups.setdefault(c, []).append(v)
         accepted = []
         for c, members in groups.items():
-            if variant == "A":                                # coloring.py:56-70
+            if speculative:                                   # one-shot: lower-rank same-colour proposer loses v
+                mem = set(members)
+                for v in members:
+                    if not any(u in mem and (rkey[u], u) < (rkey[v], v) for u in adj[v]):
+                        accepted.append((v, c))
+            elif variant == "A":                              # coloring.py:56-70
                 taken = set()
-                for v in sorted(members, key=lambda x: deg[x]):
+                for v in sorted(members, key=lambda x: rkey[x]):
                     if not any(u in taken for u in adj[v]):
                         taken.add(v)
                         accepted.append((v, c))
