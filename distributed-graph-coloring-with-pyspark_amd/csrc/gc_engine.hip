@@ -543,13 +543,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     if (opt->priority == GC_PRIORITY_REF && (rc = gc_hubs_prepare(g, run.d))) return rc;
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
-    rc = run.go(colors_out, cround_out);
-    if (rc < 0) return rc;
-    if (stats && stats->round_cap < (long long)run.recs.size() && (stats->round_U || stats->round_F)) {
-        gc_set_error("round buffers too small: %zu rounds", run.recs.size());
-        return GC_EROUNDS;
-    }
-    return rc;
+    return run.go(colors_out, cround_out);  // stats->rounds may exceed round_cap: the caller re-asks
 }
 
 extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts) {

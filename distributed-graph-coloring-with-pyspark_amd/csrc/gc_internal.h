@@ -39,7 +39,7 @@ typedef unsigned long long ull;
 #define GC_HUB_UNR 8        // hub row walk (gc_hub_jp_wave): entries per lane in flight
 #endif
 #define GC_HUB_NOT_STARTED (1ll << 40)
-#define GC_TAIL_HMAX_HUB 32
+#define GC_TAIL_HMAX_HUB 128
 #define GC_BIGROW 4096       // a winner with longer in-rows is walked by the whole grid (k_commit_big)  // tail sweeps may take this many hubs (their sweeps read short lists)
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512

@@ -639,6 +639,125 @@ __device__ unsigned gc_hub_scan_wave(const GDev& g, int x, unsigned cv6, int cv,
     return out ? 1u : (block >= 0 ? 2u : 0u);
 }
 
+// The resumable scan (gc_hub_scan_wave) of GC_HUB_NG hubs at once, one group of
+// GC_WAVE / GC_HUB_NG lanes each: a hub's scan usually ends in its first step (at its first
+// same-candidate undecided entry, or at an IN one), so a wave that walked its hubs one after
+// another paid a chain of dependent loads per hub -- the hub-start sweep's floor.  The
+// hubs' state comes prefetched, one per lane (slot j of the prefetch = lane j).
+#ifndef GC_HUB_NG
+#define GC_HUB_NG 4
+#endif
+__device__ void gc_hub_scan_groups(GDev& g, int nj, int pv, unsigned pkv, int pcv, int px, unsigned pkill,
+                                   const GcHubPre& pp, GcStage& st, int* ho, ull* ho_cnt, ull& lsum, ull& lnv,
+                                   long long* dout, ull* dcnt) {
+    constexpr int GS = GC_WAVE / GC_HUB_NG;
+    const int lane = gc_lane();
+    const int grp = lane / GS, li = lane % GS;
+    const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
+    const unsigned char* __restrict__ hk = g.hk;
+    for (int j0 = 0; j0 < nj; j0 += GC_HUB_NG) {
+        const int j = j0 + grp;
+        const bool has = j < nj;
+        const int jj = has ? j : 0;
+        const int v = __shfl(pv, jj, GC_WAVE);
+        const unsigned kv = (unsigned)__shfl((int)pkv, jj, GC_WAVE);
+        const unsigned cv6 = gc_k8_cand(kv);
+        const int cv = __shfl(pcv, jj, GC_WAVE);
+        const int xs = __shfl(px, jj, GC_WAVE);  // every lane takes part in every shuffle: a
+        const int x = has ? xs : -1;              // disabled source lane would read back 0
+        const bool kill = __shfl((int)pkill, jj, GC_WAVE) != 0;
+        const long long base = __shfl(pp.base, jj, GC_WAVE);
+        const int full = (int)__shfl(pp.full, jj, GC_WAVE);
+        const int cursor = __shfl(pp.enc, jj, GC_WAVE);
+        const int hc0 = __shfl(pp.hc0, jj, GC_WAVE);
+        const int hstart = __shfl(pp.hlen, jj, GC_WAVE);
+        const bool act = has && x >= 0 && !kill;  // group-uniform
+        const bool first = hc0 == 0;
+        int pos = first ? hstart : cursor;
+        bool out = false, prefix = act && first;
+        int block = -1, nstart = full;
+        const int* __restrict__ row = g.hlow_col + base;
+        for (;;) {
+            const bool run = act && !out && block < 0 && pos < full;
+            if (!__ballot(run)) break;
+            int u[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                const int e = pos + k * GS + li;
+                u[k] = (run && e < full) ? row[e] : -1;
+            }
+            unsigned ku[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) ku[k] = u[k] >= 0 ? (unsigned)hk[u[k]] : GC_HK_COLOURED;
+            unsigned fl[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) fl[k] = ku[k] != GC_HK_COLOURED ? gc_jp_flag_h(g, u[k], ku[k], cv6, cv) : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                if (__ballot(fl[k] == 1u) & gmask) out = true;
+                const ull mb = __ballot(fl[k] == 2u) & gmask;
+                if (mb && block < 0) block = pos + k * GS + __builtin_ctzll(mb >> (grp * GS));
+                const ull ml = __ballot(u[k] >= 0 && ku[k] != GC_HK_COLOURED) & gmask;
+                if (prefix && ml) {  // first non-coloured entry: the end of the coloured prefix
+                    nstart = pos + k * GS + __builtin_ctzll(ml >> (grp * GS));
+                    prefix = false;
+                }
+            }
+            if (run) pos += GC_HUB_UNR * GS;
+        }
+        unsigned f = kill ? 1u : 0u;
+        const bool lead = li == 0 && has && x >= 0;
+        if (act) {
+            f = out ? 1u : (block >= 0 ? 2u : 0u);
+            if (li == 0) {
+                if (first) {
+                    g.hcur[x] = 1;
+                    if (nstart > hstart) g.hlen[x] = nstart;
+                }
+                if (!out && block >= 0) g.hpc[x] = block;
+            }
+        }
+        gc_stage_push(st, lead && (f & 3u) == 2u, v, ho, ho_cnt);  // undecided hub
+        if (lead) {
+            if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
+            else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
+            if ((f & 1u) || !(f & 2u))  // hub mirror
+                g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
+            if (dout && ((f & 1u) || !(f & 2u)))
+                dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
+            lsum += (ull)g.deg[v];
+            lnv++;
+        }
+        // not a hub (cannot happen while heavy_t is the hub threshold): row scan, a wave each
+        ull nh = __ballot(li == 0 && has && x < 0);
+        while (nh) {
+            const int l = __ffsll((long long)nh) - 1;
+            nh &= nh - 1;
+            const int vv = __shfl(v, l, GC_WAVE);
+            const unsigned kvv = (unsigned)__shfl((int)kv, l, GC_WAVE);
+            const unsigned c6 = gc_k8_cand(kvv);
+            const int cvv = __shfl(cv, l, GC_WAVE);
+            const int dl = g.nlow[vv];
+            const long long start = g.rp[vv];
+            unsigned lf = 0;
+            for (int e = lane; e < dl; e += GC_WAVE) {
+                const int uu = g.col[start + e];
+                lf |= gc_jp_flag(g, uu, g.k8[uu], c6, cvv);
+            }
+            const unsigned ff = (__ballot((lf & 1u) != 0u) ? 1u : 0u) | (__ballot((lf & 2u) != 0u) ? 2u : 0u);
+            gc_stage_push(st, lane == 0 && (ff & 3u) == 2u, vv, ho, ho_cnt);
+            if (lane == 0) {
+                if (ff & 1u) gc_set_state(g, vv, kvv, GC_JP_OUT);
+                else if (!(ff & 2u)) gc_set_state(g, vv, kvv, GC_JP_IN);
+                if (dout && ((ff & 1u) || !(ff & 2u)))
+                    dout[atomicAdd(dcnt, 1ull)] = gc_delta(vv, (ff & 1u) ? GC_JP_OUT : GC_JP_IN);
+                lsum += (ull)g.deg[vv];
+                lnv++;
+            }
+        }
+    }
+}
+
 // First read of the LONG hub rows (static length > hub_long) in the sweep that starts the
 // hubs, by the whole grid: one wave per GC_HCH-entry chunk (static chunk index hch_rp /
 // hch_own, scanned in a scattered order so a long row's chunks land on many waves).  It
@@ -776,6 +895,10 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             }
             const long long left = (hcnt - i0 + waves - 1) / waves;
             const int nj = left < GC_WAVE ? (int)left : GC_WAVE;
+            if (g.hub_scan) {
+                gc_hub_scan_groups(g, nj, pv, pkv, pcv, px, pkill, pp, st, ho, ho_cnt, lsum, lnv, dout, dcnt);
+                continue;
+            }
             for (int j = 0; j < nj; ++j) {
                 const int v = __shfl(pv, j, GC_WAVE);
                 const unsigned kv = (unsigned)__shfl((int)pkv, j, GC_WAVE);

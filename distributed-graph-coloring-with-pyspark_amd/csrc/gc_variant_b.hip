@@ -340,10 +340,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         st->jp_sweeps = sweeps_total;
         st->fail_round = fail_round;
         st->fail_count = fail_count;
-        if (st->round_cap < (long long)recs.size() && (st->round_U || st->round_F)) {
-            gc_set_error("round buffers too small: %zu rounds", recs.size());
-            return GC_EROUNDS;
-        }
         for (long long i = 0; i < (long long)recs.size() && i < st->round_cap; ++i) {
             const RoundRec& rr = recs[(size_t)i];
             if (st->round_U) st->round_U[i] = rr.U;

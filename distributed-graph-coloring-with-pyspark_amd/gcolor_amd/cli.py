@@ -22,6 +22,8 @@ import random
 import sys
 import time
 
+import numpy as np
+
 from . import graphio
 from .generators import reference_csr
 
@@ -88,6 +90,9 @@ def build_parser():
                    help="write the reference's failed-attempt snapshot instead of the valid colouring")
     p.add_argument("--no-e1", action="store_true", help="disable the stall re-seed extension (E1)")
     p.add_argument("--device", type=int, default=None, help="GPU ordinal")
+    p.add_argument("--native-gen", action="store_true",
+                   help="generate with the native generator (graph.py:30-43's process on a splitmix64 stream seeded "
+                        "by --seed) instead of Python's random -- for node counts past what Python can build")
     p.add_argument("--priority-seed", type=int, default=None,
                    help="variant A: order each colour's conflict resolution by the seeded priority "
                         "prio_hash(seed, v) instead of the reference's (deg, pos)")
@@ -108,17 +113,23 @@ def main(argv=None, out=None):
     # Load or generate graph (coloring.py:174-187)
     if args.input:
         try:
-            ids, rp, col = graphio.load_graph(args.input)
+            ids, rp, col, symmetric = graphio.load_graph_ex(args.input)
         except Exception as e:  # same message and status as coloring.py:179-181
             say(f"Error loading graph: {e}")
             sys.exit(1)
     else:
         if not args.node_count or not args.max_degree:
             parser.error("--node-count and --max-degree are required when not using --input")
-        if args.seed is not None:
-            random.seed(args.seed)
-        rp, col = reference_csr(args.node_count, args.max_degree)
-        ids = list(range(args.node_count))
+        if args.native_gen:  # graph.py:30-43's process on a splitmix64 stream (gc_gen_uniform), any size
+            from .engine import uniform_csr
+            rp, col = uniform_csr(args.node_count, args.max_degree, 0 if args.seed is None else args.seed)
+            ids = np.arange(args.node_count, dtype=np.int64)
+        else:
+            if args.seed is not None:
+                random.seed(args.seed)
+            rp, col = reference_csr(args.node_count, args.max_degree)
+            ids = list(range(args.node_count))
+        symmetric = True  # the generator links both ends
         if args.output_graph:
             if args.output_graph.endswith(".gcsr"):  # binary CSR
                 graphio.write_csr(args.output_graph, rp, col, symmetric=True)
@@ -130,7 +141,7 @@ def main(argv=None, out=None):
         from . import _native
         _native.check("gc_set_device", _native.load().gc_set_device(args.device))
     n = len(ids)
-    dg = DeviceGraph.from_csr(rp, col)
+    dg = DeviceGraph.from_csr(rp, col, symmetric=symmetric)
     maxdeg = int((rp[1:] - rp[:-1]).max()) if n else 0
     K0 = args.max_degree + 1 if args.max_degree else maxdeg + 1   # coloring.py:212
     e1 = not args.no_e1

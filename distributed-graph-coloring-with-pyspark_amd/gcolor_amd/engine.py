@@ -161,8 +161,11 @@ class DeviceGraph:
                             priority=nat.GC_PRIORITY_REF if priority is None else nat.GC_PRIORITY_SEEDED,
                             seed=0 if priority is None else int(priority) & (2**64 - 1),
                             speculative=1 if speculative else 0, reserved=0)
+        return self._color(opt, want_rounds, want_colors, ROUND_CAP)
+
+    def _color(self, opt, want_rounds, want_colors, cap):
         st = nat.GcStats()
-        cap = ROUND_CAP if want_rounds else 0
+        cap = cap if want_rounds else 0
         rb = {k: np.zeros(max(cap, 1), np.int64) for k in ("U", "F", "maxmex", "accepted", "seeds")}
         if want_rounds:
             st.round_cap = cap
@@ -173,6 +176,8 @@ class DeviceGraph:
         status = self._lib.gc_color(self._h, ctypes.byref(opt), _ptr(colors), _ptr(cround), ctypes.byref(st))
         nat.check("gc_color", status, ok=(nat.GC_OK, nat.GC_FAILED, nat.GC_STALLED))
         r = st.rounds
+        if want_rounds and r > cap:  # more rounds than the buffers hold (long paths): once more, sized
+            return self._color(opt, want_rounds, want_colors, int(r))
         kernels = {}
         for i, name in enumerate(nat.KERNEL_CLASSES):
             kernels[name] = {"launches": int(st.k_launches[i]), "ms": float(st.k_ms[i]), "bytes": float(st.k_bytes[i])}

@@ -110,10 +110,20 @@ def is_gcsr(path):
 
 def load_graph(path):
     """(ids, rp, col) from a reference JSON graph or a .gcsr file (by magic bytes)."""
+    ids, rp, col, _ = load_graph_ex(path)
+    return ids, rp, col
+
+
+def load_graph_ex(path):
+    """(ids, rp, col, symmetric): symmetric is the .gcsr writer's assertion (True/False),
+    or None for JSON (the engine then checks the lists itself)."""
     if is_gcsr(path):
-        ids, rp, col, _ = read_csr(path)
-        return (np.arange(len(rp) - 1, dtype=np.int64) if ids is None else ids), rp, col
-    return load_graph_json(path)
+        ids, rp, col, flags = read_csr(path)
+        ids = np.arange(len(rp) - 1, dtype=np.int64) if ids is None else ids
+        from . import _native
+        return ids, rp, col, bool(flags & _native.GC_GRAPH_SYMMETRIC)
+    ids, rp, col = load_graph_json(path)
+    return ids, rp, col, None
 
 
 def _int64_ids(ids):

@@ -106,7 +106,8 @@ typedef struct gc_options {
 
 typedef struct gc_stats {
     /* outputs */
-    int64_t rounds;        /* entries written to the per-round arrays                     */
+    int64_t rounds;        /* rounds run; the per-round arrays hold the first min(rounds,
+                              round_cap) of them (a caller short of room asks again)     */
     int64_t fail_round;    /* bounded attempt: round that failed, else -1                 */
     int64_t fail_count;    /* #proposers with mex >= k in that round                      */
     int64_t reseeds;       /* E1 seeds planted                                            */
