@@ -78,6 +78,7 @@ struct gc_graph {
     std::vector<hipEvent_t> evpool;
     bool has_run_state = false;
     bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
+    bool own_stream = true;    // false: the caller's stream (gc_shard_set_stream), not destroyed here
     int part_prio = 0;         // rank the rows are partitioned for (gc_set_priority)
     uint64_t part_seed = 0;
 };

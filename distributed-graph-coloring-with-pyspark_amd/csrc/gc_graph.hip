@@ -163,7 +163,7 @@ void gc_free_all(gc_graph* g) {
     for (auto e : g->evpool) hipEventDestroy(e);
     if (g->ev0) hipEventDestroy(g->ev0);
     if (g->ev1) hipEventDestroy(g->ev1);
-    if (g->stream) hipStreamDestroy(g->stream);
+    if (g->stream && g->own_stream) hipStreamDestroy(g->stream);
 }
 
 static int new_graph(gc_graph** out, long long n, long long nnz, uint32_t flags, gc_graph** res) {

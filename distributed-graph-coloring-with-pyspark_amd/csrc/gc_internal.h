@@ -114,6 +114,7 @@ struct DevCtl {
     ull list_cnt;      // E1: compacted uncoloured list
     ull ticket;        // (unused)
     ull dcnt;          // sharded: deltas written this phase
+    ull rwin_cnt;      // sharded: other ranks' winners of this round, received as state deltas
     ull bigw_cnt;      // winners deferred to k_commit_big this commit
     long long sweeps;  // JP sweeps that found work in the current round (first included)
     long long sweep_total;  // sum over rounds of sweeps beyond the first

@@ -26,6 +26,8 @@
 // MFMA involved.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gcolor.h"
 #include "gc_internal.h"
 #include "gc_launch.h"
@@ -1663,27 +1665,94 @@ __global__ void __launch_bounds__(GC_BLOCK) k_delta_cand(GDev g, GLists L) {
 }
 
 // Apply received deltas to the vertices this rank does not own ([lo, hi) already hold
-// them).  Entries with v < 0 are padding.
+// them).  Entries with v < 0 are padding (and the exchange headers, gcolor_amd/shard.py).
+// rwin != null: IN states -- other ranks' winners of the round -- are also listed there, so
+// the round's end colours them from the list instead of scanning every proposal byte.
 __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long long* recv, long long count,
-                                                    long long lo, long long hi, int round) {
+                                                    long long lo, long long hi, int round, int* rwin) {
     const bool want_cround = g.ctl->want_cround != 0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long long)gridDim.x * blockDim.x) {
-        const long long e = recv[i];
+    const int lane = gc_lane();
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i - lane < count; i += stride) {
+        const long long e = i < count ? recv[i] : -1ll;
         const int v = (int)(e >> 32);
-        if (v < 0 || (v >= lo && v < hi)) continue;
+        const bool act = !(v < 0 || (v >= lo && v < hi));
         const int val = (int)(unsigned)(e & 0xFFFFFFFFll);
-        if (kind == GC_KIND_CAND) {
-            const unsigned c6 = gc_c6_of(val);
-            if (c6 == GC_K8_BIG) g.cand[v] = val;
-            g.k8[v] = gc_k8(c6, GC_JP_UND);
-        } else if (kind == GC_KIND_STATE) {
-            g.k8[v] = (unsigned char)((g.k8[v] & ~3u) | (unsigned)val);
-        } else {
-            gc_commit_colour(g, v, val);
-            if (want_cround) g.cround[v] = round;
-            atomicMax(&g.ctl->maxcolor, (long long)val);
+        if (act) {
+            if (kind == GC_KIND_CAND) {
+                const unsigned c6 = gc_c6_of(val);
+                if (c6 == GC_K8_BIG) g.cand[v] = val;
+                g.k8[v] = gc_k8(c6, GC_JP_UND);
+            } else if (kind == GC_KIND_STATE) {
+                g.k8[v] = (unsigned char)((g.k8[v] & ~3u) | (unsigned)val);
+            } else {
+                gc_commit_colour(g, v, val);
+                if (want_cround) g.cround[v] = round;
+                atomicMax(&g.ctl->maxcolor, (long long)val);
+            }
         }
+        if (rwin) gc_wave_append(act && kind == GC_KIND_STATE && val == GC_JP_IN, v, rwin, &g.ctl->rwin_cnt);
     }
+}
+
+// End of a sharded round, every delta seam: the other ranks' winners arrived as IN state
+// deltas and sit in rwin; each is coloured here too and pushes into this rank's
+// in-neighbours (owned targets only), O(winners) instead of k_shard_scan_commit's O(n).
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_list_commit(GDev g, GLists L, const int* rwin) {
+    DevCtl* c = g.ctl;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const int nxt = c->cur ^ 1;
+    int* next = L.F[nxt];
+    ull* next_cnt = &c->fcnt[nxt];
+    const int round = (int)(c->round + 1);
+    const bool want_cround = c->want_cround != 0;
+    GcStage st{s_stage[w], 0};
+    long long lmaxc = -1;
+    ull lacc = 0;
+    const long long cnt = (long long)c->rwin_cnt;
+    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch * GC_WAVE < cnt;
+         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long idx = ch * GC_WAVE + lane;
+        const int v = idx < cnt ? rwin[idx] : -1;
+        long long tstart = 0;
+        int din = 0;
+        if (v >= 0) {
+            const unsigned b = g.k8[v];
+            const int cc = gc_k8_cand(b) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(b);
+            gc_commit_colour(g, v, cc);
+            if (want_cround) g.cround[v] = round;
+            lmaxc = cc > lmaxc ? cc : lmaxc;
+            lacc++;
+            tstart = g.trp[v];
+            din = (int)(g.trp[v + 1] - tstart);
+        }
+        s_start[w][lane] = tstart;
+        const int incl = gc_wave_incl_scan(din);
+        const int excl = incl - din;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            bool claim = false;
+            int x = 0;
+            if (e < total) {
+                x = g.tcol[s_start[w][o] + (e - eo)];
+                claim = gc_claim(g.inF, x);
+            }
+            gc_stage_push(st, claim, x, next, next_cnt);
+        }
+        gc_wave_sync();
+    }
+    gc_stage_flush_block(st, next, next_cnt);
+    __syncthreads();
+    gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
+    gc_block_add(&c->accepted, lacc, scratch);
 }
 
 // End of a sharded round, after the last sweep seam: every rank holds every proposer's
@@ -1763,6 +1832,40 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
     gc_block_add(&c->accepted, lacc, scratch);
 }
 
+// A seam's send buffer, built on the device (no host round trip): HDR header words -- the
+// rank's round scalars, encoded as (0xFFFFFFFF << 32 | value) so every delta applier reads
+// them as padding -- then up to cap of the phase's deltas, padded with -1.
+//   kind GC_KIND_CAND  (propose seam): frontier, max candidate, #candidates >= k, #deltas
+//   kind GC_KIND_STATE (sweep seam):   undecided (lists of slot `slot`), #deltas, 0, #deltas
+// With delta == null only the header is written (the slice seams).
+#define GC_SEAM_HDR 4
+__device__ __forceinline__ long long gc_hdr_word(long long x) {
+    return (long long)((0xFFFFFFFFull << 32) | (ull)(unsigned)x);
+}
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_pack(GDev g, int kind, int slot, const long long* delta,
+                                                         long long* send, long long cap) {
+    const DevCtl* c = g.ctl;
+    const long long cnt = kind == GC_KIND_CAND ? (long long)c->fcnt[c->cur] : (long long)c->dcnt;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        long long h[GC_SEAM_HDR];
+        if (kind == GC_KIND_CAND) {
+            h[0] = (long long)c->fcnt[c->cur];
+            h[1] = c->maxmex;
+            h[2] = (long long)c->failcnt;
+            h[3] = cnt;
+        } else {
+            h[0] = (long long)(c->und_cnt[slot] + c->undh_cnt[slot]);
+            h[1] = cnt;
+            h[2] = 0;
+            h[3] = cnt;
+        }
+        for (int i = 0; i < GC_SEAM_HDR; ++i) send[i] = gc_hdr_word(h[i]);
+    }
+    if (!delta) return;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (long long)gridDim.x * blockDim.x)
+        send[GC_SEAM_HDR + i] = i < cnt ? delta[i] : -1ll;
+}
+
 // per-round counter reset of a shard (one thread)
 __global__ void k_shard_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -1776,6 +1879,7 @@ __global__ void k_shard_reset(GDev g, long long round) {
     c->maxmex = -1;
     c->sweeps = 0;
     c->dcnt = 0;
+    c->rwin_cnt = 0;
     c->bigw_cnt = 0;
     c->list_cnt = 0;
     c->seed_cnt[0] = 0;
@@ -2146,12 +2250,20 @@ void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
-               hipStream_t s) {
+               int* rwin, hipStream_t s) {
     if (count <= 0) return;
-    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round);
+    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round, rwin);
+}
+void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_list_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, rwin);
 }
 void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_scan_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi);
+}
+void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, long long* send, long long cap,
+                    hipStream_t s) {
+    const int grid = (int)std::max<long long>(1, std::min<long long>((cap + GC_BLOCK - 1) / GC_BLOCK, 64));
+    hipLaunchKernelGGL(k_shard_pack, dim3(grid), dim3(GC_BLOCK), 0, s, g, kind, slot, delta, send, cap);
 }
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);

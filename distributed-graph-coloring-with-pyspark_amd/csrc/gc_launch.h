@@ -90,9 +90,12 @@ void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0);
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
-               hipStream_t s);
+               int* rwin, hipStream_t s);
 void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, hipStream_t s);
+void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, hipStream_t s);
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
+void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, long long* send, long long cap,
+                    hipStream_t s);
 void gcl_shard_flip(const GDev& g, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
 void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s);

@@ -15,7 +15,10 @@
 // resolution is the lexicographically-first MIS under the global rank (deg, pos), the
 // result does not depend on the partition: it is bit-identical to gc_color on one GPU.
 //
-// Every call is synchronous (the caller needs the counts for the exchange).
+// The phase calls that return counts synchronise (the caller needs them for the exchange);
+// apply / get_slice / put_slices only enqueue.  gc_shard_set_stream puts the shard on the
+// caller's stream (torch's, where the RCCL collectives run), so a seam -- phase, copy into
+// the send buffer, all-gather, apply -- is ordered on one stream with no host wait inside.
 #include <string.h>
 
 #include <algorithm>
@@ -143,7 +146,72 @@ extern "C" int gc_shard_propose(gc_shard* sh, int64_t round, int64_t* delta, int
     return GC_OK;
 }
 
-// apply every rank's deltas of one kind to the vertices this rank does not own
+// Run the shard's kernels on the caller's stream from now on (e.g. torch's current stream,
+// so the RCCL collectives that move the seams are ordered with them).
+extern "C" int gc_shard_set_stream(gc_shard* sh, void* stream) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    GC_HIP(hipStreamSynchronize(g->stream));
+    if (g->own_stream && g->stream) GC_HIP(hipStreamDestroy(g->stream));
+    g->stream = reinterpret_cast<hipStream_t>(stream);
+    g->own_stream = false;
+    return GC_OK;
+}
+
+// Asynchronous phases (nothing waits; the counts go into the seam's header, gc_shard_pack):
+// propose on the rank's frontier with (v, candidate) deltas, and JP sweeps i .. i+count-1
+// with (v, IN|OUT) deltas (delta == null: a slice seam follows, no deltas written).
+extern "C" int gc_shard_propose_async(gc_shard* sh, int64_t round, int64_t* delta, int64_t cap) {
+    if (!sh || !delta) { gc_set_error("null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, delta);
+    gcl_shard_reset(d, round, g->stream);
+    gcl_fsort(d, L, g->fsum, g->stream);
+    gcl_pack_c4(d, g->stream);
+    gcl_propose(d, L, g->stream);
+    gcl_propose_block(d, L, g->stream);
+    gcl_delta_cand(d, L, g->stream);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+extern "C" int gc_shard_sweep_async(gc_shard* sh, int32_t i, int32_t count, int64_t* delta, int64_t cap) {
+    if (!sh || i < 0 || count < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (delta && cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = gc_view(g);
+    const GLists L = shard_lists(sh, delta);
+    GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
+    for (int j = i; j < i + count; ++j) {
+        if (j == 0) gcl_resolve(d, L, g->stream);
+        else gcl_sweep(d, L, j, g->stream);
+    }
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+// The seam's send buffer on the device: header words (the rank's round scalars) + up to cap
+// deltas (kind GC_KIND_CAND after propose, GC_KIND_STATE after sweeps whose last list slot is
+// `slot`); send holds GC_SEAM_HDR + cap int64.  delta == null: header only (slice seams
+// put the proposal-byte slice after it with gc_shard_get_slice).
+extern "C" int gc_shard_pack(gc_shard* sh, int32_t kind, int32_t slot, const int64_t* delta, int64_t* send,
+                             int64_t cap) {
+    if (!sh || !send || cap < 0 || slot < 0 || slot > 2) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    gcl_shard_pack(gc_view(g), kind, slot, reinterpret_cast<const long long*>(delta),
+                   reinterpret_cast<long long*>(send), delta ? cap : 0, g->stream);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+// apply every rank's deltas of one kind to the vertices this rank does not own (enqueued,
+// no wait); IN states are also listed as the round's remote winners (gc_shard_finish)
 extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, int64_t count, int64_t round) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     if (kind < GC_KIND_CAND || kind > GC_KIND_COLOUR) { gc_set_error("bad delta kind %d", kind); return GC_EINVAL; }
@@ -151,9 +219,8 @@ extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, i
     GC_HIP(hipSetDevice(g->device));
     if (count > 0 && !recv) { gc_set_error("null delta buffer"); return GC_EINVAL; }
     gcl_apply(gc_view(g), kind, reinterpret_cast<const long long*>(recv), count, sh->lo, sh->hi, (int)round + 1,
-              g->stream);
+              kind == GC_KIND_STATE ? g->parent : nullptr, g->stream);
     GC_HIP(hipGetLastError());
-    GC_HIP(hipStreamSynchronize(g->stream));
     return GC_OK;
 }
 
@@ -191,7 +258,6 @@ extern "C" int gc_shard_get_slice(gc_shard* sh, uint8_t* dst) {
     GC_HIP(hipSetDevice(g->device));
     if (sh->hi > sh->lo)
         GC_HIP(hipMemcpyAsync(dst, g->k8 + sh->lo, (size_t)(sh->hi - sh->lo), hipMemcpyDeviceToDevice, g->stream));
-    GC_HIP(hipStreamSynchronize(g->stream));
     return GC_OK;
 }
 
@@ -208,22 +274,24 @@ extern "C" int gc_shard_put_slices(gc_shard* sh, const uint8_t* src, int64_t str
         GC_HIP(hipMemcpyAsync(g->k8 + starts[p], src + (size_t)p * (size_t)stride, (size_t)lens[p],
                               hipMemcpyDeviceToDevice, g->stream));
     }
-    GC_HIP(hipStreamSynchronize(g->stream));
     return GC_OK;
 }
 
 // End of the round (coloring.py:114-127): colour every winner -- the rank's own through
-// its frontier (losers stay in it), the other ranks' read off the replicated proposal
-// bytes -- push them into this rank's in-neighbours and make that frontier current.
+// its frontier (losers stay in it), the other ranks' from the IN state deltas received
+// this round (from_deltas: every sweep seam of the round moved deltas) or read off the
+// replicated proposal bytes (a slice seam moved some states without deltas) -- push them
+// into this rank's in-neighbours and make that frontier current.
 // acc_out: winners of ALL ranks (the same on every rank); F_out: the rank's new frontier.
-extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int64_t* acc_out, int64_t* F_out) {
+extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int32_t from_deltas, int64_t* acc_out, int64_t* F_out) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
     const GDev d = gc_view(g);
     const GLists L = shard_lists(sh, nullptr);
     gcl_commit(d, L, GC_CM_SHARD, 0, g->stream);
-    gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->stream);
+    if (from_deltas) gcl_shard_list_commit(d, L, g->parent, g->stream);
+    else gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->stream);
     gcl_shard_flip(d, g->stream);
     int rc = shard_sync(sh);
     if (rc) return rc;

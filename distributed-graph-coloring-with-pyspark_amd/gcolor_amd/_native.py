@@ -26,7 +26,8 @@ EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", 
            "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_graph_lower_counts", "gc_color", "gc_validate",
            "gc_gen_uniform", "gc_last_error", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
-           "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors",
+           "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors", "gc_shard_set_stream",
+           "gc_shard_propose_async", "gc_shard_sweep_async", "gc_shard_pack",
            "gc_shard_get_slice", "gc_shard_put_slices",
            "gc_json_read_graph", "gc_json_write_coloring", "gc_json_write_graph", "gc_csr_write", "gc_csr_read",
            "gc_csr_free"]
@@ -107,7 +108,11 @@ def load():
         "gc_shard_sweep": ([P, I32, I32, P, I64, _I64P], ctypes.c_int),
         "gc_shard_get_slice": ([P, P], ctypes.c_int),
         "gc_shard_put_slices": ([P, P, I64, _I64P, _I64P, I32], ctypes.c_int),
-        "gc_shard_finish": ([P, I64, _I64P, _I64P], ctypes.c_int),
+        "gc_shard_finish": ([P, I64, I32, _I64P, _I64P], ctypes.c_int),
+        "gc_shard_set_stream": ([P, P], ctypes.c_int),
+        "gc_shard_propose_async": ([P, I64, P, I64], ctypes.c_int),
+        "gc_shard_sweep_async": ([P, I32, I32, P, I64], ctypes.c_int),
+        "gc_shard_pack": ([P, I32, I32, P, P, I64], ctypes.c_int),
         "gc_shard_reseed": ([P, I64, _I64P, _I64P], ctypes.c_int),
         "gc_shard_colors": ([P, P, P], ctypes.c_int),
         "gc_json_read_graph": ([ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(GcCsr))], ctypes.c_int),

@@ -13,7 +13,10 @@ it, as every rank's slice of the proposal bytes (cand6 << 2 | state), copied bac
 place.  After the last sweep seam every rank holds every proposer's final state, so each
 colours ALL the round's winners itself (coloring.py:114-127) and pushes them into its own
 in-neighbours: no exchange at commit.  The round scalars (frontier size, max proposal,
-failures, undecided) travel in a small all-gather before each data all-gather.
+failures, undecided) travel as a header in front of each seam's payload, so a seam is
+one all-gather unless some rank's deltas overflow the inline part.  When every seam of a
+round moved deltas, the other ranks' winners are the IN states received, and the round
+ends in O(winners); after a dense (slice) seam it scans the replicated proposal bytes.
 Conflict resolution is the lexicographically-first MIS under the global rank (deg, pos),
 so the colouring does not depend on the partition: it is bit-identical to one GPU.  E1
 re-seeding runs on every rank over the replicated state, so every rank plants the same
@@ -104,6 +107,15 @@ class TorchTransport:
         send = buf if self._cdev(dev) == dev else buf.to(self._cdev(dev))
         return self._gather_padded(send, dev)
 
+    def allgather(self, t):
+        """t (1-D, the same length on every rank) of every rank, concatenated, on t's
+        device.  With RCCL it is enqueued on the current stream: no host wait."""
+        dev = t.device
+        send = t if self._cdev(dev) == dev else t.to(self._cdev(dev))
+        recv = torch.empty(self.size * send.numel(), dtype=send.dtype, device=send.device)
+        self._allgather(recv, send)
+        return recv if recv.device == dev else recv.to(dev)
+
 
 class ThreadHub:
     """Rendezvous for ``parts`` shards driven by threads of one process."""
@@ -146,6 +158,9 @@ class ThreadTransport:
         part = self._settle(buf.clone())
         return self._settle(torch.cat(self._gather(part)))
 
+    def allgather(self, t):
+        return self._settle(torch.cat(self._gather(self._settle(t.clone()))))
+
 
 # ------------------------------------------------------------------------------------------
 # HIP phase implementation (libgcolor.so)
@@ -166,9 +181,14 @@ class HipShard:
         h = ctypes.c_void_p()
         nat.check("gc_shard_create", self._lib.gc_shard_create(dg._h, self.lo, self.hi, ctypes.byref(h)))
         self._h = h
+        # the shard's kernels run on torch's current stream, where the collectives run
+        if self.device.type == "cuda":
+            nat.check("gc_shard_set_stream", self._lib.gc_shard_set_stream(
+                h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
         self.cap = max(self.hi - self.lo, 1)
         self.delta = torch.empty(self.cap, dtype=torch.int64, device=self.device)
         self._slice = None
+        self._bufs = {}
         self._st = (ctypes.c_int64 * 4)()
         self._a = ctypes.c_int64()
         self._b = ctypes.c_int64()
@@ -194,6 +214,38 @@ class HipShard:
         nat.check("gc_shard_propose", self._lib.gc_shard_propose(self._h, r, _p(self.delta), self.cap, self._st))
         return self._st[0], self._st[1], self._st[2], self._st[3]
 
+    # ---- seams: the phase, then its send buffer built on the device (no host round trip) --
+    def _send(self, n, dtype):
+        key = (n, dtype)
+        if key not in self._bufs:
+            self._bufs[key] = torch.empty(n, dtype=dtype, device=self.device)
+        return self._bufs[key]
+
+    def propose_seam(self, r, C):
+        """propose (enqueued) + send buffer: HDR header words and up to C deltas."""
+        lib = self._lib
+        nat.check("gc_shard_propose_async", lib.gc_shard_propose_async(self._h, r, _p(self.delta), self.cap))
+        send = self._send(HDR + C, torch.int64)
+        nat.check("gc_shard_pack", lib.gc_shard_pack(self._h, KIND_CAND, 0, _p(self.delta), _p(send), C))
+        return send
+
+    def sweep_seam(self, i, count, C, emit, stride):
+        """JP sweeps i .. i+count-1 (enqueued) + send buffer: HDR header words and up to C
+        deltas, or (emit=False, a slice seam) the header bytes and the rank's proposal-byte
+        slice (stride bytes)."""
+        lib = self._lib
+        nat.check("gc_shard_sweep_async", lib.gc_shard_sweep_async(self._h, i, count, _p(self.delta) if emit else None,
+                                                                   self.cap))
+        last = (i + count - 1) % 3
+        if emit:
+            send = self._send(HDR + C, torch.int64)
+            nat.check("gc_shard_pack", lib.gc_shard_pack(self._h, KIND_STATE, last, _p(self.delta), _p(send), C))
+            return send
+        buf = self._send(8 * HDR + stride, torch.uint8)
+        nat.check("gc_shard_pack", lib.gc_shard_pack(self._h, KIND_STATE, last, None, _p(buf), 0))
+        nat.check("gc_shard_get_slice", lib.gc_shard_get_slice(self._h, _p(buf[8 * HDR:])))
+        return buf
+
     def apply(self, kind, recv, count, r):
         if count:
             nat.check("gc_shard_apply", self._lib.gc_shard_apply(self._h, kind, _p(recv), count, r))
@@ -204,10 +256,12 @@ class HipShard:
         return self._st[0], self._st[1]
 
     def slice_buffer(self, stride):
-        # empty, not zeros: a fill on torch's stream would race the shard stream's copy
-        if self._slice is None or self._slice.numel() != stride:
-            self._slice = torch.empty(stride, dtype=torch.uint8, device=self.device)
-        return self._slice
+        # one cached buffer per size (header + slice, or the bare slice of an overflow)
+        if self._slice is None:
+            self._slice = {}
+        if stride not in self._slice:
+            self._slice[stride] = torch.empty(stride, dtype=torch.uint8, device=self.device)
+        return self._slice[stride]
 
     def get_slice(self, buf):
         nat.check("gc_shard_get_slice", self._lib.gc_shard_get_slice(self._h, _p(buf)))
@@ -218,9 +272,10 @@ class HipShard:
         b = (ct.c_int64 * len(lens))(*lens)
         nat.check("gc_shard_put_slices", self._lib.gc_shard_put_slices(self._h, _p(recv), stride, a, b, len(starts)))
 
-    def finish(self, r):
+    def finish(self, r, from_deltas=False):
         ct = self._ct
-        nat.check("gc_shard_finish", self._lib.gc_shard_finish(self._h, r, ct.byref(self._a), ct.byref(self._b)))
+        nat.check("gc_shard_finish", self._lib.gc_shard_finish(self._h, r, 1 if from_deltas else 0,
+                                                               ct.byref(self._a), ct.byref(self._b)))
         return self._a.value, self._b.value
 
     def reseed(self, r):
@@ -268,27 +323,47 @@ class ShardResult:
 
 
 K8_BIG = 62  # candidates >= 62 do not fit the 6-bit proposal byte (gc_internal.h)
+HDR = 4      # header words carried in front of every seam's payload
+
+
+def _hdr_words(vals):
+    """Header values as int64 words that read as padding to the delta appliers (vertex
+    field -1): (0xFFFFFFFF << 32) | value, value as unsigned 32 bits."""
+    return torch.tensor([((0xFFFFFFFF << 32) | (int(x) & 0xFFFFFFFF)) - (1 << 64) for x in vals], dtype=torch.int64)
+
+
+def _hdr_values(words):
+    """int64 array [P, HDR] of header words -> their signed 32-bit values."""
+    x = np.asarray(words, dtype=np.int64) & 0xFFFFFFFF
+    return np.where(x >= 1 << 31, x - (1 << 32), x)
 
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
-                want_colors=True):
+                want_colors=True, inline=4096):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
-    Each seam is a stats all-gather then a data all-gather: the deltas, or -- when the
-    padded deltas would outweigh them (``dense=None``; True/False force it) -- every
-    rank's slice of the proposal bytes, copied back in place without a scatter.
-    ``local_sweeps`` JP sweeps run between two exchanges of the sweep seam (more than one
-    pays where neighbours are mostly rank-local, e.g. meshes cut into slabs).
-    ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them later)."""
+    Each seam is ONE all-gather in the usual case: a header (the round scalars: frontier,
+    max proposal, failures, undecided, count) in front of up to ``inline`` deltas, or in
+    front of the rank's slice of the proposal bytes when the seam is dense.  Only when some
+    rank has more deltas than fit inline does a second all-gather follow: the rest of the
+    deltas, or -- when they would outweigh it (``dense=None``; True/False force it) -- every
+    rank's slice, copied back in place without a scatter.  ``local_sweeps`` JP sweeps run
+    between two exchanges of the sweep seam (more than one pays where neighbours are
+    mostly rank-local, e.g. meshes cut into slabs).  A round whose seams all moved deltas
+    ends from the received IN states (O(winners)), otherwise from a scan of the proposal
+    bytes.  ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them)."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
     dev = ops.delta.device
+    P = comm.size
     rng = comm.gather_stats([ops.lo, ops.hi], dev)
     starts = [int(x) for x in rng[:, 0]]
     lens = [int(x) for x in rng[:, 1] - rng[:, 0]]
     stride = max(max(lens), 1)
+    C = max(int(inline), 0)
+    hdr_bytes = 8 * HDR
 
     def rec(u, f, mm, acc, seeds):
         res.round_U.append(int(u))
@@ -297,22 +372,37 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
         res.round_accepted.append(int(acc))
         res.round_seeds.append(int(seeds))
 
-    def slices():
-        res.exchanges += 1
-        res.dense_exchanges += 1
-        buf = ops.slice_buffer(stride)
-        ops.get_slice(buf)
-        ops.put_slices(comm.gather_slices(buf), stride, starts, lens)
-
-    def deltas(S, kind, r):
-        res.exchanges += 1
-        maxc = int(S[:, -1].max())
-        if maxc:
-            recv = comm.gather_deltas(ops.delta, int(S[comm.rank, -1]), maxc)
-            ops.apply(kind, recv, int(recv.numel()), r)
-
     def slice_for(maxc):  # a slice seam moves stride bytes per rank, deltas 8 * maxc
         return dense if dense is not None else 8 * maxc > stride
+
+    def gather(send):
+        """one all-gather of the seams' send buffers; -> (headers [P, HDR], received)."""
+        res.exchanges += 1
+        recv = comm.allgather(send)
+        if recv.dtype == torch.int64:
+            words = recv.view(P, -1)[:, :HDR]
+        else:  # slice seam: header bytes in front of each rank's slice
+            res.dense_exchanges += 1
+            words = recv.view(P, -1)[:, :hdr_bytes].contiguous().view(torch.int64)
+        return _hdr_values(words.cpu().numpy()), recv
+
+    def finish_deltas(kind, hdr, recv, r, dense_ok):
+        """after a delta seam: apply, or move what did not fit inline.  -> dense?"""
+        maxc = int(hdr[:, -1].max())
+        if maxc > C and dense_ok and slice_for(maxc):
+            res.exchanges += 1
+            res.dense_exchanges += 1
+            buf = ops.slice_buffer(stride)
+            ops.get_slice(buf)
+            ops.put_slices(comm.allgather(buf), stride, starts, lens)
+            return True
+        ops.apply(kind, recv, int(recv.numel()), r)
+        if maxc > C:
+            res.exchanges += 1
+            own = int(hdr[comm.rank, -1])
+            rest = comm.gather_deltas(ops.delta[C:], max(own - C, 0), maxc - C)
+            ops.apply(kind, rest, int(rest.numel()), r)
+        return False
 
     max_rounds = 4 * ops.n + 16
     r = 0
@@ -322,9 +412,8 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             break
         if r > max_rounds:
             raise RuntimeError("round limit exceeded")
-        cnt, f_loc, mm, fails = ops.propose(r)
-        S = comm.gather_stats([f_loc, mm, fails, cnt], dev)
-        F, maxmex, fails = int(S[:, 0].sum()), int(S[:, 1].max()), int(S[:, 2].sum())
+        hdr, recv = gather(ops.propose_seam(r, C))
+        F, maxmex, fails = int(hdr[:, 0].sum()), int(hdr[:, 1].max()), int(hdr[:, 2].sum())
         if F == 0:  # no proposer anywhere: the reference spins (coloring.py:93-95) -> E1
             if not e1:
                 rec(U, 0, -1, 0, 0)
@@ -341,27 +430,25 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             res.status, res.fail_round, res.fail_count = FAILED, r, fails
             break
         # candidates >= 62 live in cand[], outside the proposal bytes: deltas only
-        if maxmex < K8_BIG and slice_for(int(S[:, -1].max())):
-            slices()
-        else:
-            deltas(S, KIND_CAND, r)
+        finish_deltas(KIND_CAND, hdr, recv, r, maxmex < K8_BIG)
         # JP sweeps; a rank decides at most what it has left, so the seam's form is known
         # before the sweep runs (and a slice seam writes no deltas)
-        i, left = 0, int(S[:, 0].max())
+        i, left, any_dense = 0, int(hdr[:, 0].max()), False
         while True:
             sl = slice_for(left)
-            cnt, und = ops.sweep(i, local_sweeps if i else 1, emit=not sl)
-            i += local_sweeps if i else 1
-            S = comm.gather_stats([und, cnt], dev)
+            cnt = local_sweeps if i else 1
+            hdr, recv = gather(ops.sweep_seam(i, cnt, C, not sl, stride))
+            i += cnt
             if sl:
-                slices()
+                ops.put_slices(recv[hdr_bytes:], hdr_bytes + stride, starts, lens)
+                any_dense = True
             else:
-                deltas(S, KIND_STATE, r)
-            if int(S[:, 0].sum()) == 0:
+                any_dense |= finish_deltas(KIND_STATE, hdr, recv, r, True)
+            if int(hdr[:, 0].sum()) == 0:
                 break
-            left = int(S[:, 0].max())
+            left = int(hdr[:, 0].max())
             res.jp_sweeps += 1
-        acc, _ = ops.finish(r)
+        acc, _ = ops.finish(r, not any_dense)
         rec(U, F, maxmex, acc, 0)
         U -= acc
         r += 1

@@ -161,7 +161,16 @@ void gc_shard_destroy(gc_shard* s);
 int gc_shard_begin(gc_shard* s, int64_t num_colors, int32_t track_rounds, int64_t* U_out, int64_t* F_out);
 /* stats[4]: deltas written, frontier size, max candidate (-1 none), #candidates >= k    */
 int gc_shard_propose(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
-int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);
+int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);  /* enqueued */
+/* the same phases, only enqueued (no wait, no stats): their counts travel in the seam's
+   header, written on the device by gc_shard_pack                                        */
+int gc_shard_propose_async(gc_shard* s, int64_t round, int64_t* delta, int64_t cap);
+int gc_shard_sweep_async(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap);
+/* a seam's send buffer (device, 4 + cap int64): 4 header words -- propose: frontier, max
+   candidate, #candidates >= k, #deltas; sweep: undecided in list slot `slot`, #deltas, 0,
+   #deltas -- each encoded (0xFFFFFFFF << 32 | value) so appliers skip it as padding, then
+   up to cap deltas padded with -1 (delta == NULL: the header only)                      */
+int gc_shard_pack(gc_shard* s, int32_t kind, int32_t slot, const int64_t* delta, int64_t* send, int64_t cap);
 /* sweeps i .. i+count-1 (i = 0: first sweep over the frontier, then over the undecided);
    delta may be NULL (slice seam).  stats[2]: deltas written, still undecided here      */
 int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats);
@@ -170,9 +179,14 @@ int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_
 int gc_shard_get_slice(gc_shard* s, uint8_t* dst);
 int gc_shard_put_slices(gc_shard* s, const uint8_t* src, int64_t stride, const int64_t* starts,
                         const int64_t* lens, int32_t parts);
-/* end of round: colour ALL ranks' winners (read off the replicated proposal bytes), push
-   them into the rank's in-neighbours; *acc_out = winners (global), *F_out = new frontier */
-int gc_shard_finish(gc_shard* s, int64_t round, int64_t* acc_out, int64_t* F_out);
+/* end of round: colour ALL ranks' winners -- from the IN state deltas applied this round
+   (from_deltas = 1: every sweep seam moved deltas) or read off the replicated proposal
+   bytes -- push them into the rank's in-neighbours; *acc_out = winners (global), *F_out =
+   new frontier                                                                         */
+int gc_shard_finish(gc_shard* s, int64_t round, int32_t from_deltas, int64_t* acc_out, int64_t* F_out);
+/* run the shard's kernels on the caller's stream (a hipStream_t, e.g. torch's current one,
+   where the collectives run): apply / get_slice / put_slices then only enqueue          */
+int gc_shard_set_stream(gc_shard* s, void* stream);
 /* E1 re-seed on the replicated state (same seeds on every rank)                        */
 int gc_shard_reseed(gc_shard* s, int64_t round, int64_t* nseeds, int64_t* F_out);
 int gc_shard_colors(gc_shard* s, int32_t* colors_out, int32_t* colored_round_out);

@@ -88,6 +88,32 @@ class NumpyShard:
             pairs.append((v, mex))
         return self._emit(pairs), len(self.F), mm, fails
 
+    # ---- seams (gcolor_amd.shard.HipShard's interface): header words + inline deltas ----
+    @staticmethod
+    def _words(vals):
+        return [((0xFFFFFFFF << 32) | (int(x) & 0xFFFFFFFF)) - (1 << 64) for x in vals]
+
+    def _pack(self, vals, cnt, C):
+        send = torch.full((4 + C,), -1, dtype=torch.int64)
+        send[:4] = torch.tensor(self._words(vals), dtype=torch.int64)
+        k = min(cnt, C)
+        if k:
+            send[4:4 + k] = self.delta[:k]
+        return send
+
+    def propose_seam(self, r, C):
+        cnt, f, mm, fails = self.propose(r)
+        return self._pack([f, mm, fails, cnt], cnt, C)
+
+    def sweep_seam(self, i, count, C, emit, stride):
+        cnt, und = self.sweep(i, count, emit)
+        if emit:
+            return self._pack([und, cnt, 0, cnt], cnt, C)
+        buf = torch.zeros(32 + stride, dtype=torch.uint8)
+        buf[:32] = torch.tensor(self._words([und, 0, 0, 0]), dtype=torch.int64).view(torch.uint8)
+        self.get_slice(buf[32:])
+        return buf
+
     def apply(self, kind, recv, tot, r):
         for v, val in self._decode(recv, tot):
             if self._owned(v):
@@ -145,7 +171,7 @@ class NumpyShard:
             self.cand[s0:s0 + ln] = np.where(c6 == 63, -1, np.where(c6 == 62, cur, c6))
             self.state[s0:s0 + ln] = b & 3
 
-    def finish(self, r):
+    def finish(self, r, from_deltas=False):
         # every proposer's final state is replicated: all ranks colour all winners
         win = [v for v in range(self.n) if self.state[v] == IN and self.cand[v] >= 0]
         for v in win:

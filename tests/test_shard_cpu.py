@@ -107,22 +107,24 @@ def test_threads_directed_selfloops_bounded_and_stalled(seed):
     assert r.status == s["status"] and np.array_equal(r.colors, s["colors"])
 
 
-@pytest.mark.parametrize("dense", [True, False])
+@pytest.mark.parametrize("dense", [True, False, None])
 @pytest.mark.parametrize("local_sweeps", [1, 3])
-def test_dense_seams_and_local_sweeps(dense, local_sweeps):
-    """Slices of the proposal bytes instead of deltas, and several JP sweeps between
-    exchanges, leave the result unchanged."""
+@pytest.mark.parametrize("inline", [4096, 5, 0])
+def test_dense_seams_and_local_sweeps(dense, local_sweeps, inline):
+    """Slices of the proposal bytes instead of deltas, several JP sweeps between
+    exchanges, and deltas that overflow the inline part of a seam's all-gather (a second
+    exchange: the rest of the deltas, or slices) leave the result unchanged."""
     for seed in range(3):
         rp, col = _random_directed(400, 2000, 10 + seed)
         o = oracle.c_color(rp, col, "A")
-        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps)
+        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps, inline=inline)
         assert_matches_oracle(res[seed % 3], o)
         if dense:
             assert res[0].dense_exchanges > 0
-        else:
+        elif dense is False:
             assert res[0].dense_exchanges == 0
     ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
-    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps)[1],
+    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps, inline=inline)[1],
                           oracle.c_color(rp, col, "A"))
 
 
@@ -134,7 +136,7 @@ def test_more_ranks_than_vertices():
 
 
 # ---- two processes over torch.distributed (gloo), the transport the GPU ranks use -------
-def _gloo_worker(rank, world, port, path, out_dir, dense=None):
+def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096):
     import torch.distributed as dist
     sys.path[:0] = [PKG_DIR, REPO, os.path.dirname(os.path.abspath(__file__))]
     from shard_numpy import NumpyShard as NS
@@ -143,7 +145,8 @@ def _gloo_worker(rank, world, port, path, out_dir, dense=None):
     d = np.load(path)
     rp, col = d["rp"], d["col"]
     lo, hi = shm.balanced_ranges(rp, world)[rank]
-    res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, track_rounds=True, dense=dense)
+    res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, track_rounds=True, dense=dense,
+                          inline=inline)
     out = {"status": res.status, "colors": res.colors.tolist(), "cround": res.colored_round.tolist(),
            "U": res.round_U, "F": res.round_F, "maxmex": res.round_maxmex, "acc": res.round_accepted,
            "seeds": res.round_seeds}
@@ -152,13 +155,16 @@ def _gloo_worker(rank, world, port, path, out_dir, dense=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,dense", [("gen_1000_8_s1", None), ("gen_1000_8_s1", True), ("asymmetric", None)])
-def test_gloo_world_size_2(case, dense, tmp_path):
+@pytest.mark.parametrize("case,dense,inline", [("gen_1000_8_s1", None, 4096), ("gen_1000_8_s1", True, 4096),
+                                               ("asymmetric", None, 4096), ("gen_1000_8_s1", None, 3),
+                                               ("gen_1000_8_s1", False, 0)])
+def test_gloo_world_size_2(case, dense, inline, tmp_path):
     ids, adj, rp, col = fixture_csr(load_golden(case))
     path = str(tmp_path / "g.npz")
     np.savez(path, rp=rp, col=col)
     port = 29500 + random.randint(0, 2000)
-    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path), dense), nprocs=2, join=True)
+    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path), dense, inline), nprocs=2,
+                                join=True)
     o = oracle.c_color(rp, col, "A")
     for r in range(2):
         got = json.load(open(tmp_path / f"r{r}.json"))

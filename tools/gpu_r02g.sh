@@ -1,0 +1,8 @@
+set -euo pipefail
+mkdir -p gpurun_out/r02g
+timeout -k 10 600 python -u -m pytest tests/test_shard_gpu.py tests/test_abi.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r02g/pytest.log 2>&1 || { tail -40 gpurun_out/r02g/pytest.log; exit 1; }
+tail -3 gpurun_out/r02g/pytest.log
+timeout -k 10 300 python -u tools/shard_timing.py mesh256 1 2 4 8 > gpurun_out/r02g/shard_mesh256.log 2>&1
+cat gpurun_out/r02g/shard_mesh256.log
+timeout -k 10 400 python -u tools/shard_timing.py rmat24 1 2 4 8 > gpurun_out/r02g/shard_rmat24.log 2>&1
+cat gpurun_out/r02g/shard_rmat24.log

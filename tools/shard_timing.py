@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
-"""Time the sharded engine with P shards on ONE GPU (threads, no network): how much the
-seam exchanges and per-phase syncs cost next to the single-GPU engine.
-python tools/shard_timing.py [n] [parts...]"""
-import collections
+"""Rehearse the sharded engine with P shards on ONE GPU (threads, no network): how much
+the seam exchanges and per-phase host syncs cost next to the single-GPU engine.
+
+  python tools/shard_timing.py WORKLOAD [parts...]     WORKLOAD: rmat24 | mesh256 | uniform10M | rmat20
+
+Shard views run the row-scan engine (no hubs: their pushed state is not exchanged), so
+the single-GPU reference for the seam overhead is the engine with GC_HUB_T=off; the hub
+engine's time is printed beside it.  The P shards share one device and one stream, so
+their kernels run one after another: the P-shard time is the sum of the shards' kernels
+plus the seams, and `seams` below is that time minus the P-way split of the engine's
+kernels (an estimate of what the exchange protocol costs per colouring)."""
+import json
 import os
 import sys
 import threading
@@ -15,25 +23,46 @@ import torch  # noqa: E402
 from gcolor_amd import shard as sh  # noqa: E402
 from gcolor_amd.engine import DeviceGraph, uniform_csr  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-parts_list = [int(x) for x in sys.argv[2:]] or [1, 2, 4]
+wl = sys.argv[1] if len(sys.argv) > 1 else "rmat24"
+parts_list = [int(x) for x in sys.argv[2:]] or [1, 2, 4, 8]
 torch.cuda.set_device(0)
-rp, col = uniform_csr(n, 16, 42)
-dg = DeviceGraph.from_csr(rp, col, symmetric=True)
-dg.color("A")
-t0 = time.perf_counter()
-for _ in range(3):
-    one = dg.color("A", want_rounds=False)
-print(f"single engine: {(time.perf_counter() - t0) / 3 * 1e3:.1f} ms", flush=True)
+if wl.startswith("rmat"):
+    dg = DeviceGraph.rmat(int(wl[4:]), 16, seed=1)
+elif wl.startswith("mesh"):
+    d = int(wl[4:])
+    dg = DeviceGraph.mesh(d, d, d)
+else:
+    rp, col = uniform_csr(10_000_000 if wl == "uniform10M" else 1_000_000, 16, 42)
+    dg = DeviceGraph.from_csr(rp, col, symmetric=True)
+
+
+def engine_ms(env=None):
+    if env:
+        os.environ.update(env)
+    dg.color("A", want_rounds=False)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        r = dg.color("A", want_rounds=False)
+    dt = (time.perf_counter() - t0) / 3 * 1e3
+    for k in (env or {}):
+        del os.environ[k]
+    return dt, r
+
+
+hub_ms, one = engine_ms()
+scan_ms, _ = engine_ms({"GC_HUB_T": "off"})
+out = {"workload": wl, "engine_ms": round(hub_ms, 1), "engine_rowscan_ms": round(scan_ms, 1),
+       "rounds": one.rounds, "shards": {}}
+print(json.dumps(out), flush=True)
 
 
 def run_parts(shards, **kw):
     hub = sh.ThreadHub(len(shards))
-    out, err = [None] * len(shards), []
+    res, err = [None] * len(shards), []
 
     def go(i):
         try:
-            out[i] = sh.shard_color(shards[i], sh.ThreadTransport(hub, i), **kw)
+            res[i] = sh.shard_color(shards[i], sh.ThreadTransport(hub, i), want_colors=False, **kw)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             hub.barrier.abort()
@@ -44,53 +73,26 @@ def run_parts(shards, **kw):
         t.join()
     if err:
         raise err[0]
-    return out
+    return res
 
 
-rp_d, _ = dg.export()
+rp_d, _ = dg.export(col=False)
 for p in parts_list:
-    t0 = time.perf_counter()
     shards = [sh.HipShard(dg, lo, hi) for lo, hi in sh.balanced_ranges(rp_d, p)]
     torch.cuda.synchronize()
-    print(f"{p} shards: create {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
-    for kw in ({}, {"dense": False}, {"local_sweeps": 1}):
-        run_parts(shards, **kw)
-        t0 = time.perf_counter()
-        for _ in range(2):
-            res = run_parts(shards, **kw)
-        dt = (time.perf_counter() - t0) / 2
-        ok = (res[0].colors == one.colors).all()
-        print(f"  {kw or 'default'}: {dt * 1e3:.1f} ms  exchanges={res[0].exchanges} "
-              f"dense={res[0].dense_exchanges} identical={ok}", flush=True)
+    run_parts(shards)
+    t0 = time.perf_counter()
+    res = run_parts(shards)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) * 1e3
+    colors, _ = shards[0].colors(False)
+    ok = bool((colors == one.colors).all()) if one.colors is not None else None
+    seams = res[0].exchanges
+    e = {"ms": round(dt, 1), "exchanges": seams, "dense": res[0].dense_exchanges,
+         "seam_overhead_ms_est": round(dt - scan_ms, 1), "per_exchange_us": round((dt - scan_ms) * 1e3 / max(seams, 1), 1),
+         "identical": ok}
+    out["shards"][p] = e
+    print(p, json.dumps(e), flush=True)
     for s in shards:
         s.close()
-
-# per-phase wall time of one shard (1 part) -------------------------------------------
-acc = collections.defaultdict(float)
-
-
-def timed(obj, name):
-    f = getattr(obj, name)
-
-    def g(*a, **k):
-        t = time.perf_counter()
-        out = f(*a, **k)
-        torch.cuda.synchronize()
-        acc[name] += time.perf_counter() - t
-        return out
-    setattr(obj, name, g)
-
-
-ops = sh.HipShard(dg, 0, dg.n)
-for name in ("begin", "propose", "apply", "sweep", "finish", "reseed", "colors", "get_slice", "put_slices"):
-    timed(ops, name)
-hub = sh.ThreadHub(1)
-tr = sh.ThreadTransport(hub, 0)
-for name in ("gather_stats", "gather_deltas", "gather_slices"):
-    timed(tr, name)
-sh.shard_color(ops, tr)
-acc.clear()
-t0 = time.perf_counter()
-sh.shard_color(ops, tr)
-print(f"1 shard total {(time.perf_counter() - t0) * 1e3:.1f} ms; per phase (ms):",
-      {k: round(v * 1e3, 1) for k, v in acc.items()})
+print(json.dumps(out))
