@@ -230,6 +230,20 @@ struct Run {
     bool resort_hint = false;    // enqueue the frontier re-sort kernels (last snapshot's frontier >= n/256)
     bool c4_hint = true;         // enqueue k_pack_c4 (last snapshot's frontier >= n/64, colours < 14)
     const int batch_max = getenv("GC_BATCH_MAX") ? atoi(getenv("GC_BATCH_MAX")) : 4;
+    // k_sweep_loop's grid: one workgroup per CU (all resident: its grid barrier needs it).
+    // Off unless GC_SWEEP_LOOP=1: it cuts the sweep launches ~2.5x but measured slower
+    // (R-MAT-26 588 -> 610 ms, C2 8.0 -> 12.2 ms: a grid barrier costs about a launch, and
+    // the resident grid has a quarter of the waves for the latency-bound sweeps)
+    int loop_grid = 0;
+    void init_loop() {
+        const char* e = getenv("GC_SWEEP_LOOP");
+        if (!e || atoi(e) <= 0) return;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
+            return;
+        const char* w = getenv("GC_LOOP_WG");
+        loop_grid = w && atoi(w) > 0 ? std::min(atoi(w), cus) : cus;
+    }
     // k_propose_block has no work unless some vertex can be heavy or wide: skip its launch
     // (meshes: ~5 us of a ~80 us round)
     bool need_pblock() const { return g->maxdeg > d.heavy_t || g->maxdeg >= 64; }  // heavy_t is final once hubs are set
@@ -276,6 +290,11 @@ struct Run {
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
         const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
+        if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch
+            kt.begin(GC_K_SWEEP);
+            gcl_sweep_loop(d, L, nsweeps, loop_grid, s);
+            kt.end();
+        }
         if (tail) {
             kt.begin(GC_K_SWEEP);
             gcl_sweep_tail(d, L, nsweeps, s);
@@ -344,7 +363,10 @@ struct Run {
     int pick_sweeps(const DevCtl& h) {
         skip_tail = h.maxdepth <= 1 && h.round >= 16;
         if (h.maxdepth <= 1) return 0;
-        return (int)std::min<long long>(64, h.lastbig + sweep_pad);  // the small-list tail runs in k_sweep_tail
+        // the small-list tail runs in k_sweep_tail; with the loop kernel, the full grid only
+        // takes the sweeps past its limits
+        if (loop_grid > 0) return (int)std::min<long long>(64, h.lasthuge + 1);
+        return (int)std::min<long long>(64, h.lastbig + sweep_pad);
     }
     // rounds per batch: small while the frontier is tiny or the colouring is nearly done
     int pick_batch(const DevCtl& h, long long n, int prev) const {
@@ -466,6 +488,7 @@ struct Run {
             gc_set_error("unexpected device halt code %d", halt);
             return GC_EHIP;
         }
+        if (h.loop_err) { gc_set_error("k_sweep_loop: a grid barrier wait gave up"); return GC_EHIP; }
         kt.begin(GC_K_OTHER);
         gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
         gcl_stat_reduce(d, s);
@@ -541,6 +564,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
             {}, 0};
     // hubs rank above every light vertex only under (deg, pos): seeded ranks use row scans
     if (opt->priority == GC_PRIORITY_REF && (rc = gc_hubs_prepare(g, run.d))) return rc;
+    run.init_loop();
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
     return run.go(colors_out, cround_out);  // stats->rounds may exceed round_cap: the caller re-asks

@@ -46,6 +46,8 @@ typedef unsigned long long ull;
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
 #define GC_ROUND_GRID 1024
 #define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
+#define GC_LOOP_MAX 65536 // ... and over at most this many light vertices in k_sweep_loop
+#define GC_LOOP_HMAX 16384 //   (hubs)
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
 #define GC_BLOCK_GRID 1024
 #define GC_STAT_SLOTS 256
@@ -124,6 +126,13 @@ struct DevCtl {
     long long bigsweeps;    // this round: last full-grid sweep whose input exceeded the tail limits
     long long lastbig;      // bigsweeps of the last closed round (host: full-grid sweeps to enqueue)
     long long tail_last;    // this round: index of the last sweep run (k_sweep_tail)
+    long long hugesweeps;   // this round: last sweep whose input exceeded the loop kernel's limits
+    long long lasthuge;     // hugesweeps of the last closed round (host: full-grid sweeps to enqueue)
+    long long loop_last;    // this round: index of the last sweep run by k_sweep_loop (0: none)
+    unsigned bar;           // k_sweep_loop's grid barrier: arrivals, monotonic over a colouring
+    unsigned bar_base;      //   arrivals at the end of the previous k_sweep_loop launch
+    int loop_err;           //   a barrier wait gave up (never expected; the host reports it)
+    int pad2;
     int use_c4;             // this round's propose gathers the nibble mirror
     int resort;             // this round's frontier is rebuilt in vertex order
     int fsort_all;          // variant B: rebuild the list as EVERY claimed uncoloured vertex, and count it

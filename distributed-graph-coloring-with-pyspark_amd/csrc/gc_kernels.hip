@@ -1105,6 +1105,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
         c->undh_cnt[z] = 0;
         if (cl + ch > 0) c->sweeps += 1;
         if (cl > GC_TAIL_MAX || ch > gc_tail_hmax(g)) c->bigsweeps = i;
+        if (cl > GC_LOOP_MAX || ch > GC_LOOP_HMAX) c->hugesweeps = i;
         if (hub_start) c->hub_start = i;
     }
     if (cl + ch == 0) return;
@@ -1112,6 +1113,85 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                 &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt, hub_start && g.hprep);
     __syncthreads();
+    gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
+}
+
+// Grid barrier of k_sweep_loop (cdna_hip_programming.md §6 G16): every wave drains its
+// stores, the workgroup meets, lane 0 writes back its XCD's L2 (agent release), arrives on
+// the monotonic counter and polls it (relaxed, s_sleep), then invalidates its CU's L1
+// (agent acquire) before the workgroup reads what the other workgroups wrote.  The wait is
+// bounded: a give-up sets DevCtl.loop_err (the host turns it into an error).
+__device__ __forceinline__ void gc_grid_barrier(DevCtl* c, unsigned& target, int* s_err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        target += gridDim.x;
+        __hip_atomic_fetch_add(&c->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        int err = 0;
+        while (__hip_atomic_load(&c->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {  // far beyond any real wait: give up instead of hanging
+                err = 1;
+                __hip_atomic_store(&c->loop_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *s_err = err | __hip_atomic_load(&c->loop_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+// The middle of a round's JP chain in ONE launch: after the host's full-grid sweeps (lists
+// past the loop limits), every later sweep whose lists still exceed the one-workgroup tail's
+// limits runs here, a grid barrier apart, on a grid every workgroup of which is resident
+// (one per CU).  Each such sweep used to be a full-grid launch of ~8-50 us: on R-MAT-26
+// ~12 launches a round, 60% of the sweeps' time.  Sweep bookkeeping as k_sweep.
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_loop(GDev g, GLists L, int S) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    __shared__ long long s_cl, s_ch;
+    __shared__ int s_err;
+    unsigned target = c->bar_base;
+    int j = S;
+    ull lsum = 0, lnv = 0;
+    for (;;) {
+        const int in = j % 3;
+        if (threadIdx.x == 0) {
+            s_cl = (long long)__hip_atomic_load(&c->und_cnt[in], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_ch = (long long)__hip_atomic_load(&c->undh_cnt[in], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        const long long cl = s_cl;
+        long long ch = s_ch;
+        const int* hl = L.undH[in];
+        const bool hub_start = gc_hub_gate(g, c, j + 1, cl, hl, ch, L);
+        // empty, or small enough for the one-workgroup tail (k_sweep_tail takes it from here)
+        if (cl + ch == 0 || (cl <= GC_TAIL_MAX && ch <= gc_tail_hmax(g))) break;
+        ++j;
+        const int out = j % 3, z = (j + 1) % 3;
+        __syncthreads();  // every workgroup has read hub_start before block 0 moves it
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            c->und_cnt[z] = 0;
+            c->undh_cnt[z] = 0;
+            c->sweeps += 1;
+            c->bigsweeps = j;
+            if (cl > GC_LOOP_MAX || ch > GC_LOOP_HMAX) c->hugesweeps = j;
+            if (hub_start) c->hub_start = j;
+        }
+        gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out], &c->undh_cnt[out], lsum,
+                    lnv, L.delta, &c->dcnt, hub_start && g.hprep);
+        gc_grid_barrier(c, target, &s_err);
+        if (s_err) break;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->loop_last = j;
+        c->bar_base = target;
+    }
     gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
 }
 
@@ -1128,7 +1208,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S
     if (c->halt) return;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ long long s_cl, s_ch;
-    int j = S;
+    int j = c->loop_last > S ? (int)c->loop_last : S;  // after k_sweep_loop's sweeps, if it ran
     ull lsum = 0, lnv = 0;
     for (;;) {
         const int in = j % 3;
@@ -1217,6 +1297,8 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
         gc_st(&c->lastdepth, sw);
         gc_st(&c->lastbig, c->bigsweeps);
         gc_st(&c->bigsweeps, 0ll);
+        gc_st(&c->lasthuge, c->hugesweeps);
+        gc_st(&c->hugesweeps, 0ll);
         gc_record(L, c, U, F, c->maxmex, acc, 0, sw);
         U -= acc;
         gc_st(&c->fcnt[cur], 0ull);  // becomes the next round's output slot
@@ -1236,6 +1318,7 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->maxmex, -1ll);
     gc_st(&c->sweeps, 0ll);
     gc_st(&c->hub_start, GC_HUB_NOT_STARTED);
+    gc_st(&c->loop_last, 0ll);
     for (int k = 0; k < 3; ++k) {
         gc_st(&c->und_cnt[k], 0ull);
         gc_st(&c->undh_cnt[k], 0ull);
@@ -2274,6 +2357,9 @@ void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allo
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
+}
+void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep_loop, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S);
 }
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep_tail, dim3(1), dim3(GC_BLOCK), 0, s, g, L, S);

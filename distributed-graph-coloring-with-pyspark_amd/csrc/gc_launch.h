@@ -84,6 +84,7 @@ void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // one-workgroup tail sweeps
+void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0);

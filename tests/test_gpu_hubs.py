@@ -41,14 +41,17 @@ SETTINGS = [
     {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "0"},               # no hub in the one-workgroup tail sweeps
     {"GC_HUB_T": "2", "GC_TAIL_HMAX_HUB": "128"},
     {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "4096"},            # every hub sweep in the tail once lights converge
+    {"GC_HUB_T": "2", "GC_SWEEP_LOOP": "1"},                  # the middle of each JP chain in k_sweep_loop
+    {"GC_HUB_T": "off", "GC_SWEEP_LOOP": "1", "GC_LOOP_WG": "8"},
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
-       "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096"]
+       "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
+       "T2loop", "offloop8"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
-    for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB"):
+    for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP", "GC_LOOP_WG"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
