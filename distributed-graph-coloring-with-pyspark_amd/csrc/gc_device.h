@@ -62,7 +62,7 @@ __device__ __forceinline__ void gc_commit_colour(GDev& g, int v, int cc) {
     g.k8[v] = (unsigned char)gc_k8(GC_K8_NONE, GC_JP_UND);
     if (g.hub_w) {  // hub mirror (gc_hubs.hip)
         const int x = g.hid[v];
-        if (x >= 0) g.hk[x] = (unsigned char)GC_HK_COLOURED;
+        if (x >= 0) g.hk[x] = GC_HK_COLOURED;
     }
 }
 

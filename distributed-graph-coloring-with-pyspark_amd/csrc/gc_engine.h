@@ -64,8 +64,7 @@ struct gc_graph {
     int* hch_own = nullptr;       // static chunk -> hub
     int* hkcnt = nullptr;         // hub x: kept-row entries written by the long-row first pass this round
     long long nhch = 0;           // static chunks
-    unsigned char* hk = nullptr;  // hub-indexed mirror of k8 (0xFF: coloured)
-    int* hcand = nullptr;         // hub-indexed mirror of cand (candidates >= 62)
+    unsigned* hk = nullptr;       // hub-indexed mirror of (candidate, JP state) (gc_hk; GC_HK_COLOURED)
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;

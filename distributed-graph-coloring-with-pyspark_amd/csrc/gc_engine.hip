@@ -78,7 +78,6 @@ GDev gc_view(const gc_graph* g) {
     d.hprep = 0;
     d.hub_scan = 0;
     d.hk = nullptr;
-    d.hcand = nullptr;
     d.hid = nullptr;
     d.hub_v = nullptr;
     d.hin_rp = nullptr;

@@ -112,7 +112,7 @@ __global__ void k_hlow_fill(const long long* rp, const int* col, const int* nlow
             const int hu = e < e1 ? hid[u] : -1;
             const bool p = hu >= 0;
             const ull m = __ballot(p);
-            if (p) hlow_col[o + __popcll(m & gc_lanemask_lt())] = hu;  // hub index (mirrors hk / hcand)
+            if (p) hlow_col[o + __popcll(m & gc_lanemask_lt())] = hu;  // hub index (mirror hk)
             o += __popcll(m);
         }
     }
@@ -267,8 +267,7 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(hipMemcpy(&g->nhch, g->hch_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
     GC_HIP(hipMalloc((void**)&g->hch_own, sizeof(int) * (size_t)std::max<long long>(g->nhch, 1)));
     GC_HIP(hipMalloc((void**)&g->hkcnt, sizeof(int) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hk, (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hcand, sizeof(int) * (size_t)H));
+    GC_HIP(hipMalloc((void**)&g->hk, sizeof(unsigned) * (size_t)H));
     hipLaunchKernelGGL(k_hch_fill, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, g->hch_rp, H, g->hch_own);
     GC_HIP(hipGetLastError());
     GC_HIP(hipStreamSynchronize(s));
@@ -283,13 +282,13 @@ int build(gc_graph* g, int T, int W) {
 void gc_hubs_free(gc_graph* g) {
     void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
                     g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen,
-                    g->hch_rp, g->hch_own, g->hkcnt, g->hk, g->hcand};
+                    g->hch_rp, g->hch_own, g->hkcnt, g->hk};
     for (void* p : ptrs)
         if (p) hipFree(p);
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
     g->hlow2[0] = g->hlow2[1] = g->hrow = g->hlen = nullptr;
     g->hin_rp = g->hlow_rp = g->hch_rp = nullptr;
-    g->hch_own = g->hkcnt = g->hcand = nullptr;
+    g->hch_own = g->hkcnt = nullptr;
     g->hk = nullptr;
     g->nhch = 0;
     g->hbits = g->hkill = nullptr;
@@ -336,7 +335,6 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hch_own = g->hch_own;
     d.hkcnt = g->hkcnt;
     d.hk = g->hk;
-    d.hcand = g->hcand;
     d.nhch = g->nhch;
     d.hub_scan = env_int("GC_HUB_SCAN", 1) > 0;
     d.hprep = !d.hub_scan && env_int("GC_HUB_PREP", 1) > 0 && g->nhch > 0 && d.hub_long >= 0;

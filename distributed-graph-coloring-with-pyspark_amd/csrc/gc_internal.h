@@ -319,7 +319,11 @@ __device__ __forceinline__ unsigned char gc_c8_of(long long c) {
 // the candidate is in cand[]) or GC_K8_NONE (not proposing this round)
 #define GC_K8_BIG 62u
 #define GC_K8_NONE 63u
-#define GC_HK_COLOURED 0xFFu  // hub mirror hk: coloured (cand NONE, state 3)
+// hub mirror hk (one 32-bit word per hub): full candidate << 2 | JP state, so a hub JP
+// step needs ONE gather per row entry (no separate candidate gather past colour 61)
+#define GC_HK_COLOURED 0xFFFFFFFFu  // coloured
+#define GC_HK_NOCAND 0x3FFFFFFEu    // candidate field of a hub that does not propose
+__device__ __forceinline__ unsigned gc_hk(unsigned cand, unsigned st) { return (cand << 2) | st; }
 __device__ __forceinline__ unsigned char gc_k8(unsigned c6, unsigned st) { return (unsigned char)((c6 << 2) | st); }
 __device__ __forceinline__ unsigned gc_c6_of(long long c) { return c >= 62 ? GC_K8_BIG : (unsigned)c; }
 __device__ __forceinline__ unsigned gc_k8_cand(unsigned k) { return k >> 2; }

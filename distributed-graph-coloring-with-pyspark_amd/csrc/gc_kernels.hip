@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
             g.c8[v] = iso ? 0 : (unsigned char)GC_C8_NONE;
             g.k8[v] = push0 ? gc_k8(0u, GC_JP_IN) : gc_k8(GC_K8_NONE, GC_JP_UND);
             if (g.hub_w && g.hid[v] >= 0)  // hub mirror (never isolated)
-                g.hk[g.hid[v]] = gc_k8(GC_K8_NONE, GC_JP_UND);
+                g.hk[g.hid[v]] = gc_hk(GC_HK_NOCAND, GC_JP_UND);
             g.mark[v] = 0;
             if (!iso) {
                 unc++;
@@ -95,7 +95,7 @@ __global__ void k_seed_prep(GDev g, int* seed_light, int* seed_heavy) {
     const int s = (int)(sk & 0xFFFFFFFFull);
     const int d = g.deg[s];
     g.k8[s] = gc_k8(0u, GC_JP_IN);
-    if (g.hub_w && g.hid[s] >= 0) g.hk[g.hid[s]] = gc_k8(0u, GC_JP_IN);
+    if (g.hub_w && g.hid[s] >= 0) g.hk[g.hid[s]] = gc_hk(0u, GC_JP_IN);
     atomicOr(&g.inF[s >> 5], 1u << (s & 31));
     if (d > GC_HEAVY_T) seed_heavy[atomicAdd(&g.ctl->seed_cnt[1], 1ull)] = s;
     else seed_light[atomicAdd(&g.ctl->seed_cnt[0], 1ull)] = s;
@@ -374,8 +374,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
                 g.hpc[x] = 0;
                 if (g.hprep) g.hkcnt[x] = 0;
                 gc_set_cand(g, v, mex);
-                g.hk[x] = gc_k8(gc_c6_of(mex), GC_JP_UND);  // hub mirror
-                g.hcand[x] = (int)mex;
+                g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);  // hub mirror
                 lmax = mex > lmax ? mex : lmax;
                 if (kbound >= 0 && mex >= kbound) lfail++;
                 lsum += (ull)g.deg[v];
@@ -427,8 +426,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
         if (threadIdx.x == 0) {
             gc_set_cand(g, v, mex);
             if (x >= 0) {  // hub mirror
-                g.hk[x] = gc_k8(gc_c6_of(mex), GC_JP_UND);
-                g.hcand[x] = (int)mex;
+                g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);
             }
             lmax = mex > lmax ? mex : lmax;
             if (kbound >= 0 && mex >= kbound) lfail++;
@@ -458,12 +456,12 @@ __device__ __forceinline__ unsigned gc_jp_flag(const GDev& g, int u, unsigned ku
     return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
 }
 
-// gc_jp_flag for a hub entry hx (hub index) from the hub mirrors: hk = k8 of the hub, or
-// GC_HK_COLOURED (cand NONE: never a proposer's candidate)
+// gc_jp_flag for a hub entry hx (hub index) from the hub mirror hk = gc_hk(candidate, state)
+// of the hub, or GC_HK_COLOURED (its candidate field matches no proposal)
 __device__ __forceinline__ unsigned gc_jp_flag_h(const GDev& g, int hx, unsigned hk, unsigned cv6, int cv) {
-    if (gc_k8_cand(hk) != cv6) return 0u;
-    if (cv6 == GC_K8_BIG && g.hcand[hx] != cv) return 0u;
-    const unsigned st = gc_k8_state(hk);
+    (void)g; (void)hx; (void)cv6;
+    if ((hk >> 2) != (unsigned)cv) return 0u;
+    const unsigned st = hk & 3u;
     return st == GC_JP_IN ? 1u : (st == GC_JP_UND ? 2u : 0u);
 }
 
@@ -495,7 +493,7 @@ struct GcHubPre {
 __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv, GcHubPre p) {
     const int lane = gc_lane();
     const ull lt = gc_lanemask_lt();
-    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
+    const unsigned* __restrict__ hk = g.hk;  // rows hold hub indices
     int enc = p.enc;
     const int hc0 = p.hc0;
     const bool first = hc0 == 0;
@@ -597,7 +595,7 @@ __device__ unsigned gc_hub_jp_wave(const GDev& g, int x, unsigned cv6, int cv, G
 // p.hc0 = hcur (0: first evaluation this round), p.enc = cursor, p.hlen = coloured prefix.
 __device__ unsigned gc_hub_scan_wave(const GDev& g, int x, unsigned cv6, int cv, GcHubPre p) {
     const int lane = gc_lane();
-    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
+    const unsigned* __restrict__ hk = g.hk;  // rows hold hub indices
     const bool first = p.hc0 == 0;
     const int full = (int)p.full;
     const int* __restrict__ row = g.hlow_col + p.base;
@@ -656,7 +654,7 @@ __device__ void gc_hub_scan_groups(GDev& g, int nj, int pv, unsigned pkv, int pc
     const int lane = gc_lane();
     const int grp = lane / GS, li = lane % GS;
     const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
-    const unsigned char* __restrict__ hk = g.hk;
+    const unsigned* __restrict__ hk = g.hk;
     for (int j0 = 0; j0 < nj; j0 += GC_HUB_NG) {
         const int j = j0 + grp;
         const bool has = j < nj;
@@ -724,7 +722,7 @@ __device__ void gc_hub_scan_groups(GDev& g, int nj, int pv, unsigned pkv, int pc
             if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
             else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
             if ((f & 1u) || !(f & 2u))  // hub mirror
-                g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
+                g.hk[x] = gc_hk((unsigned)cv, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
             if (dout && ((f & 1u) || !(f & 2u)))
                 dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
             lsum += (ull)g.deg[v];
@@ -775,7 +773,7 @@ __device__ void gc_hub_first_long(GDev& g) {
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const ull lt = gc_lanemask_lt();
-    const unsigned char* __restrict__ hk = g.hk;  // rows hold hub indices
+    const unsigned* __restrict__ hk = g.hk;  // rows hold hub indices
     const long long NC = g.nhch;
     const long long wstride = (long long)gridDim.x * GC_WAVES_PER_BLOCK * GC_WAVE;
     for (long long j0 = ((long long)blockIdx.x * GC_WAVES_PER_BLOCK + w) * GC_WAVE; j0 < NC; j0 += wstride) {
@@ -793,7 +791,8 @@ __device__ void gc_hub_first_long(GDev& g) {
                 len = hr ? g.hlen[x] : (int)full;
             }
             // short row / no proposer / past the live row / flagged (OUT without a read)
-            if (full <= g.hub_long || gc_k8_cand(kx) == GC_K8_NONE || (long long)part * GC_HCH >= len || g.hkill[x])
+            if (full <= g.hub_long || kx == GC_HK_COLOURED || (kx >> 2) == GC_HK_NOCAND || (long long)part * GC_HCH >= len ||
+                g.hkill[x])
                 x = -1;
         }
         ull act = __ballot(x >= 0);
@@ -804,8 +803,8 @@ __device__ void gc_hub_first_long(GDev& g) {
             const int e0 = __shfl(part, sl, GC_WAVE) * GC_HCH;
             const int hl = __shfl(len, sl, GC_WAVE);
             const int hhr = __shfl(hr, sl, GC_WAVE);
-            const unsigned cv6 = gc_k8_cand(__shfl(kx, sl, GC_WAVE));
-            const int cv = cv6 == GC_K8_BIG ? g.hcand[hx] : (int)cv6;
+            const int cv = (int)(__shfl(kx, sl, GC_WAVE) >> 2);
+            const unsigned cv6 = gc_c6_of(cv);
             const long long base = g.hlow_rp[hx];
             const int* __restrict__ hc = g.hlowb[hhr] + base;
             int u[K];
@@ -942,7 +941,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                     if (f & 1u) gc_set_state(g, v, kv, GC_JP_OUT);
                     else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
                     if (x >= 0 && ((f & 1u) || !(f & 2u)))  // hub mirror
-                        g.hk[x] = (unsigned char)((kv & ~3u) | ((f & 1u) ? GC_JP_OUT : GC_JP_IN));
+                        g.hk[x] = gc_hk((unsigned)cv, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
                     if (dout && ((f & 1u) || !(f & 2u)))
                         dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
                     lsum += (ull)g.deg[v];
@@ -1043,10 +1042,9 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
             gc_wave_sync();
             gc_chunk_edges(
-                g.hin_col, s_start[w], hexcl, htotal, [&](int hx) { return (unsigned)k8[g.hub_v[hx]]; },
-                [&](int o, int hx, unsigned kh) {
-                    if (gc_k8_cand(kh) != s_c6[w][o]) return;
-                    if (s_c6[w][o] == GC_K8_BIG && g.cand[g.hub_v[hx]] != s_cv[w][o]) return;
+                g.hin_col, s_start[w], hexcl, htotal, [&](int hx) { return g.hk[hx]; },
+                [&](int o, int hx, unsigned kh) {  // the hub proposes the winner's colour
+                    if ((kh >> 2) != (unsigned)s_cv[w][o]) return;
                     if (!g.hkill[hx]) g.hkill[hx] = 1u;
                 });
         }

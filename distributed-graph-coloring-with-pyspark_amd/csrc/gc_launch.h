@@ -42,8 +42,8 @@ struct GDev {
     long long hch_mul;        //   coprime to nhch, ~0.618 nhch: chunk scan order (a long row's chunks spread out)
     int hprep;                // long-row first pass on (GC_HUB_PREP)
     int hub_scan;             // hub JP by a resumable scan of the rank-sorted row (GC_HUB_SCAN, default on)
-    unsigned char* hk;        // hub x: k8 of hub_v[x], or GC_HK_COLOURED; the hlow rows and pending lists hold
-    int* hcand;               //   hub indices, so hub JP gathers these L2-resident mirrors, not k8 / c8 / cand
+    unsigned* hk;             // hub x: gc_hk(candidate, state) of hub_v[x], or GC_HK_COLOURED; the hlow rows and
+                              //   pending lists hold hub indices, so hub JP gathers this L2-resident mirror
     const int* hid;           // hub index of v, -1 if v is no hub
     const int* hub_v;         // vertex of hub index x
     const long long* hin_rp;  // for every u: the hubs (indices) whose rows list u
