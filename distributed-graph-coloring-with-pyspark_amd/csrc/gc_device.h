@@ -66,6 +66,14 @@ __device__ __forceinline__ void gc_commit_colour(GDev& g, int v, int cc) {
     }
 }
 
+// the same without resetting k8 (fused commit, k_commit<1>: the winner's IN byte stays, so
+// waves proposing for the next round see its colour before its c8 byte lands)
+__device__ __forceinline__ void gc_commit_colour_keep(GDev& g, int v, int cc) {
+    const unsigned char b = gc_c8_of(cc);
+    g.c8[v] = b;
+    if (b == GC_C8_BIG) g.color[v] = cc;
+}
+
 // counters shared across workgroups: read with an atomic RMW, written agent-scope
 __device__ __forceinline__ ull gc_aread(ull* p) { return atomicAdd(p, 0ull); }
 template <typename T>

@@ -71,6 +71,7 @@ struct gc_graph {
     DevCtl* ctl = nullptr;
     DevCtl* hctl = nullptr;    // pinned host mirror
     DevCtl* hsnap = nullptr;   // pinned per-batch snapshots (2, pipelined)
+    DevCtl* hsnap_dev = nullptr;  // the same, as the device addresses k_close writes them through
     hipEvent_t evsnap[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

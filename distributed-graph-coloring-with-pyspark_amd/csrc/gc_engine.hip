@@ -159,6 +159,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->fsum, (size_t)gcl_fsort_blocks(g->n) + 1);
 #undef A
     GC_HIP(hipHostMalloc((void**)&g->hsnap, 2 * sizeof(DevCtl), hipHostMallocDefault));
+    GC_HIP(hipHostGetDevicePointer((void**)&g->hsnap_dev, g->hsnap, 0));
     GC_HIP(hipEventCreateWithFlags(&g->evsnap[0], hipEventDisableTiming));
     GC_HIP(hipEventCreateWithFlags(&g->evsnap[1], hipEventDisableTiming));
     g->rcap = kRoundCap;
@@ -246,6 +247,13 @@ struct Run {
     // k_propose_block has no work unless some vertex can be heavy or wide: skip its launch
     // (meshes: ~5 us of a ~80 us round)
     bool need_pblock() const { return g->maxdeg > d.heavy_t || g->maxdeg >= 64; }  // heavy_t is final once hubs are set
+    // Fused commits (k_commit<1>) make the next round's proposals themselves, so a round
+    // after one runs no k_propose: low-degree graphs (no heavy or wide proposer, no hubs),
+    // small rounds (the big-round frontier rebuild and nibble mirror stay unfused).
+    // GC_FUSE=0 turns it off (A/B measurements).
+    bool fuse_ok = false;
+    bool proposed = false;  // the next round's proposals were made by the last commit enqueued
+    bool fuse_now() const { return fuse_ok && !resort_hint && !c4_hint; }
 
     int sync_ctl() {
         kt.close();
@@ -283,8 +291,8 @@ struct Run {
 
     // big = the host also enqueues the big-round frontier build (k_pull, k_front_*): the
     // device then decides per round (gc_big_on) whether the commit pushes or marks.
-    void launch_commit(int mode, int nsweeps) {
-        const int big = mode == GC_CM_ROUND && resort_hint;
+    void launch_commit(int mode, int nsweeps, bool fuse = false) {
+        const int big = mode == GC_CM_ROUND && resort_hint && !fuse;
         // no sweeps enqueued and >= 16 rounds so far all decided by their first sweep (meshes):
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
@@ -300,7 +308,7 @@ struct Run {
             kt.end();
         }
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
-        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big);
+        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0);
         kt.end();
         if (big) {
             kt.begin(GC_K_COMMIT);
@@ -311,9 +319,11 @@ struct Run {
             kt.end();
         }
         kt.begin(GC_K_OTHER);
-        gcl_close(d, L, mode, s, big);
+        gcl_close(d, L, mode, s, big, fuse ? 1 : 0, mode == GC_CM_ROUND ? snap_ptr : nullptr);
+        if (mode == GC_CM_ROUND) snap_ptr = nullptr;
         kt.end();
         kt.close();  // a round's runs end with it
+        proposed = fuse;
     }
     void launch_sweeps(int from, int to) {  // sweeps from..to inclusive
         for (int i = from; i <= to; ++i) {
@@ -323,6 +333,15 @@ struct Run {
         }
     }
     void enqueue_round(int S) {
+        const bool fuse = fuse_now();
+        if (!proposed) enqueue_propose();
+        kt.begin(GC_K_RESOLVE);
+        gcl_resolve(d, L, s);
+        kt.end();
+        launch_sweeps(1, S);
+        launch_commit(GC_CM_ROUND, S, fuse);
+    }
+    void enqueue_propose() {
         if (resort_hint) {  // device decides; enqueued only while frontiers are within reach of n/64
             kt.begin(GC_K_OTHER);
             gcl_fsort(d, L, g->fsum, s);
@@ -341,17 +360,20 @@ struct Run {
             gcl_propose_block(d, L, s);
             kt.end();
         }
-        kt.begin(GC_K_RESOLVE);
-        gcl_resolve(d, L, s);
-        kt.end();
-        launch_sweeps(1, S);
-        launch_commit(GC_CM_ROUND, S);
     }
     // a batch of rounds followed by an async snapshot of the control block
+    // The batch's last k_close writes the snapshot into the pinned slot itself (a copy
+    // engine blit of the control block cost ~16 us of stream time per batch; GC_SNAP_COPY=1
+    // restores it for A/B measurements).
+    const bool snap_copy = getenv("GC_SNAP_COPY") && atoi(getenv("GC_SNAP_COPY")) > 0;
+    DevCtl* snap_ptr = nullptr;  // handed to the next k_close
     int enqueue_batch(int B, int S, int slot) {
-        for (int b = 0; b < B; ++b) enqueue_round(S);
+        for (int b = 0; b < B; ++b) {
+            if (b == B - 1 && !snap_copy) snap_ptr = g->hsnap_dev + slot;
+            enqueue_round(S);
+        }
         kt.close();
-        GC_HIP(hipMemcpyAsync(&g->hsnap[slot], g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
+        if (snap_copy) GC_HIP(hipMemcpyAsync(&g->hsnap[slot], g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipEventRecord(g->evsnap[slot], s));
         return GC_OK;
     }
@@ -413,6 +435,7 @@ struct Run {
         h.e1 = opt->e1 ? 1 : 0;
         h.rcap = g->rcap;
         h.maxmex = -1;
+        h.nx_maxmex = -1;
         h.hub_start = GC_HUB_NOT_STARTED;
         h.maxcolor = -1;
         h.fail_round = -1;
@@ -450,6 +473,7 @@ struct Run {
                 slot ^= 1;
             }
             if ((rc = sync_ctl())) return rc;
+            proposed = h.proposed != 0;
             if (h.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
             int halt = h.halt;
             // a round deeper than the sweeps enqueued: finish its sweeps, then its commit
@@ -459,10 +483,11 @@ struct Run {
                 const int more = std::max(4, done);
                 if ((rc = clear_halt())) return rc;
                 launch_sweeps(done + 1, done + more);
-                launch_commit(GC_CM_ROUND, done + more);
+                launch_commit(GC_CM_ROUND, done + more, fuse_now());
                 if ((rc = sync_ctl())) return rc;
                 halt = h.halt;
             }
+            proposed = h.proposed != 0;
             S = pick_sweeps(h);
             resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
             c4_hint = pick_c4(h, g->n);
@@ -476,6 +501,7 @@ struct Run {
             if (halt == GC_H_RESEED) {
                 if ((rc = drain_records())) return rc;
                 if ((rc = clear_halt()) || (rc = e1_reseed()) || (rc = sync_ctl())) return rc;
+                proposed = false;
                 if (h.halt == GC_H_DONE) break;
                 if (h.halt == GC_H_RESEED || h.halt == GC_H_ROUNDCAP || h.halt == GC_H_STALLED) {
                     // handled by the synchronous path of the next pass (no rounds run first)
@@ -564,6 +590,10 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     // hubs rank above every light vertex only under (deg, pos): seeded ranks use row scans
     if (opt->priority == GC_PRIORITY_REF && (rc = gc_hubs_prepare(g, run.d))) return rc;
     run.init_loop();
+    {
+        const char* f = getenv("GC_FUSE");
+        run.fuse_ok = !run.need_pblock() && run.d.hub_w == 0 && !(f && atoi(f) == 0);
+    }
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
     return run.go(colors_out, cround_out);  // stats->rounds may exceed round_cap: the caller re-asks

@@ -114,7 +114,7 @@ struct DevCtl {
     ull uncolored;     // init: #uncoloured; validate: #uncoloured
     ull conflicts;     // validate
     ull list_cnt;      // E1: compacted uncoloured list
-    ull ticket;        // (unused)
+    ull nx_failcnt;    // fused commit (k_commit<1>): next round's proposers with mex >= k
     ull dcnt;          // sharded: deltas written this phase
     ull rwin_cnt;      // sharded: other ranks' winners of this round, received as state deltas
     ull bigw_cnt;      // winners deferred to k_commit_big this commit
@@ -141,6 +141,9 @@ struct DevCtl {
     int want_cround;        // commit records the round each vertex was coloured in
     int pad1;
     long long hub_start;    // hubs on: the sweep of this round that started the hubs' JP (the lights had converged)
+    long long nx_maxmex;    // fused commit: next round's max candidate (k_close moves both into place)
+    int proposed;           // the current round's proposals were made by the last (fused) commit
+    int pad3;
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };

@@ -1283,7 +1283,9 @@ __device__ __forceinline__ void gc_precheck(const GLists& L, DevCtl* c, long lon
 // Run by ONE thread of the last workgroup of a commit, after every other workgroup's
 // counter atomics (counters are read back with atomic RMWs, written with agent-scope
 // stores; the next kernel reads them after the launch boundary).
-__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode) {
+// A fused commit (k_commit<1>) made the next round's proposals: their failure count and
+// max candidate move from the nx_ slots into place (else the nx_ slots hold 0 / -1).
+__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode, int fused) {
     const long long acc = (long long)gc_aread(&c->accepted);
     long long U = c->U;
     int cur = c->cur;
@@ -1311,9 +1313,12 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->U, U);
     gc_st(&c->heavy_cnt, 0ull);
     gc_st(&c->wide_cnt, 0ull);
-    gc_st(&c->failcnt, 0ull);
+    gc_st(&c->failcnt, c->nx_failcnt);
     gc_st(&c->accepted, 0ull);
-    gc_st(&c->maxmex, -1ll);
+    gc_st(&c->maxmex, c->nx_maxmex);
+    gc_st(&c->nx_failcnt, 0ull);
+    gc_st(&c->nx_maxmex, -1ll);
+    gc_st(&c->proposed, mode == GC_CM_ROUND && fused ? 1 : 0);
     gc_st(&c->sweeps, 0ll);
     gc_st(&c->hub_start, GC_HUB_NOT_STARTED);
     gc_st(&c->loop_last, 0ll);
@@ -1325,7 +1330,6 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->bigw_cnt, 0ull);
     gc_st(&c->use_c4, 0);  // k_pack_c4 (when the host enqueues it) turns it on for its round
     gc_st(&c->seed_cnt[1], 0ull);
-    gc_st(&c->ticket, 0ull);
     gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
 }
 
@@ -1350,14 +1354,63 @@ __device__ __forceinline__ bool gc_pull_on(const DevCtl* c) {
     return 2 * (c->U - F) <= F && !c->pull_off;
 }
 
+// Fused commit (k_commit<1>; low-degree graphs, no heavy and no wide proposer possible):
+// the wave that stages a vertex for the next frontier also makes its proposal for the
+// next round (k_propose's mex, coloring.py:44-54), saving the next round's k_propose
+// launch.  Every winner of this round is decided before the commit starts, but another
+// wave may not have written its c8 byte yet; under a fused commit a winner keeps its k8
+// byte (IN, candidate = its colour), so colour(u) = c8[u] if set, else the candidate of
+// an IN k8[u], else none.  (A stale IN byte of an earlier winner never blocks a JP step:
+// a proposer's candidate differs from every coloured listed neighbour's colour.)
+__device__ __forceinline__ void gc_fused_propose(GDev& g, const int* buf, int cnt, ull* s_mask, long long* s_start,
+                                                 long long kbound, long long& lmax, ull& lfail, ull& lsum, ull& lnv) {
+    const int lane = gc_lane();
+    for (int b = 0; b < cnt; b += GC_WAVE) {  // cnt is wave-uniform
+        const int i = b + lane;
+        const int v = i < cnt ? buf[i] : -1;
+        const int d = v >= 0 ? g.deg[v] : 0;
+        s_mask[lane] = 0;
+        s_start[lane] = v >= 0 ? g.rp[v] : 0;
+        const int incl = gc_wave_incl_scan(d);
+        const int excl = incl - d;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        gc_chunk_edges(
+            g.col, s_start, excl, total,
+            [&](int u) {
+                const unsigned cb = g.c8[u], kb = g.k8[u];
+                if (cb != GC_C8_NONE) return cb;
+                if (gc_k8_state(kb) != GC_JP_IN) return 255u;
+                const unsigned c6 = gc_k8_cand(kb);
+                return c6 == GC_K8_BIG ? (unsigned)g.cand[u] : c6;
+            },
+            [&](int o, int, unsigned cc) {
+                if (cc < 64u) atomicOr(&s_mask[o], 1ull << cc);
+            });
+        gc_wave_sync();
+        if (v >= 0) {
+            const int mex = __builtin_ctzll(~s_mask[lane]);  // deg < 64: the mask is never full
+            gc_set_cand(g, v, mex);
+            lmax = mex > lmax ? mex : lmax;
+            if (kbound >= 0 && mex >= kbound) lfail++;
+            lsum += (ull)d;
+            lnv++;
+        }
+        gc_wave_sync();
+    }
+}
+
 // mode GC_CM_ROUND: light = F[cur] (hubs skipped), heavy = the heavy list, output F[cur^1];
 // GC_CM_INIT / GC_CM_RESEED: light = seeds[0], heavy = seeds[1], output F[cur].
 // nsweeps: sweeps enqueued for this round; undecided vertices left in the last sweep's
 // slot mean the host must enqueue more sweeps first (GC_H_SWEEPS, resume after nsweeps).
+template <int FUSE>
 __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps, int allow_big) {
     DevCtl* c = g.ctl;
     if (mode == GC_CM_ROUND && c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    __shared__ ull s_pmask[FUSE ? GC_WAVES_PER_BLOCK : 1][GC_WAVE];
+    __shared__ long long s_pstart[FUSE ? GC_WAVES_PER_BLOCK : 1][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
@@ -1392,6 +1445,24 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     GcStage st{s_stage[w], 0};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
+    // fused: the next round's proposals of the staged vertices (before every flush)
+    const long long kbound = c->kbound;
+    long long pmax = -1;
+    ull pfail = 0, psum = 0, pnv = 0;
+    auto propose_staged = [&]() {
+        if (FUSE) gc_fused_propose(g, st.buf, st.cnt, s_pmask[FUSE ? w : 0], s_pstart[FUSE ? w : 0], kbound, pmax, pfail,
+                                   psum, pnv);
+    };
+    auto push = [&](bool pred, int val) {
+        if (FUSE) {
+            const int np = __popcll(__ballot(pred));
+            if (np && st.cnt + np > GC_STAGE_CAP) {
+                propose_staged();
+                gc_stage_flush(st, next, next_cnt);
+            }
+        }
+        gc_stage_push(st, pred, val, next, next_cnt);
+    };
     // hubs on: a wave per hub (in-rows past bigrow are deferred to k_commit_big)
     if (g.hub_w) {
         for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
@@ -1414,7 +1485,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                     if (!walk) L.bigw[atomicAdd(&c->bigw_cnt, 1ull)] = v;  // the whole grid walks it
                 }
             }
-            gc_stage_push(st, lane == 0 && js == GC_JP_OUT && !big, v, next, next_cnt);  // losers stay
+            push(lane == 0 && js == GC_JP_OUT && !big, v);  // losers stay
             if (walk) {
                 gc_hub_mark_row(g, v, cc, lane, GC_WAVE);  // gc_hubs.hip
                 if (mark || !big) {
@@ -1428,7 +1499,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                             if (mark) g.mark[x] = 1;
                             else claim = gc_claim(g.inF, x);
                         }
-                        gc_stage_push(st, claim, x, next, next_cnt);
+                        push(claim, x);
                     }
                 }
             }
@@ -1458,7 +1529,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             s_lose = js == GC_JP_OUT && !big;
         }
         __syncthreads();
-        if (w == 0) gc_stage_push(st, lane == 0 && s_lose, v, next, next_cnt);  // losers stay
+        if (w == 0) push(lane == 0 && s_lose, v);  // losers stay
         if (s_acc && g.hub_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
         if (s_acc && (mark || !big)) {
             const long long ts = g.trp[v], te = g.trp[v + 1];
@@ -1471,7 +1542,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                     if (mark) g.mark[x] = 1;
                     else claim = gc_claim(g.inF, x);
                 }
-                gc_stage_push(st, claim, x, next, next_cnt);
+                push(claim, x);
             }
         }
         __syncthreads();
@@ -1492,7 +1563,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         long long tstart = 0;
         if (acc) {
             cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
-            gc_commit_colour(g, v, cc);
+            if (FUSE) gc_commit_colour_keep(g, v, cc);
+            else gc_commit_colour(g, v, cc);
             if (want_cround) g.cround[v] = round;
             lmaxc = cc > lmaxc ? cc : lmaxc;
             lacc++;
@@ -1502,7 +1574,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             if (big && !mark) din = 0;
         }
         // losers stay in the frontier (they still have a coloured neighbour)
-        gc_stage_push(st, js == GC_JP_OUT && !big, v, next, next_cnt);
+        push(js == GC_JP_OUT && !big, v);
         s_start[w][lane] = tstart;
         const int incl = gc_wave_incl_scan(din);
         const int excl = incl - din;
@@ -1519,7 +1591,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 if (mark) g.mark[x] = 1;
                 else claim = gc_claim(g.inF, x);
             }
-            gc_stage_push(st, claim, x, next, next_cnt);
+            push(claim, x);
         }
         if (g.hub_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
             int dh = 0;
@@ -1543,9 +1615,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         }
         gc_wave_sync();
     }
+    propose_staged();
     gc_stage_flush_block(st, next, next_cnt);
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
+    if (FUSE) {
+        gc_block_max(&c->nx_maxmex, pmax, (long long*)scratch);
+        gc_block_add(&c->nx_failcnt, pfail, scratch);
+        gc_stat_add(g, GC_K_PROPOSE, psum, pnv, scratch);
+    }
     if (g.accs) {  // slotted (k_close sums them): 1024 workgroups on one counter cost ~10 us
         const ull wacc = gc_wave_sum(lacc);
         if (gc_lane() == 0 && wacc) atomicAdd(&g.accs[(blockIdx.x * GC_WAVES_PER_BLOCK + w) % GC_ACC_SLOTS], wacc);
@@ -1709,9 +1787,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_front_count(GDev g, unsigned* bsum
 
 // Closes the round (or the INIT / RESEED seeding) after its commit: one thread, so every
 // counter the commit's workgroups updated is visible across the launch boundary.
-__global__ void k_close(GDev g, GLists L, int mode, int allow_big) {
-    DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) return;
+__device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big, int fused) {
     if (g.accs && blockIdx.x == 0 && threadIdx.x < GC_WAVE) {  // the commit's slotted winner counts
         ull a = 0;
         for (int k = threadIdx.x; k < GC_ACC_SLOTS; k += GC_WAVE) {
@@ -1723,9 +1799,26 @@ __global__ void k_close(GDev g, GLists L, int mode, int allow_big) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
-        gc_close_round(L, c, mode);
+        gc_close_round(L, c, mode, fused);
     }
 }
+
+// snap (host-mapped, or null): afterwards the whole control block is copied there, halted or
+// not, with vector stores; the host reads it once the batch's event has completed.
+__global__ void k_close(GDev g, GLists L, int mode, int allow_big, int fused, DevCtl* snap) {
+    DevCtl* c = g.ctl;
+    if (!(mode == GC_CM_ROUND && c->halt)) gc_close_body(g, L, c, mode, allow_big, fused);
+    if (snap) {
+        static_assert(sizeof(DevCtl) % 8 == 0, "DevCtl is copied as 8-byte words");
+        __syncthreads();
+        const ull* src = reinterpret_cast<const ull*>(c);
+        ull* dst = reinterpret_cast<ull*>(snap);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevCtl) / 8); i += blockDim.x)
+            dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+    }
+}
+
 
 // ------------------------------------------------------------------------------------
 // Sharded rounds (gc_shard.hip): a rank runs the round kernels on its own
@@ -2350,8 +2443,8 @@ void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
 }
 void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
-void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big) {
-    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big);
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big, int fused, DevCtl* snap) {
+    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big, fused, snap);
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
@@ -2365,8 +2458,12 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
-void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big) {
-    hipLaunchKernelGGL(k_commit, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused) {
+    if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
+        hipLaunchKernelGGL(k_commit<1>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+        return;
+    }
+    hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
         hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }

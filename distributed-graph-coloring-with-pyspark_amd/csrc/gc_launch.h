@@ -87,8 +87,10 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // o
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
-void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0);
-void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0);
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0,
+                int fused = 0);
+void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0, int fused = 0,
+               DevCtl* snap = nullptr);
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                int* rwin, hipStream_t s);
