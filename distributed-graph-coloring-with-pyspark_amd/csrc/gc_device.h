@@ -16,35 +16,36 @@ __device__ __forceinline__ long long gc_nchunks(long long cnt, int vpw) { return
 #ifndef GC_SLOTS
 #define GC_SLOTS 2
 #endif
-template <typename Load, typename Apply>
+template <int SLOTS = GC_SLOTS, typename Load, typename Apply>
 __device__ __forceinline__ void gc_chunk_edges_at(const int* __restrict__ col, const long long* s_start, int excl,
                                                   int total, Load load, Apply apply) {
     const int lane = gc_lane();
-    for (int base = 0; base < total; base += GC_SLOTS * GC_WAVE) {
-        int o[GC_SLOTS], x[GC_SLOTS], u[GC_SLOTS];
-        bool ok[GC_SLOTS];
+    for (int base = 0; base < total; base += SLOTS * GC_WAVE) {
+        int o[SLOTS], x[SLOTS], u[SLOTS];
+        bool ok[SLOTS];
 #pragma unroll
-        for (int k = 0; k < GC_SLOTS; ++k) {
+        for (int k = 0; k < SLOTS; ++k) {
             const int e = base + k * GC_WAVE + lane;
             o[k] = gc_owner(excl, e);
             x[k] = e - __shfl(excl, o[k], GC_WAVE);
             ok[k] = e < total;
         }
 #pragma unroll
-        for (int k = 0; k < GC_SLOTS; ++k) u[k] = ok[k] ? col[s_start[o[k]] + x[k]] : 0;
-        decltype(load(0)) gv[GC_SLOTS];
+        for (int k = 0; k < SLOTS; ++k) u[k] = ok[k] ? col[s_start[o[k]] + x[k]] : 0;
+        decltype(load(0)) gv[SLOTS];
 #pragma unroll
-        for (int k = 0; k < GC_SLOTS; ++k) gv[k] = ok[k] ? load(u[k]) : decltype(load(0)){};
+        for (int k = 0; k < SLOTS; ++k) gv[k] = ok[k] ? load(u[k]) : decltype(load(0)){};
 #pragma unroll
-        for (int k = 0; k < GC_SLOTS; ++k)
+        for (int k = 0; k < SLOTS; ++k)
             if (ok[k]) apply(o[k], u[k], gv[k], x[k]);
     }
 }
 
-template <typename Load, typename Apply>
+template <int SLOTS = GC_SLOTS, typename Load, typename Apply>
 __device__ __forceinline__ void gc_chunk_edges(const int* __restrict__ col, const long long* s_start, int excl,
                                                int total, Load load, Apply apply) {
-    gc_chunk_edges_at(col, s_start, excl, total, load, [&](int o, int u, decltype(load(0)) v, int) { apply(o, u, v); });
+    gc_chunk_edges_at<SLOTS>(col, s_start, excl, total, load,
+                             [&](int o, int u, decltype(load(0)) v, int) { apply(o, u, v); });
 }
 
 // colour of u from the byte mirror (-1 uncoloured)

@@ -66,6 +66,7 @@ GDev gc_view(const gc_graph* g) {
     d.accs = nullptr;  // the single-GPU variant-A engine turns it on (Run)
     d.bigrow = getenv("GC_BIGROW") ? atoi(getenv("GC_BIGROW")) : GC_BIGROW;  // env: tests / tuning
     d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= d.bigrow);
+    d.claim_direct = getenv("GC_CLAIM_DIRECT") ? atoi(getenv("GC_CLAIM_DIRECT")) : 0;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hub_long = 0;
@@ -307,9 +308,20 @@ struct Run {
             gcl_sweep_tail(d, L, nsweeps, s);
             kt.end();
         }
+        // the commit's last workgroup closes the round unless k_pull / the big-round frontier
+        // rebuild / k_commit_big must run between the commit and the close
+        const bool tclose = mode == GC_CM_ROUND && !big && (fuse || !d.big_rows) && ticket_close;
+        DevCtl* snap = mode == GC_CM_ROUND ? snap_ptr : nullptr;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
-        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0);
+        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0, tclose ? snap : nullptr,
+                   tclose ? 1 : 0);
         kt.end();
+        if (mode == GC_CM_ROUND) snap_ptr = nullptr;
+        if (tclose) {
+            kt.close();
+            proposed = fuse;
+            return;
+        }
         if (big) {
             kt.begin(GC_K_COMMIT);
             gcl_pull(d, big, s);
@@ -319,8 +331,7 @@ struct Run {
             kt.end();
         }
         kt.begin(GC_K_OTHER);
-        gcl_close(d, L, mode, s, big, fuse ? 1 : 0, mode == GC_CM_ROUND ? snap_ptr : nullptr);
-        if (mode == GC_CM_ROUND) snap_ptr = nullptr;
+        gcl_close(d, L, mode, s, big, fuse ? 1 : 0, snap);
         kt.end();
         kt.close();  // a round's runs end with it
         proposed = fuse;
@@ -366,7 +377,9 @@ struct Run {
     // engine blit of the control block cost ~16 us of stream time per batch; GC_SNAP_COPY=1
     // restores it for A/B measurements).
     const bool snap_copy = getenv("GC_SNAP_COPY") && atoi(getenv("GC_SNAP_COPY")) > 0;
-    DevCtl* snap_ptr = nullptr;  // handed to the next k_close
+    DevCtl* snap_ptr = nullptr;  // handed to the next round's k_close (or closing commit)
+    // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
+    const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
     int enqueue_batch(int B, int S, int slot) {
         for (int b = 0; b < B; ++b) {
             if (b == B - 1 && !snap_copy) snap_ptr = g->hsnap_dev + slot;

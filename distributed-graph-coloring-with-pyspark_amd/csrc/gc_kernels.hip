@@ -989,17 +989,22 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+        // the vertex's words are loaded together (none waits on another: one memory trip)
         const int d = v >= 0 ? g.deg[v] : 0;
+        const int lc0 = (v >= 0 && !skip_heavy) ? g.lcur[v] : 0;
+        const int nl0 = v >= 0 ? g.nlow[v] : 0;
+        const unsigned kv0 = v >= 0 ? (unsigned)k8[v] : 0xFFu;
+        const long long rs0 = v >= 0 ? g.rp[v] : 0;
         const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
         // resumable: entries before lcur[v] were seen decided-not-IN or off-candidate in an
         // earlier sweep of this round (states only move UND -> IN/OUT), so skip them
-        const int lc = (skip || skip_heavy) ? 0 : g.lcur[v];
-        const int dl = skip ? 0 : g.nlow[v] - lc;
-        const unsigned kv = skip ? 0xFFu : (unsigned)k8[v];
+        const int lc = skip ? 0 : lc0;
+        const int dl = skip ? 0 : nl0 - lc;
+        const unsigned kv = skip ? 0xFFu : kv0;
         const unsigned cv6 = skip ? 0x100u : gc_k8_cand(kv);
         s_flag[w][lane] = 0;
         s_first[w][lane] = 0x7FFFFFFF;
-        s_start[w][lane] = v >= 0 ? g.rp[v] + lc : 0;
+        s_start[w][lane] = v >= 0 ? rs0 + lc : 0;
         s_c6[w][lane] = cv6;
         s_cv[w][lane] = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
         const int incl = gc_wave_incl_scan(dl);
@@ -1247,6 +1252,16 @@ __device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
     if (inF[x >> 5] & bit) return false;
     return !(atomicOr(&inF[x >> 5], bit) & bit);
 }
+__device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
+    const unsigned bit = 1u << (x & 31);
+    return !(atomicOr(&inF[x >> 5], bit) & bit);
+}
+#ifndef GC_CSLOTS
+#define GC_CSLOTS 2
+#endif
+#ifndef GC_PREFETCH_ROW
+#define GC_PREFETCH_ROW 1
+#endif
 
 
 __device__ __forceinline__ void gc_record(const GLists& L, DevCtl* c, long long U, long long F, long long maxmex,
@@ -1313,9 +1328,9 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->U, U);
     gc_st(&c->heavy_cnt, 0ull);
     gc_st(&c->wide_cnt, 0ull);
-    gc_st(&c->failcnt, c->nx_failcnt);
+    gc_st(&c->failcnt, gc_aread(&c->nx_failcnt));
     gc_st(&c->accepted, 0ull);
-    gc_st(&c->maxmex, c->nx_maxmex);
+    gc_st(&c->maxmex, (long long)gc_aread(reinterpret_cast<ull*>(&c->nx_maxmex)));
     gc_st(&c->nx_failcnt, 0ull);
     gc_st(&c->nx_maxmex, -1ll);
     gc_st(&c->proposed, mode == GC_CM_ROUND && fused ? 1 : 0);
@@ -1331,6 +1346,65 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->use_c4, 0);  // k_pack_c4 (when the host enqueues it) turns it on for its round
     gc_st(&c->seed_cnt[1], 0ull);
     gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
+}
+
+__device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big, int fused) {
+    if (g.accs && threadIdx.x < GC_WAVE) {  // the commit's slotted winner counts
+        ull a = 0;
+        for (int k = threadIdx.x; k < GC_ACC_SLOTS; k += GC_WAVE) a += atomicExch(&g.accs[k], 0ull);
+        a = gc_wave_sum(a);
+        if (threadIdx.x == 0 && a) atomicAdd(&c->accepted, a);
+    }
+    if (threadIdx.x == 0) {
+        c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
+        gc_close_round(L, c, mode, fused);
+    }
+}
+
+// The whole control block into the host-mapped snapshot slot (one workgroup, every thread
+// calls; vector stores).  Words other workgroups of the same launch updated are read with
+// atomic RMWs, so no cache holds them back.
+__device__ void gc_snap_copy(DevCtl* c, DevCtl* snap) {
+    static_assert(sizeof(DevCtl) % 8 == 0, "DevCtl is copied as 8-byte words");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's control-block stores have landed
+    __syncthreads();
+    ull* src = reinterpret_cast<ull*>(c);
+    ull* dst = reinterpret_cast<ull*>(snap);
+    for (int i = threadIdx.x; i < (int)(sizeof(DevCtl) / 8); i += blockDim.x) dst[i] = atomicAdd(src + i, 0ull);
+    __threadfence_system();
+}
+
+// End-of-commit flush that also closes the round (k_commit with tclose): the one returning
+// atomic a workgroup already spends on the next frontier's counter also carries an arrival
+// ticket in its high bits (count + 2^40), so the workgroup that sees every other arrival
+// knows it is last, with every counter atomic of the launch performed before its ticket
+// (each wave waits for its own atomics before the workgroup barrier that precedes it).
+// Returns true in the last workgroup; *fnext = the next frontier's size.
+#define GC_TICKET_SHIFT 40
+__device__ __forceinline__ bool gc_stage_flush_ticket(GcStage& s, int* out, ull* out_cnt, ull* fnext) {
+    __shared__ int s_cnt[GC_WAVES_PER_BLOCK];
+    __shared__ ull s_base, s_fin;
+    __shared__ int s_last;
+    const int w = threadIdx.x / GC_WAVE;
+    gc_wave_sync();
+    if (gc_lane() == 0) s_cnt[w] = s.cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += s_cnt[i];
+        const ull old = atomicAdd(out_cnt, (1ull << GC_TICKET_SHIFT) | (ull)t);
+        s_base = old & ((1ull << GC_TICKET_SHIFT) - 1);
+        s_fin = s_base + (ull)t;
+        s_last = (old >> GC_TICKET_SHIFT) == (ull)gridDim.x - 1;
+    }
+    __syncthreads();
+    ull base = s_base;
+    for (int i = 0; i < w; ++i) base += (ull)s_cnt[i];
+#pragma unroll 1
+    for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+    s.cnt = 0;
+    *fnext = s_fin;
+    return s_last != 0;
 }
 
 // The frontier of a big round (F >= n/64, with the host's allow_big) is not appended to:
@@ -1362,6 +1436,9 @@ __device__ __forceinline__ bool gc_pull_on(const DevCtl* c) {
 // byte (IN, candidate = its colour), so colour(u) = c8[u] if set, else the candidate of
 // an IN k8[u], else none.  (A stale IN byte of an earlier winner never blocks a JP step:
 // a proposer's candidate differs from every coloured listed neighbour's colour.)
+#ifndef GC_FSLOTS
+#define GC_FSLOTS 4
+#endif
 __device__ __forceinline__ void gc_fused_propose(GDev& g, const int* buf, int cnt, ull* s_mask, long long* s_start,
                                                  long long kbound, long long& lmax, ull& lfail, ull& lsum, ull& lnv) {
     const int lane = gc_lane();
@@ -1375,7 +1452,7 @@ __device__ __forceinline__ void gc_fused_propose(GDev& g, const int* buf, int cn
         const int excl = incl - d;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        gc_chunk_edges(
+        gc_chunk_edges<GC_FSLOTS>(
             g.col, s_start, excl, total,
             [&](int u) {
                 const unsigned cb = g.c8[u], kb = g.k8[u];
@@ -1404,10 +1481,17 @@ __device__ __forceinline__ void gc_fused_propose(GDev& g, const int* buf, int cn
 // GC_CM_INIT / GC_CM_RESEED: light = seeds[0], heavy = seeds[1], output F[cur].
 // nsweeps: sweeps enqueued for this round; undecided vertices left in the last sweep's
 // slot mean the host must enqueue more sweeps first (GC_H_SWEEPS, resume after nsweeps).
+// tclose (ROUND mode, no big-round rebuild and no k_commit_big after it): the last
+// workgroup closes the round itself (k_close's work, see gc_stage_flush_ticket) and, with
+// snap, writes the snapshot; an early return on a halt still writes the snapshot.
 template <int FUSE>
-__global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps, int allow_big) {
+__global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps, int allow_big,
+                                                     DevCtl* snap, int tclose) {
     DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) return;
+    if (mode == GC_CM_ROUND && c->halt) {
+        if (snap && blockIdx.x == 0) gc_snap_copy(c, snap);
+        return;
+    }
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ ull s_pmask[FUSE ? GC_WAVES_PER_BLOCK : 1][GC_WAVE];
     __shared__ long long s_pstart[FUSE ? GC_WAVES_PER_BLOCK : 1][GC_WAVE];
@@ -1426,6 +1510,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             c->sweeps_enq = last;
             c->halt = GC_H_SWEEPS;
         }
+        if (snap && blockIdx.x == 0) gc_snap_copy(c, snap);
         return;
     }
     const int cur = c->cur;
@@ -1554,9 +1639,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
-        const int d = v >= 0 ? g.deg[v] : 0;
+        // the vertex's words are loaded together (its in-row bounds before knowing it won:
+        // one memory trip instead of two); fused: no heavy vertex, so no degree needed
+        const int d = (v >= 0 && !FUSE) ? g.deg[v] : 0;
+        const unsigned kv0 = v >= 0 ? (unsigned)g.k8[v] : 0u;
+#if GC_PREFETCH_ROW
+        const long long ts0 = v >= 0 ? g.trp[v] : 0, te0 = v >= 0 ? g.trp[v + 1] : 0;
+#else
+        const long long ts0 = (v >= 0 && gc_k8_state(kv0) == GC_JP_IN) ? g.trp[v] : 0;
+        const long long te0 = (v >= 0 && gc_k8_state(kv0) == GC_JP_IN) ? g.trp[v + 1] : 0;
+#endif
         const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
-        const unsigned kv = skip ? 0u : (unsigned)g.k8[v];
+        const unsigned kv = skip ? 0u : kv0;
         const unsigned js = skip ? (unsigned)GC_JP_UND : gc_k8_state(kv);
         const bool acc = js == GC_JP_IN;
         int din = 0, cc = 0;
@@ -1568,8 +1662,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             if (want_cround) g.cround[v] = round;
             lmaxc = cc > lmaxc ? cc : lmaxc;
             lacc++;
-            tstart = g.trp[v];
-            din = (int)(g.trp[v + 1] - tstart);
+            tstart = ts0;
+            din = (int)(te0 - tstart);
             lsum += (ull)din;
             if (big && !mark) din = 0;
         }
@@ -1580,18 +1674,31 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         const int excl = incl - din;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            bool claim = false;
-            int x = 0;
-            if (e < total) {
-                x = g.tcol[s_start[w][o] + (e - eo)];
-                if (mark) g.mark[x] = 1;
-                else claim = gc_claim(g.inF, x);
+        // GC_CSLOTS 64-edge groups per step: their tcol loads, then their claims, in flight
+        // together (GC_CLAIM_DIRECT=1, fused: one atomic per claim without the check-load;
+        // measured slower on meshes: neighbours share claim words)
+        for (int base = 0; base < total; base += GC_CSLOTS * GC_WAVE) {
+            int x[GC_CSLOTS];
+            bool ok[GC_CSLOTS], claim[GC_CSLOTS];
+#pragma unroll
+            for (int k = 0; k < GC_CSLOTS; ++k) {
+                const int e = base + k * GC_WAVE + lane;
+                const int o = gc_owner(excl, e);
+                const int eo = __shfl(excl, o, GC_WAVE);
+                ok[k] = e < total;
+                x[k] = ok[k] ? g.tcol[s_start[w][o] + (e - eo)] : 0;
             }
-            push(claim, x);
+#pragma unroll
+            for (int k = 0; k < GC_CSLOTS; ++k) {
+                claim[k] = false;
+                if (ok[k]) {
+                    if (mark) g.mark[x[k]] = 1;
+                    else if (FUSE && g.claim_direct) claim[k] = gc_claim_direct(g.inF, x[k]);
+                    else claim[k] = gc_claim(g.inF, x[k]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < GC_CSLOTS; ++k) push(claim[k], x[k]);
         }
         if (g.hub_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
             int dh = 0;
@@ -1616,7 +1723,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         gc_wave_sync();
     }
     propose_staged();
-    gc_stage_flush_block(st, next, next_cnt);
+    if (!tclose) gc_stage_flush_block(st, next, next_cnt);
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     if (FUSE) {
@@ -1631,6 +1738,16 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         gc_block_add(&c->accepted, lacc, scratch);
     }
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
+    if (tclose) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's counter atomics are performed
+        ull fnext = 0;
+        if (gc_stage_flush_ticket(st, next, next_cnt, &fnext)) {  // the last workgroup closes the round
+            if (threadIdx.x == 0) gc_st(next_cnt, fnext);            // without the tickets
+            __syncthreads();
+            gc_close_body(g, L, c, mode, 0, FUSE);
+            if (snap) gc_snap_copy(c, snap);
+        }
+    }
 }
 
 // Winners whose in-rows exceed bigrow (GC_BIGROW), deferred by k_commit: the grid walks the
@@ -1787,38 +1904,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_front_count(GDev g, unsigned* bsum
 
 // Closes the round (or the INIT / RESEED seeding) after its commit: one thread, so every
 // counter the commit's workgroups updated is visible across the launch boundary.
-__device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big, int fused) {
-    if (g.accs && blockIdx.x == 0 && threadIdx.x < GC_WAVE) {  // the commit's slotted winner counts
-        ull a = 0;
-        for (int k = threadIdx.x; k < GC_ACC_SLOTS; k += GC_WAVE) {
-            a += g.accs[k];
-            g.accs[k] = 0ull;
-        }
-        a = gc_wave_sum(a);
-        if (threadIdx.x == 0 && a) atomicAdd(&c->accepted, a);
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
-        gc_close_round(L, c, mode, fused);
-    }
-}
 
 // snap (host-mapped, or null): afterwards the whole control block is copied there, halted or
 // not, with vector stores; the host reads it once the batch's event has completed.
 __global__ void k_close(GDev g, GLists L, int mode, int allow_big, int fused, DevCtl* snap) {
     DevCtl* c = g.ctl;
     if (!(mode == GC_CM_ROUND && c->halt)) gc_close_body(g, L, c, mode, allow_big, fused);
-    if (snap) {
-        static_assert(sizeof(DevCtl) % 8 == 0, "DevCtl is copied as 8-byte words");
-        __syncthreads();
-        const ull* src = reinterpret_cast<const ull*>(c);
-        ull* dst = reinterpret_cast<ull*>(snap);
-        for (int i = threadIdx.x; i < (int)(sizeof(DevCtl) / 8); i += blockDim.x)
-            dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
-    }
+    if (snap) gc_snap_copy(c, snap);
 }
-
 
 // ------------------------------------------------------------------------------------
 // Sharded rounds (gc_shard.hip): a rank runs the round kernels on its own
@@ -2458,12 +2551,14 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
-void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused) {
+void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused,
+                DevCtl* snap, int tclose) {
     if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
-        hipLaunchKernelGGL(k_commit<1>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+        hipLaunchKernelGGL(k_commit<1>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap,
+                           tclose);
         return;
     }
-    hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big);
+    hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
         hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }

@@ -27,6 +27,7 @@ struct GDev {
     ull* accs;            // GC_ACC_SLOTS winner-count slots (single-GPU engine), else null
     int big_rows;         // some in-row (+ hub row) may exceed bigrow: k_commit_big is needed
     int bigrow;           // heavy winners with longer in-rows (+ hub rows) go to k_commit_big (GC_BIGROW)
+    int claim_direct;     // fused commit: claim with one atomic, no check-load first (GC_CLAIM_DIRECT)
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
@@ -87,8 +88,10 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // o
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
+// tclose: the commit's last workgroup also closes the round (no k_close; ROUND mode only,
+// never with allow_big or when k_commit_big follows); snap: its snapshot slot, or null
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0,
-                int fused = 0);
+                int fused = 0, DevCtl* snap = nullptr, int tclose = 0);
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0, int fused = 0,
                DevCtl* snap = nullptr);
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);

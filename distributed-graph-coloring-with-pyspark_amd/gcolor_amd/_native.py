@@ -11,6 +11,10 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "lib", "libgcolor.so")
+# measurement builds of the same sources with other compile-time settings
+# (tools/build_variant.sh); never a fallback: the path must exist
+if os.environ.get("GC_LIB_PATH"):
+    LIB_PATH = os.environ["GC_LIB_PATH"]
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 GC_OK, GC_FAILED, GC_STALLED = 0, 1, 2
