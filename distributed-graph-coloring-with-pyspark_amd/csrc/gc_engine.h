@@ -80,6 +80,8 @@ struct gc_graph {
     bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
     bool own_stream = true;    // false: the caller's stream (gc_shard_set_stream), not destroyed here
     int part_prio = 0;         // rank the rows are partitioned for (gc_set_priority)
+    bool bpart = false;        // low parts also split by degree (variant B: equal-degree entries last, neq counts them)
+    int* neq = nullptr;
     uint64_t part_seed = 0;
 };
 

@@ -142,6 +142,8 @@ struct DevCtl {
     int pad1;
     long long hub_start;    // hubs on: the sweep of this round that started the hubs' JP (the lights had converged)
     long long nx_maxmex;    // fused commit: next round's max candidate (k_close moves both into place)
+    ull bcnt[9];            // variant B work lists: kind (0 light admission, 1 heavy admission, 2 eviction) x 3 rotating slots
+    ull pad4;
     int proposed;           // the current round's proposals were made by the last (fused) commit
     int pad3;
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)

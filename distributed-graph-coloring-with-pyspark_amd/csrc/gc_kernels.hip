@@ -2385,8 +2385,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, in
 // first), written to `out` with the marks cleared.  Each 64-slot step ranks a lane among
 // the same-owner, same-side lanes before it with a ballot; running counts per row live
 // in LDS.  Deterministic; rows of any length (a wave walks its 64 rows' edges).
-__global__ void __launch_bounds__(GC_BLOCK) k_partition_rows(const long long* rp, const int* col, const int* deg,
-                                                             const int* nlow, int n, int* out) {
+// Row v's range is [rp[v], rp[v] + len[v]); its unmarked entries go first, the marked ones
+// from rp[v] + split[v] (len = deg, split = nlow: the rank partition; variant B also splits
+// the low parts, gc_variant_b.hip).
+__global__ void __launch_bounds__(GC_BLOCK) k_partition_rows(const long long* rp, const int* col, const int* len,
+                                                             const int* split, int n, int* out) {
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_lo[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ long long s_hi[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -2397,11 +2400,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_partition_rows(const long long* rp
          chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long v = chunk * GC_WAVE + lane;
         const bool valid = v < n;
-        const int d = valid ? deg[v] : 0;
+        const int d = valid ? len[v] : 0;
         const long long st = valid ? rp[v] : 0;
         s_start[w][lane] = st;
         s_lo[w][lane] = st;
-        s_hi[w][lane] = st + (valid ? nlow[v] : 0);
+        s_hi[w][lane] = st + (valid ? split[v] : 0);
         const int incl = gc_wave_incl_scan(d);
         const int excl = incl - d;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -2583,9 +2586,9 @@ void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStr
 void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, key, n, nlow);
 }
-void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
+void gcl_partition_rows(const long long* rp, const int* col, const int* len, const int* split, int n, int* out,
                         int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_partition_rows, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, deg, nlow, n, out);
+    hipLaunchKernelGGL(k_partition_rows, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, len, split, n, out);
 }
 void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, deg, maxdeg);

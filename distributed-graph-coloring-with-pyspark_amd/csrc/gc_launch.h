@@ -105,7 +105,7 @@ void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, l
 void gcl_shard_flip(const GDev& g, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
 void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s);
-void gcl_partition_rows(const long long* rp, const int* col, const int* deg, const int* nlow, int n, int* out,
+void gcl_partition_rows(const long long* rp, const int* col, const int* len, const int* split, int n, int* out,
                         int grid, hipStream_t s);
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);

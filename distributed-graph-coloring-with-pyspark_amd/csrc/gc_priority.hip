@@ -175,6 +175,7 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
     }
     g->part_prio = prio;
     g->part_seed = seed;
+    g->bpart = false;  // the low parts were rebuilt
     return GC_OK;
 }
 

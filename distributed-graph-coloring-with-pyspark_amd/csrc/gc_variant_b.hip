@@ -64,6 +64,7 @@ __global__ void k_b_reset(GDev g, long long round) {
     c->accepted = 0;
     c->fsort_all = 1;
     for (int k = 0; k < 3; ++k) c->und_cnt[k] = 0;
+    for (int k = 0; k < 9; ++k) c->bcnt[k] = 0;
 }
 
 // bounded attempt with k = 0: only proposers WITH a coloured neighbour fail
@@ -84,22 +85,109 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_fail0(GDev g, GLists L) {
     gc_block_add(&c->failcnt, lf, scratch);
 }
 
-// ev pass over the admitted vertices whose eviction time is not final
-__global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, GLists L, int* ev) {
+// Work lists.  Every pass reads slot i % 3 of three lists -- light admission (UND
+// vertices), heavy admission (UND vertices whose remaining range exceeds GC_B_HEAVY: a
+// workgroup each) and eviction (admitted vertices whose eviction time is not final) --
+// writes slot (i + 1) % 3 and clears the counters of slot (i + 2) % 3 (read by pass i - 1,
+// written by pass i + 1): one launch per list kind per pass, no host round trip.
+#define GC_B_HEAVY 2048
+struct BLists {
+    int* l[3][3];  // [kind][slot]
+};
+__device__ __forceinline__ ull* b_cnt(DevCtl* c, int kind, int slot) { return &c->bcnt[kind * 3 + slot]; }
+
+// Row layout (ensure_bpart): [lower degree | equal degree, earlier | higher rank].  The
+// admission of v can only be blocked by an earlier u with deg(u) >= deg(v): the entries
+// from nlow[v] - neq[v] on.  An evictor of u has a higher degree: the entries from
+// nlow[u] on.
+__global__ void __launch_bounds__(GC_BLOCK) k_b_eqflags(const long long* rp, int* col, const int* deg, const int* nlow,
+                                                         int n, int* neq, int* split) {
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cnt[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
+    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
+         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v = chunk * GC_WAVE + lane;
+        const bool valid = v < n;
+        const int len = valid ? nlow[v] : 0;
+        s_start[w][lane] = valid ? rp[v] : 0;
+        s_cnt[w][lane] = 0;
+        s_d[w][lane] = valid ? deg[v] : 0;
+        const int incl = gc_wave_incl_scan(len);
+        const int excl = incl - len;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            if (e < total) {
+                const long long ei = s_start[w][o] + (e - eo);
+                const int u = col[ei];
+                if (deg[u] == s_d[w][o]) {
+                    atomicAdd(&s_cnt[w][o], 1);
+                    col[ei] = (int)((unsigned)u | 0x80000000u);
+                }
+            }
+        }
+        gc_wave_sync();
+        if (valid) {
+            neq[v] = s_cnt[w][lane];
+            split[v] = len - s_cnt[w][lane];
+        }
+    }
+}
+
+// Round start: every proposer is undecided; its admission range starts at the equal-degree
+// entries; eviction times unknown (-1).
+__global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B, int* ev, const int* neq) {
     DevCtl* c = g.ctl;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    const int w = threadIdx.x / GC_WAVE;
+    GcStage st{s_stage[w], 0};
+    const long long cnt = (long long)c->fcnt[c->cur];
+    const int* list = L.F[c->cur];
+    const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long i = sidx * GC_WAVE + gc_lane();
+        const int v = i < cnt ? list[i] : -1;
+        bool heavy = false;
+        if (v >= 0) {
+            const int bc = g.nlow[v] - neq[v];
+            g.lcur[v] = bc;
+            ev[v] = -1;
+            heavy = g.deg[v] - bc > GC_B_HEAVY;
+        }
+        gc_wave_append(heavy, v, B.l[1][0], b_cnt(c, 1, 0));
+        gc_stage_push(st, v >= 0 && !heavy, v, B.l[0][0], b_cnt(c, 0, 0));
+    }
+    gc_stage_flush_block(st, B.l[0][0], b_cnt(c, 0, 0));
+}
+
+// eviction pass over list slot i % 3: ev(u) = the smallest not-refused potential evictor
+// (v' > u listed by u, same candidate, deg(v') > deg(u)); final once that evictor is
+// admitted or there is none (INF), else u stays listed
+__global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, BLists B, int* ev, int pass) {
+    DevCtl* c = g.ctl;
+    const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
+    if (blockIdx.x == 0 && threadIdx.x < 3) *b_cnt(c, threadIdx.x, zs) = 0ull;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_min[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const int* __restrict__ list = L.F[c->cur];
-    const long long cnt = (long long)c->fcnt[c->cur];
+    const int* __restrict__ list = B.l[2][rs];
+    const long long cnt = (long long)*b_cnt(c, 2, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    ull pend = 0;
+    GcStage st{s_stage[w], 0};
     const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -107,56 +195,91 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, GLists L, int* ev) {
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0u;
-        bool act = false;
-        if (v >= 0 && gc_k8_state(kv) == GC_JP_IN) {
-            const int e = ev[v];
-            act = e < 0 || (e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN);
-        }
-        const int d = act ? g.deg[v] : 0;
-        s_start[w][lane] = act ? g.rp[v] : 0;
+        const int d = v >= 0 ? g.deg[v] : 0;
+        const int lo = v >= 0 ? g.nlow[v] : 0;
+        const int len = d - lo;
+        s_start[w][lane] = v >= 0 ? g.rp[v] + lo : 0;
         s_min[w][lane] = GC_B_INF;
         s_v[w][lane] = v;
         s_d[w][lane] = d;
-        s_c6[w][lane] = act ? gc_k8_cand(kv) : 0x100u;
-        s_cv[w][lane] = act ? b_cand(g, v, kv) : -1;
-        const int incl = gc_wave_incl_scan(d);
-        const int excl = incl - d;
+        s_c6[w][lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        s_cv[w][lane] = v >= 0 ? b_cand(g, v, kv) : -1;
+        const int incl = gc_wave_incl_scan(len);
+        const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
         gc_chunk_edges(
-            g.col, s_start[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
-            [&](int o, int u, unsigned ku) {
+            g.col, s_start[w], excl, total,
+            [&](int u) { return ((ull)(unsigned)g.deg[u] << 32) | (ull)k8[u]; },
+            [&](int o, int u, ull du) {
+                const unsigned ku = (unsigned)du & 0xFFu;
                 if (u <= s_v[w][o] || gc_k8_state(ku) == GC_JP_OUT) return;
+                if ((int)(du >> 32) <= s_d[w][o]) return;
                 if (!b_same(g, u, ku, s_c6[w][o], s_cv[w][o])) return;
-                if (g.deg[u] > s_d[w][o]) atomicMin(&s_min[w][o], u);
+                atomicMin(&s_min[w][o], u);
             });
         gc_wave_sync();
-        if (act) {
+        bool pend = false;
+        if (v >= 0) {
             const int e = s_min[w][lane];
             ev[v] = e;
-            if (e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN) pend++;
+            pend = e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN;
         }
+        gc_stage_push(st, pend, v, B.l[2][ws], b_cnt(c, 2, ws));
     }
-    __syncthreads();
-    gc_block_add(&c->und_cnt[1], pend, scratch);
+    gc_stage_flush_block(st, B.l[2][ws], b_cnt(c, 2, ws));
 }
 
-// admission pass over the undecided vertices
-__global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, GLists L, const int* ev) {
+// admission flag of one entry u for v (vo): 1 = u admitted and still present at v's
+// arrival (v refused), 2 = not known yet, 0 = never matters again.  Entries in the range
+// all have deg(u) >= deg(v) (row layout above).
+__device__ __forceinline__ unsigned b_adm_flag(const GDev& g, int vo, int u, unsigned ku, unsigned c6, int cv,
+                                               const int* ev) {
+    if (u >= vo) return 0u;  // later arrivals (and self-loops) never count
+    const unsigned st = gc_k8_state(ku);
+    if (st == GC_JP_OUT || !b_same(g, u, ku, c6, cv)) return 0u;
+    if (st != GC_JP_IN) return 2u;
+    const int e = ev[u];
+    if (e > vo) return 1u;                                   // still admitted at v's arrival
+    if (e >= 0 && gc_k8_state(g.k8[e]) == GC_JP_IN) return 0u;  // evicted before v
+    return 2u;                                               // eviction time not known yet
+}
+
+// decision of v after a scan: OUT / IN (listed for its eviction time) / still undecided
+// (resumes at its first pending entry; light or heavy list by the range left)
+__device__ __forceinline__ void b_adm_decide(GDev& g, BLists& B, DevCtl* c, int ws, int v, unsigned kv, unsigned f,
+                                             int first, int* dst_kind) {
+    *dst_kind = -1;
+    if (f & 1u) {
+        g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_OUT);
+    } else if (f & 2u) {
+        const int bc = g.lcur[v] + first;
+        g.lcur[v] = bc;
+        *dst_kind = g.deg[v] - bc > GC_B_HEAVY ? 1 : 0;
+    } else {
+        g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
+        *dst_kind = 2;
+    }
+}
+
+// admission pass over the light list, slot i % 3
+__global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int* ev, int pass) {
     DevCtl* c = g.ctl;
+    const int rs = pass % 3, ws = (pass + 1) % 3;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    __shared__ int s_estage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_first[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    const int* __restrict__ list = L.F[c->cur];
-    const long long cnt = (long long)c->fcnt[c->cur];
+    const int* __restrict__ list = B.l[0][rs];
+    const long long cnt = (long long)*b_cnt(c, 0, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    ull und = 0;
+    GcStage st{s_stage[w], 0}, est{s_estage[w], 0};
     const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -164,44 +287,89 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, GLists L, const int*
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0u;
-        const bool act = v >= 0 && gc_k8_state(kv) == GC_JP_UND;
-        const int d = act ? g.deg[v] : 0;
-        s_start[w][lane] = act ? g.rp[v] : 0;
+        const int d = v >= 0 ? g.deg[v] : 0;
+        const int bc = v >= 0 ? g.lcur[v] : 0;
+        const long long rs0 = v >= 0 ? g.rp[v] : 0;
+        const int len = d - bc;
+        s_start[w][lane] = rs0 + bc;
         s_flag[w][lane] = 0;
+        s_first[w][lane] = 0x7FFFFFFF;
         s_v[w][lane] = v;
-        s_d[w][lane] = d;
-        s_c6[w][lane] = act ? gc_k8_cand(kv) : 0x100u;
-        s_cv[w][lane] = act ? b_cand(g, v, kv) : -1;
-        const int incl = gc_wave_incl_scan(d);
-        const int excl = incl - d;
+        s_c6[w][lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        s_cv[w][lane] = v >= 0 ? b_cand(g, v, kv) : -1;
+        const int incl = gc_wave_incl_scan(len);
+        const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        gc_chunk_edges(
+        gc_chunk_edges_at(
             g.col, s_start[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
-            [&](int o, int u, unsigned ku) {
-                const int vo = s_v[w][o];
-                if (u >= vo) return;  // later arrivals (and self-loops) never count
-                const unsigned st = gc_k8_state(ku);
-                if (st == GC_JP_OUT || !b_same(g, u, ku, s_c6[w][o], s_cv[w][o])) return;
-                if (g.deg[u] < s_d[w][o]) return;
-                unsigned f = 2u;  // undecided, or admitted with an eviction time not yet known
-                if (st == GC_JP_IN) {
-                    const int e = ev[u];
-                    if (e > vo) f = 1u;                                   // still admitted at v's arrival
-                    else if (e >= 0 && gc_k8_state(k8[e]) == GC_JP_IN) f = 0u;  // evicted before v
-                }
+            [&](int o, int u, unsigned ku, int slot) {
+                const unsigned f = b_adm_flag(g, s_v[w][o], u, ku, s_c6[w][o], s_cv[w][o], ev);
                 if (f) atomicOr(&s_flag[w][o], f);
+                if (f == 2u) atomicMin(&s_first[w][o], slot);
             });
         gc_wave_sync();
-        if (act) {
-            const unsigned f = s_flag[w][lane];
-            if (f & 1u) g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_OUT);
-            else if (f & 2u) und++;
-            else g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
-        }
+        int kind = -1;
+        if (v >= 0) b_adm_decide(g, B, c, ws, v, kv, s_flag[w][lane], s_first[w][lane], &kind);
+        gc_wave_append(kind == 1, v, B.l[1][ws], b_cnt(c, 1, ws));
+        gc_stage_push(st, kind == 0, v, B.l[0][ws], b_cnt(c, 0, ws));
+        gc_stage_push(est, kind == 2, v, B.l[2][ws], b_cnt(c, 2, ws));
     }
-    __syncthreads();
-    gc_block_add(&c->und_cnt[0], und, scratch);
+    gc_stage_flush_block(st, B.l[0][ws], b_cnt(c, 0, ws));
+    gc_stage_flush_block(est, B.l[2][ws], b_cnt(c, 2, ws));
+}
+
+// admission pass over the heavy list, slot i % 3: a workgroup per vertex
+__global__ void __launch_bounds__(GC_BLOCK) k_b_adm_heavy(GDev g, BLists B, const int* ev, int pass) {
+    DevCtl* c = g.ctl;
+    const int rs = pass % 3, ws = (pass + 1) % 3;
+    const long long cnt = (long long)*b_cnt(c, 1, rs);
+    if (cnt == 0) return;
+    __shared__ unsigned s_flag;
+    __shared__ int s_first;
+    const int* list = B.l[1][rs];
+    for (long long i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int v = list[i];
+        const unsigned kv = g.k8[v];
+        const unsigned c6 = gc_k8_cand(kv);
+        const int cv = b_cand(g, v, kv);
+        const int bc = g.lcur[v];
+        const long long s0 = g.rp[v] + bc, s1 = g.rp[v] + g.deg[v];
+        if (threadIdx.x == 0) {
+            s_flag = 0u;
+            s_first = 0x7FFFFFFF;
+        }
+        __syncthreads();
+        for (long long e0 = s0; e0 < s1; e0 += GC_SLOTS * (long long)blockDim.x) {
+            int u[GC_SLOTS];
+            unsigned ku[GC_SLOTS];
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) {
+                const long long e = e0 + (long long)k * blockDim.x + threadIdx.x;
+                u[k] = e < s1 ? g.col[e] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) ku[k] = u[k] >= 0 ? (unsigned)g.k8[u[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) {
+                if (u[k] < 0) continue;
+                const unsigned f = b_adm_flag(g, v, u[k], ku[k], c6, cv, ev);
+                if (f) atomicOr(&s_flag, f);
+                if (f == 2u) atomicMin(&s_first, (int)(e0 + (long long)k * blockDim.x + threadIdx.x - s0));
+            }
+            __syncthreads();
+            const bool refused = (s_flag & 1u) != 0;  // refused: the rest cannot change it
+            __syncthreads();
+            if (refused) break;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int kind = -1;
+            b_adm_decide(g, B, c, ws, v, kv, s_flag, s_first, &kind);
+            if (kind >= 0) B.l[kind][ws][atomicAdd(b_cnt(c, kind, ws), 1ull)] = v;
+        }
+        __syncthreads();
+    }
 }
 
 // winners: admitted and never evicted, coloured (coloring_optimized.py:129-140)
@@ -250,8 +418,41 @@ struct RunB {
 
 }  // namespace
 
+// Splits every row's low part (once per graph and row partition): lower-degree entries
+// first, then the equal-degree ones (all earlier in file order under the (deg, pos) rank);
+// neq[v] counts the latter.  Variant A never looks inside a low part, so it is unaffected.
+static int ensure_bpart(gc_graph* g) {
+    if (g->bpart) return GC_OK;
+    if (g->part_prio != GC_PRIORITY_REF) { gc_set_error("variant B needs the (deg, pos) row partition"); return GC_EINVAL; }
+    const hipStream_t s = g->stream;
+    if (!g->neq) GC_HIP(hipMalloc((void**)&g->neq, sizeof(int) * (size_t)std::max<long long>(g->n, 1)));
+    if (g->n > 0) GC_HIP(hipMemsetAsync(g->neq, 0, sizeof(int) * (size_t)g->n, s));
+    if (g->n > 0 && g->nnz > 0) {
+        int *tmp = nullptr, *split = nullptr;
+        if (hipMalloc((void**)&tmp, sizeof(int) * (size_t)g->nnz) != hipSuccess ||
+            hipMalloc((void**)&split, sizeof(int) * (size_t)g->n) != hipSuccess) {
+            hipFree(tmp);
+            gc_set_error("hipMalloc of the variant B row split scratch failed");
+            return GC_ENOMEM;
+        }
+        const int grid = gc_grid_for_waves(g->n, 8192);
+        hipMemcpyAsync(tmp, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);  // keeps the high parts
+        hipLaunchKernelGGL(k_b_eqflags, dim3(grid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->deg, g->nlow, (int)g->n,
+                           g->neq, split);
+        gcl_partition_rows(g->rp, g->col, g->nlow, split, (int)g->n, tmp, grid, s);
+        hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
+        const hipError_t e = hipStreamSynchronize(s);
+        hipFree(tmp);
+        hipFree(split);
+        if (e != hipSuccess || hipGetLastError() != hipSuccess) { gc_set_error("variant B row split failed"); return GC_EHIP; }
+    }
+    g->bpart = true;
+    return GC_OK;
+}
+
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out, gc_stats* st) {
     RunB R{g, gc_view(g), gc_lists(g), g->stream};
+    int rc;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
@@ -273,8 +474,14 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // every vertex counts as claimed: the re-sort then lists exactly the uncoloured ones
     GC_HIP(hipMemsetAsync(g->inF, 0xFF, sizeof(unsigned) * (size_t)((g->n + 63) / 32 + 2), s));
     int* ev = g->parent;  // E1 scratch, unused by variant B
+    if ((rc = ensure_bpart(g))) return rc;
+    // work lists (variant A's undecided, seed and E1 lists are free during variant B)
+    BLists B;
+    int* const wl[9] = {g->undL[0], g->undL[1], g->undL[2], g->seeds[0], g->seeds[1], g->bigw,
+                        g->undH[0], g->undH[1], g->undH[2]};
+    for (int k = 0; k < 9; ++k) B.l[k / 3][k % 3] = wl[k];
     std::vector<RoundRec> recs;
-    int status = GC_OK, rc;
+    int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;
     const long long max_rounds = 4ll * g->n + 16;
     for (long long r = 0;; ++r) {
@@ -303,25 +510,24 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             fail_count = (long long)h.failcnt;
             break;
         }
-        GC_HIP(hipMemsetAsync(ev, 0xFF, sizeof(int) * (size_t)g->n, s));
+        // the fold's passes over the work lists until no vertex is undecided and every
+        // admitted vertex's eviction time is final
+        hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
         long long passes = 0;
         for (int batch = 2;; batch = std::min(batch * 2, 16)) {
-            for (int j = 0; j < batch; ++j) {
-                if ((rc = R.zero(&g->ctl->und_cnt[0])) || (rc = R.zero(&g->ctl->und_cnt[1]))) return rc;
-                hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, ev);
-                hipLaunchKernelGGL(k_b_adm, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev);
+            for (int j = 0; j < batch; ++j, ++passes) {
+                const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
+                hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+                hipLaunchKernelGGL(k_b_adm, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
+                hipLaunchKernelGGL(k_b_adm_heavy, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
-            passes += batch;
             if ((rc = R.sync())) return rc;
-            if (h.und_cnt[0] == 0) break;
-            if (passes > g->n + 64) { gc_set_error("variant B passes do not converge"); return GC_EROUNDS; }
+            const int ws = (int)(passes % 3);  // written by the last pass
+            if (h.bcnt[ws] + h.bcnt[3 + ws] + h.bcnt[6 + ws] == 0) break;
+            if (passes > 2 * g->n + 64) { gc_set_error("variant B passes do not converge"); return GC_EROUNDS; }
         }
-        // every admission is decided: one more ev pass makes every eviction time final
-        if ((rc = R.zero(&g->ctl->und_cnt[1]))) return rc;
-        hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, ev);
         hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev);
         if ((rc = R.sync())) return rc;
-        if (h.und_cnt[1] != 0) { gc_set_error("variant B: eviction times not final"); return GC_EHIP; }
         recs.push_back(RoundRec{U, U, maxmex, (long long)h.accepted, 0, passes});
         sweeps_total += passes;
     }

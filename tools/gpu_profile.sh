@@ -27,5 +27,9 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -T -f csv -d "$OUT/pmc_write" -o 
   python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --steps 2 --warmup 0 "$@" > "$OUT/pmc_write.log" 2>&1
 cd "$ROOT"
 python tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.json"
-head -c 1500 "$OUT/pmc_summary.json"
+python tools/sweep_view.py "$OUT/trace/run_kernel_trace.csv" > "$OUT/sweep_view.txt" || true
+python tools/gaps.py "$OUT/trace/run_kernel_trace.csv" 8 > "$OUT/gaps.txt" || true
+# the raw per-dispatch CSVs run to tens of MB per workload (gpurun merges back <= 64 MiB):
+# keep the summaries above and the kernel stats only
+rm -f "$OUT"/trace/run_kernel_trace.csv "$OUT"/pmc_fetch/run_counter_collection.csv "$OUT"/pmc_write/run_counter_collection.csv
 echo "gpu_profile done: $OUT"
