@@ -61,6 +61,8 @@ __global__ void k_b_reset(GDev g, long long round) {
     c->wide_cnt = 0;
     c->failcnt = 0;
     c->maxmex = -1;
+    c->bigw_cnt = 0;
+    c->dcnt = c->accepted;  // the previous round's winners (read with this round's snapshot)
     c->accepted = 0;
     c->fsort_all = 1;
     for (int k = 0; k < 3; ++k) c->und_cnt[k] = 0;
@@ -262,8 +264,64 @@ __device__ __forceinline__ void b_adm_decide(GDev& g, BLists& B, DevCtl* c, int 
     }
 }
 
-// admission pass over the light list, slot i % 3
+// admission of the heavy list, slot i % 3: a workgroup per vertex (k_b_adm's workgroups,
+// before their light chunks)
+__device__ void b_adm_heavy(GDev& g, BLists& B, const int* ev, int pass) {
+    DevCtl* c = g.ctl;
+    const int rs = pass % 3, ws = (pass + 1) % 3;
+    const long long cnt = (long long)*b_cnt(c, 1, rs);
+    if (cnt == 0) return;
+    __shared__ unsigned s_flag;
+    __shared__ int s_first;
+    const int* list = B.l[1][rs];
+    for (long long i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int v = list[i];
+        const unsigned kv = g.k8[v];
+        const unsigned c6 = gc_k8_cand(kv);
+        const int cv = b_cand(g, v, kv);
+        const int bc = g.lcur[v];
+        const long long s0 = g.rp[v] + bc, s1 = g.rp[v] + g.deg[v];
+        if (threadIdx.x == 0) {
+            s_flag = 0u;
+            s_first = 0x7FFFFFFF;
+        }
+        __syncthreads();
+        for (long long e0 = s0; e0 < s1; e0 += GC_SLOTS * (long long)blockDim.x) {
+            int u[GC_SLOTS];
+            unsigned ku[GC_SLOTS];
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) {
+                const long long e = e0 + (long long)k * blockDim.x + threadIdx.x;
+                u[k] = e < s1 ? g.col[e] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) ku[k] = u[k] >= 0 ? (unsigned)g.k8[u[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_SLOTS; ++k) {
+                if (u[k] < 0) continue;
+                const unsigned f = b_adm_flag(g, v, u[k], ku[k], c6, cv, ev);
+                if (f) atomicOr(&s_flag, f);
+                if (f == 2u) atomicMin(&s_first, (int)(e0 + (long long)k * blockDim.x + threadIdx.x - s0));
+            }
+            __syncthreads();
+            const bool refused = (s_flag & 1u) != 0;  // refused: the rest cannot change it
+            __syncthreads();
+            if (refused) break;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int kind = -1;
+            b_adm_decide(g, B, c, ws, v, kv, s_flag, s_first, &kind);
+            if (kind >= 0) B.l[kind][ws][atomicAdd(b_cnt(c, kind, ws), 1ull)] = v;
+        }
+        __syncthreads();
+    }
+}
+
+// admission pass, slot i % 3: the heavy list (a workgroup per vertex), then the light list
+// (wave chunks)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int* ev, int pass) {
+    b_adm_heavy(g, B, ev, pass);
     DevCtl* c = g.ctl;
     const int rs = pass % 3, ws = (pass + 1) % 3;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
@@ -319,84 +377,77 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
     gc_stage_flush_block(est, B.l[2][ws], b_cnt(c, 2, ws));
 }
 
-// admission pass over the heavy list, slot i % 3: a workgroup per vertex
-__global__ void __launch_bounds__(GC_BLOCK) k_b_adm_heavy(GDev g, BLists B, const int* ev, int pass) {
-    DevCtl* c = g.ctl;
-    const int rs = pass % 3, ws = (pass + 1) % 3;
-    const long long cnt = (long long)*b_cnt(c, 1, rs);
-    if (cnt == 0) return;
-    __shared__ unsigned s_flag;
-    __shared__ int s_first;
-    const int* list = B.l[1][rs];
-    for (long long i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const int v = list[i];
-        const unsigned kv = g.k8[v];
-        const unsigned c6 = gc_k8_cand(kv);
-        const int cv = b_cand(g, v, kv);
-        const int bc = g.lcur[v];
-        const long long s0 = g.rp[v] + bc, s1 = g.rp[v] + g.deg[v];
-        if (threadIdx.x == 0) {
-            s_flag = 0u;
-            s_first = 0x7FFFFFFF;
-        }
-        __syncthreads();
-        for (long long e0 = s0; e0 < s1; e0 += GC_SLOTS * (long long)blockDim.x) {
-            int u[GC_SLOTS];
-            unsigned ku[GC_SLOTS];
-#pragma unroll
-            for (int k = 0; k < GC_SLOTS; ++k) {
-                const long long e = e0 + (long long)k * blockDim.x + threadIdx.x;
-                u[k] = e < s1 ? g.col[e] : -1;
-            }
-#pragma unroll
-            for (int k = 0; k < GC_SLOTS; ++k) ku[k] = u[k] >= 0 ? (unsigned)g.k8[u[k]] : 0u;
-#pragma unroll
-            for (int k = 0; k < GC_SLOTS; ++k) {
-                if (u[k] < 0) continue;
-                const unsigned f = b_adm_flag(g, v, u[k], ku[k], c6, cv, ev);
-                if (f) atomicOr(&s_flag, f);
-                if (f == 2u) atomicMin(&s_first, (int)(e0 + (long long)k * blockDim.x + threadIdx.x - s0));
-            }
-            __syncthreads();
-            const bool refused = (s_flag & 1u) != 0;  // refused: the rest cannot change it
-            __syncthreads();
-            if (refused) break;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int kind = -1;
-            b_adm_decide(g, B, c, ws, v, kv, s_flag, s_first, &kind);
-            if (kind >= 0) B.l[kind][ws][atomicAdd(b_cnt(c, kind, ws), 1ull)] = v;
-        }
-        __syncthreads();
-    }
-}
 
-// winners: admitted and never evicted, coloured (coloring_optimized.py:129-140)
-__global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev) {
+// winners: admitted and never evicted, coloured (coloring_optimized.py:129-140).  With
+// hubs, a winner's colour goes into the bitmap of every hub listing it: a wave walks its
+// winners' hub lists as one flat range; lists longer than GC_B_PUSH are left to
+// k_b_push_big (a workgroup each) -- one thread per winner walked hub lists of thousands.
+#define GC_B_PUSH 256
+__global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev, int* big) {
     DevCtl* c = g.ctl;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (long long)gridDim.x * blockDim.x) {
-        const int v = list[i];
-        const unsigned kv = g.k8[v];
-        if (gc_k8_state(kv) != GC_JP_IN || ev[v] != GC_B_INF) continue;
-        const int cc = b_cand(g, v, kv);
-        gc_commit_colour(g, v, cc);
-        if (want_cround) g.cround[v] = round;
-        lmaxc = cc > lmaxc ? cc : lmaxc;
-        lacc++;
-        lsum += (ull)g.deg[v];
+    const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long i = sidx * GC_WAVE + lane;
+        const int v = i < cnt ? list[i] : -1;
+        const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;
+        const bool win = v >= 0 && gc_k8_state(kv) == GC_JP_IN && ev[v] == GC_B_INF;
+        int cc = 0, hl = 0;
+        long long hs = 0;
+        if (win) {
+            cc = b_cand(g, v, kv);
+            gc_commit_colour(g, v, cc);
+            if (want_cround) g.cround[v] = round;
+            lmaxc = cc > lmaxc ? cc : lmaxc;
+            lacc++;
+            lsum += (ull)g.deg[v];
+            if (g.hub_w) {
+                hs = g.hin_rp[v];
+                hl = (int)(g.hin_rp[v + 1] - hs);
+            }
+        }
+        if (!g.hub_w) continue;  // wave-uniform
+        const bool far = hl > GC_B_PUSH;
+        gc_wave_append(far, v, big, &c->bigw_cnt);
+        if (far) hl = 0;
+        s_start[w][lane] = hs;
+        s_cc[w][lane] = cc;
+        const int incl = gc_wave_incl_scan(hl);
+        const int excl = incl - hl;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        for (int base = 0; base < total; base += GC_WAVE) {
+            const int e = base + lane;
+            const int o = gc_owner(excl, e);
+            const int eo = __shfl(excl, o, GC_WAVE);
+            if (e < total) gc_hub_mark(g, g.hin_col[s_start[w][o] + (e - eo)], s_cc[w][o]);
+        }
+        gc_wave_sync();
     }
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
     gc_block_add(&c->accepted, lacc, scratch);
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
+}
+
+// the winners with long hub lists (k_b_commit): a workgroup each
+__global__ void __launch_bounds__(GC_BLOCK) k_b_push_big(GDev g, const int* big) {
+    const long long nb = (long long)g.ctl->bigw_cnt;
+    for (long long i = blockIdx.x; i < nb; i += gridDim.x) {
+        const int v = big[i];
+        gc_hub_mark_row(g, v, gc_colour(g, v), threadIdx.x, blockDim.x);  // committed: k8 was reset
+    }
 }
 
 struct RunB {
@@ -453,6 +504,9 @@ static int ensure_bpart(gc_graph* g) {
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out, gc_stats* st) {
     RunB R{g, gc_view(g), gc_lists(g), g->stream};
     int rc;
+    // hubs keep their forbidden colours as pushed bitmaps (every uncoloured vertex proposes
+    // every round: without them k_propose_block re-reads every hub row each round)
+    if ((rc = gc_hubs_prepare(g, R.d))) return rc;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
@@ -484,16 +538,16 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;
     const long long max_rounds = 4ll * g->n + 16;
+    // One host wait per round in the common case: the round's re-sort, proposals and its
+    // first batch of fold passes are enqueued together (as many passes as the previous
+    // round needed); the previous round's winner count comes back in the same snapshot
+    // (k_b_reset keeps it).  A round that ends the colouring (no uncoloured vertex) or
+    // fails (bounded attempt) has only run fold passes, which change no colour.
+    long long prev_passes = 2, prevU = 0, prev_maxmex = -1;
     for (long long r = 0;; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
         hipLaunchKernelGGL(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
         gcl_fsort(d, L, g->fsum, s);
-        if ((rc = R.sync())) return rc;
-        const long long U = (long long)h.fcnt[0];
-        if (U == 0) {  // coloring_optimized.py: no uncoloured vertex left
-            recs.push_back(RoundRec{0, 0, -1, 0, 0, 0});
-            break;
-        }
         gcl_pack_c4(d, s);
         gcl_propose(d, L, s);
         gcl_propose_block(d, L, s);
@@ -501,7 +555,28 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if ((rc = R.zero(&g->ctl->failcnt))) return rc;
             hipLaunchKernelGGL(k_b_fail0, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
         }
+        // the fold's passes over the work lists until no vertex is undecided and every
+        // admitted vertex's eviction time is final
+        hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
+        long long passes = 0;
+        auto enqueue_passes = [&](long long k) {
+            for (long long j = 0; j < k; ++j, ++passes) {
+                const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
+                hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+                hipLaunchKernelGGL(k_b_adm, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
+            }
+        };
+        enqueue_passes(std::max(2ll, std::min(prev_passes, 24ll)));
         if ((rc = R.sync())) return rc;
+        if (r > 0) {
+            recs.push_back(RoundRec{prevU, prevU, prev_maxmex, (long long)h.dcnt, 0, prev_passes});
+            sweeps_total += prev_passes;
+        }
+        const long long U = (long long)h.fcnt[0];
+        if (U == 0) {  // coloring_optimized.py: no uncoloured vertex left
+            recs.push_back(RoundRec{0, 0, -1, 0, 0, 0});
+            break;
+        }
         const long long maxmex = h.maxmex;
         if (h.kbound >= 0 && h.failcnt > 0) {  // state at the round start is returned
             recs.push_back(RoundRec{U, U, maxmex, 0, 0, 0});
@@ -510,26 +585,18 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             fail_count = (long long)h.failcnt;
             break;
         }
-        // the fold's passes over the work lists until no vertex is undecided and every
-        // admitted vertex's eviction time is final
-        hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
-        long long passes = 0;
-        for (int batch = 2;; batch = std::min(batch * 2, 16)) {
-            for (int j = 0; j < batch; ++j, ++passes) {
-                const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
-                hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
-                hipLaunchKernelGGL(k_b_adm, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
-                hipLaunchKernelGGL(k_b_adm_heavy, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
-            }
-            if ((rc = R.sync())) return rc;
+        for (long long batch = 4;; batch = std::min(batch * 2, 16ll)) {
             const int ws = (int)(passes % 3);  // written by the last pass
             if (h.bcnt[ws] + h.bcnt[3 + ws] + h.bcnt[6 + ws] == 0) break;
             if (passes > 2 * g->n + 64) { gc_set_error("variant B passes do not converge"); return GC_EROUNDS; }
+            enqueue_passes(batch);
+            if ((rc = R.sync())) return rc;
         }
-        hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev);
-        if ((rc = R.sync())) return rc;
-        recs.push_back(RoundRec{U, U, maxmex, (long long)h.accepted, 0, passes});
-        sweeps_total += passes;
+        hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
+        if (d.hub_w) hipLaunchKernelGGL(k_b_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, (const int*)g->ulist);
+        prev_passes = passes;
+        prevU = U;
+        prev_maxmex = maxmex;
     }
     gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
     gcl_stat_reduce(d, s);

@@ -121,6 +121,31 @@ def test_heavy_vertices_and_wide_mex_variant_b():
         assert o["max_color"] >= 100
 
 
+@pytest.mark.parametrize("hub_t,hub_w", [("0", "128"), ("64", "1"), ("512", "4"), ("off", "128")])
+def test_variant_b_hub_bitmaps(monkeypatch, hub_t, hub_w):
+    """Variant B proposes through the hubs' pushed forbidden-colour bitmaps: every threshold,
+    a bitmap too small for the colours (row-scan fallback) and hubs off agree with the oracle."""
+    monkeypatch.setenv("GC_HUB_T", hub_t)
+    monkeypatch.setenv("GC_HUB_W", hub_w)
+    with _dg().rmat(13, 16, seed=5) as dg:
+        rp, col = dg.export()
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+    n = 40 + 3000
+    adj = [[] for _ in range(n)]
+    for i in range(40):  # a clique of hubs (colours past a 1-word bitmap), each with leaves
+        adj[i] += [j for j in range(40) if j != i]
+    for leaf in range(40, n):
+        hub = leaf % 40
+        adj[hub].append(leaf)
+        adj[leaf].append(hub)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    with _dg().from_csr(rp, col) as dg:
+        o = oracle.c_color(rp, col, "B")
+        assert_same_run(dg.color("B"), o)
+        assert_same_run(dg.color("B", num_colors=int(o["max_color"])), oracle.c_color(rp, col, "B", k=int(o["max_color"])))
+
+
 def test_mesh_and_edgeless_variant_b():
     DG = _dg()
     with DG.mesh(16, 8, 4) as dg:
