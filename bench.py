@@ -256,6 +256,10 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: colour N independent copies (one per GPU) instead of one sharded graph")
+    ap.add_argument("--priority-seed", type=int, default=None,
+                    help="north_star mode N1: JP rounds ranked by prio_hash(seed, v) instead of (deg, pos)")
+    ap.add_argument("--speculative", action="store_true",
+                    help="north_star mode N1: speculative first-fit rounds with one-shot resolution")
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
@@ -286,6 +290,10 @@ def main():
     _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
     w = WORKLOADS[args.workload]
     V = args.variant
+    # north_star N1 modes (variant A only): seeded priorities / speculative first-fit
+    mode = {"priority": args.priority_seed, "speculative": args.speculative}
+    if V == "B" and (args.priority_seed is not None or args.speculative):
+        raise SystemExit("--priority-seed / --speculative are variant A modes")
     t0 = time.time()
     dg, host_csr = build_graph(w)
     gen_s = time.time() - t0
@@ -301,7 +309,8 @@ def main():
     # (bracketing every launch costs ~30% of the step in inter-kernel gaps)
     probe = None
     for i in range(max(args.warmup, 1)):
-        probe = dg.color(V, kernel_timing=(i == max(args.warmup, 1) - 1), want_rounds=False, want_colors=False)
+        probe = dg.color(V, kernel_timing=(i == max(args.warmup, 1) - 1), want_rounds=False, want_colors=False,
+                         **mode)
     dom_class = max(probe.kernels.items(), key=lambda kv: kv[1]["ms"])[0]
     barrier()
     # Timed region: K full colourings from the resident CSR, no events.  Then the same K
@@ -313,7 +322,7 @@ def main():
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            r = dg.color(V, kernel_timing=timing, want_rounds=False, want_colors=False)
+            r = dg.color(V, kernel_timing=timing, want_rounds=False, want_colors=False, **mode)
             for k, v in r.kernels.items():
                 a = kern.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0.0})
                 a["ms"] += v["ms"]
@@ -337,7 +346,7 @@ def main():
         a["bytes"] /= args.steps
 
     # validity of the colouring (outside the timed region)
-    res = dg.color(V, want_colors=True, want_rounds=False)
+    res = dg.color(V, want_colors=True, want_rounds=False, **mode)
     unc, conf = dg.validate()
     assert unc == 0 and (conf == 0 or not dg.symmetric), f"invalid colouring: {unc} uncoloured, {conf} conflicts"
     pmc, pmc_src = pmc_class_bytes(args.workload, V)
@@ -359,7 +368,7 @@ def main():
             dist.destroy_process_group()
         return
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and V == "A":
+    if world == 1 and not args.no_cpu_baseline and V == "A" and args.priority_seed is None and not args.speculative:
         cpu = cpu_baseline(w, host_csr, dg, res.colors)
         assert cpu.pop("identical"), "GPU colouring differs from the CPU restatement"
         cpu.pop("colors")
@@ -380,6 +389,9 @@ def main():
         "config": {"workload": w["desc"], "n": dg.n, "m_undirected": m, "nnz": dg.nnz,
                    "max_degree": dg.max_degree, "variant": "A (coloring.py)" if V == "A" else
                    "B (coloring_optimized.py)", "parallelism": "replicas" if world > 1 else "single",
+                   "rank": ("(deg, pos) (coloring.py:64)" if args.priority_seed is None
+                            else f"prio_hash(seed={args.priority_seed}, v), pos"),
+                   "resolution": "speculative first-fit, one-shot" if args.speculative else "Jones-Plassmann LFMIS",
                    "rounds": rounds, "jp_extra_sweeps": sweeps, "reseeds": reseeds,
                    "graph_build_s": round(gen_s, 2),
                    "event_timed_class": None if args.no_event_timing else dom_class},
