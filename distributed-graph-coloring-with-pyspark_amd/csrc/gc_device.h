@@ -85,8 +85,8 @@ __device__ __forceinline__ void gc_st(T* p, T v) {
 // hubs (gc_hubs.hip): set colour cc in hub x's forbidden-colour bitmap (colours past the
 // bitmap are not tracked: such a hub scans its row when its mex could lie beyond it)
 __device__ __forceinline__ void gc_hub_mark(const GDev& g, int x, int cc) {
-    if (cc >= 32 * g.hub_w) return;
-    unsigned* p = g.hbits + (long long)x * g.hub_w + (cc >> 5);
+    if (cc >= 32 * g.hbits_w) return;
+    unsigned* p = g.hbits + (long long)x * g.hbits_w + (cc >> 5);
     const unsigned bit = 1u << (cc & 31);
     if (!(*p & bit)) atomicOr(p, bit);
 }
@@ -95,6 +95,38 @@ __device__ __forceinline__ void gc_hub_mark_row(const GDev& g, int v, int cc, in
     const long long e1 = g.hin_rp[v + 1];
     for (long long e = g.hin_rp[v] + t0; e < e1; e += step) gc_hub_mark(g, g.hin_col[e], cc);
 }
+// Pushes of this wave's winners' colours into the hub bitmaps (hbits_w), the wave walking
+// its lanes' hub lists as one flat range; a list longer than GC_PUSH_FLAT is appended to
+// `big` for gcl_hub_push_big (a workgroup each: one thread per winner walked lists of
+// thousands).  All 64 lanes call; s_start / s_cc are this wave's LDS rows.
+#define GC_PUSH_FLAT 256
+__device__ __forceinline__ void gc_hub_push_wave(const GDev& g, bool win, int v, int cc, long long* s_start, int* s_cc,
+                                                 int* big, ull* big_cnt) {
+    const int lane = gc_lane();
+    long long hs = 0;
+    int hl = 0;
+    if (win) {
+        hs = g.hin_rp[v];
+        hl = (int)(g.hin_rp[v + 1] - hs);
+    }
+    const bool far = hl > GC_PUSH_FLAT;
+    gc_wave_append(far, v, big, big_cnt);
+    if (far) hl = 0;
+    s_start[lane] = hs;
+    s_cc[lane] = cc;
+    const int incl = gc_wave_incl_scan(hl);
+    const int excl = incl - hl;
+    const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+    gc_wave_sync();
+    for (int base = 0; base < total; base += GC_WAVE) {
+        const int e = base + lane;
+        const int o = gc_owner(excl, e);
+        const int eo = __shfl(excl, o, GC_WAVE);
+        if (e < total) gc_hub_mark(g, g.hin_col[s_start[o] + (e - eo)], s_cc[o]);
+    }
+    gc_wave_sync();
+}
+
 // heavy entries the one-workgroup tail sweeps may take
 __device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.tail_hmax; }
 

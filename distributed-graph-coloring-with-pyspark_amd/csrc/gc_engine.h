@@ -80,6 +80,8 @@ struct gc_graph {
     bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
     bool own_stream = true;    // false: the caller's stream (gc_shard_set_stream), not destroyed here
     int part_prio = 0;         // rank the rows are partitioned for (gc_set_priority)
+    int hub_prio = 0;          // row partition the hub lists were built under
+    uint64_t hub_seed = 0;
     bool bpart = false;        // low parts also split by degree (variant B: equal-degree entries last, neq counts them)
     int* neq = nullptr;
     uint64_t part_seed = 0;

@@ -69,6 +69,7 @@ GDev gc_view(const gc_graph* g) {
     d.claim_direct = getenv("GC_CLAIM_DIRECT") ? atoi(getenv("GC_CLAIM_DIRECT")) : 0;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
+    d.hbits_w = 0;
     d.hub_long = 0;
     d.tail_hmax = GC_TAIL_HMAX;
     d.hch_rp = nullptr;
@@ -600,8 +601,13 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     if (opt->speculative) return gc_color_speculative(g, opt, colors_out, cround_out, stats);
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
-    // hubs rank above every light vertex only under (deg, pos): seeded ranks use row scans
-    if (opt->priority == GC_PRIORITY_REF && (rc = gc_hubs_prepare(g, run.d))) return rc;
+    // hubs: forbidden-colour bitmaps for their proposals; the hub JP (hubs rank above every
+    // light vertex) only under (deg, pos) -- seeded ranks resolve hubs by row scans
+    if ((rc = gc_hubs_prepare(g, run.d))) return rc;
+    if (opt->priority != GC_PRIORITY_REF) {
+        run.d.hub_w = 0;
+        run.d.tail_hmax = GC_TAIL_HMAX;
+    }
     run.init_loop();
     {
         const char* f = getenv("GC_FUSE");

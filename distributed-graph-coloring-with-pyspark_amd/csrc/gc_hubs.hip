@@ -300,7 +300,9 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     const int T = env_int("GC_HUB_T", GC_HUB_T);
     const int W = std::max(1, env_int("GC_HUB_W", GC_HUB_W));
     if (T < 0 || g->maxdeg <= T || g->borrowed) return GC_OK;
-    if (g->hub_t != T || (g->nhub && g->hub_w != W)) {
+    // (hlow, the lower-rank hubs of each hub, follows the row partition it was built under)
+    const bool stale = g->nhub && (g->hub_prio != g->part_prio || g->hub_seed != g->part_seed);
+    if (g->hub_t != T || (g->nhub && g->hub_w != W) || stale) {
         gc_hubs_free(g);
         int rc = build(g, T, W);
         if (rc) {
@@ -308,10 +310,13 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
             return rc;
         }
     }
+    g->hub_prio = g->part_prio;
+    g->hub_seed = g->part_seed;
     if (g->nhub == 0) return GC_OK;
     GC_HIP(hipMemsetAsync(g->hbits, 0, sizeof(unsigned) * (size_t)g->nhub * g->hub_w, g->stream));
     d.heavy_t = T;
     d.hub_w = g->hub_w;
+    d.hbits_w = g->hub_w;
     d.hid = g->hid;
     d.hub_v = g->hub_v;
     d.hin_rp = g->hin_rp;

@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
     ull lfail = 0, lsum = 0, lnv = 0;
     // Hubs whose bitmap covers every colour in use: a wave each (first zero bit of a
     // <= 4096-bit bitmap), not a workgroup with its barriers.  Heavy == hub while hubs are on.
-    const bool hub_waves = g.hub_w && maxc + 2 <= 32ll * g.hub_w;
+    const bool hub_waves = g.hbits_w && maxc + 2 <= 32ll * g.hbits_w;
     if (hub_waves) {
         const int lane = gc_lane();
         const int w = threadIdx.x / GC_WAVE;
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
              i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
             const int v = L.heavy[i];
             const int x = g.hid[v];
-            const unsigned* hb = g.hbits + (long long)x * g.hub_w;
+            const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
             long long mex = -1;
             for (int t0 = 0; t0 < words && mex < 0; t0 += GC_WAVE) {  // a zero bit lies in range
                 const int t = t0 + lane;
@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
         const int d = g.deg[v];
         const long long start = g.rp[v];
         long long mex = -1;
-        const int x = (g.hub_w && i < na) ? g.hid[v] : -1;
+        const int x = (g.hbits_w && i < na) ? g.hid[v] : -1;
         if (x >= 0) {
             // hub (gc_hubs.hip): forbidden colours pushed by its neighbours' commits; clear
             // its conflict flag for this round
@@ -399,8 +399,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
                 s_first = 0x7FFFFFFF;
             }
             __syncthreads();
-            if (maxc + 2 <= 32ll * g.hub_w) {  // mex <= maxcolor + 1: a zero bit lies in range
-                const unsigned* hb = g.hbits + (long long)x * g.hub_w;
+            if (maxc + 2 <= 32ll * g.hbits_w) {  // mex <= maxcolor + 1: a zero bit lies in range
+                const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
                 for (int t = threadIdx.x; t < words; t += blockDim.x)
                     if (~hb[t]) atomicMin(&s_first, t);
                 __syncthreads();
@@ -1604,7 +1604,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 if (want_cround) g.cround[v] = round;
                 lmaxc = cc > lmaxc ? cc : lmaxc;
                 lacc++;
-                const long long rows = (g.trp[v + 1] - g.trp[v]) + (g.hub_w ? g.hin_rp[v + 1] - g.hin_rp[v] : 0);
+                const long long rows = (g.trp[v + 1] - g.trp[v]) + (g.hbits_w ? g.hin_rp[v + 1] - g.hin_rp[v] : 0);
                 lsum += (ull)(g.trp[v + 1] - g.trp[v]);
                 if (rows > g.bigrow) {  // the whole grid walks it (k_commit_big)
                     L.bigw[atomicAdd(&c->bigw_cnt, 1ull)] = v;
@@ -1615,7 +1615,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         }
         __syncthreads();
         if (w == 0) push(lane == 0 && s_lose, v);  // losers stay
-        if (s_acc && g.hub_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
+        if (s_acc && g.hbits_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
         if (s_acc && (mark || !big)) {
             const long long ts = g.trp[v], te = g.trp[v + 1];
             for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
@@ -1700,7 +1700,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) push(claim[k], x[k]);
         }
-        if (g.hub_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
+        if (g.hbits_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
             int dh = 0;
             if (acc) {
                 tstart = g.hin_rp[v];
@@ -1785,7 +1785,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
         if (t < tn) {
             const int v = L.bigw[j0 + t];
             int hl = 0;
-            if (g.hub_w) {
+            if (g.hbits_w) {
                 s_hs[t] = g.hin_rp[v];
                 hl = (int)(g.hin_rp[v + 1] - s_hs[t]);
                 s_cc[t] = gc_colour(g, v);
@@ -2539,6 +2539,17 @@ void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
 }
 void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
+// the winners gc_hub_push_wave left in `big`: a workgroup each walks its hub list
+__global__ void __launch_bounds__(GC_BLOCK) k_hub_push_big(GDev g, const int* big, const ull* cnt) {
+    const long long nb = (long long)*cnt;
+    for (long long i = blockIdx.x; i < nb; i += gridDim.x) {
+        const int v = big[i];
+        gc_hub_mark_row(g, v, gc_colour(g, v), threadIdx.x, blockDim.x);  // committed: its colour is in c8
+    }
+}
+void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_hub_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, big, cnt);
+}
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big, int fused, DevCtl* snap) {
     hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big, fused, snap);
 }

@@ -33,7 +33,10 @@ struct GDev {
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
     // list, both pushed to it, instead of re-reading its whole row every round / sweep.
     int heavy_t;
-    int hub_w;                // words per hub bitmap (0 = hubs off)
+    int hub_w;                // words per hub bitmap (0 = hubs off); > 0 also turns on the hub JP
+    int hbits_w;              // words per hub forbidden-colour bitmap for the proposals and the
+                              //   commits' pushes (0 = none): == hub_w, or alone (seeded ranks,
+                              //   speculative rounds, variant B, whose resolution has no hub JP)
     int tail_hmax;            // heavy entries the one-workgroup tail sweeps may take (GC_TAIL_HMAX[_HUB])
     long long hub_long;       // hub-start sweep: hubs whose hlow row exceeds this are first-read by the whole grid
     const long long* hch_rp;  // static GC_HCH-entry chunks of the hlow rows (hub x: [hch_rp[x], hch_rp[x+1]))
@@ -94,6 +97,7 @@ void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream
                 int fused = 0, DevCtl* snap = nullptr, int tclose = 0);
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0, int fused = 0,
                DevCtl* snap = nullptr);
+void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s);  // see gc_hub_push_wave
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                int* rwin, hipStream_t s);

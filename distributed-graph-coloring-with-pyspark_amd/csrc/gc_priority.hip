@@ -62,6 +62,7 @@ __global__ void k_spec_reset(GDev g, long long round) {
     c->failcnt = 0;
     c->maxmex = -1;
     c->accepted = 0;
+    c->bigw_cnt = 0;
     c->fsort_all = 1;
 }
 
@@ -110,25 +111,36 @@ __global__ void __launch_bounds__(GC_BLOCK) k_spec_resolve(GDev g, GLists L) {
 }
 
 // winners take their candidate (coloring.py:117-127)
-__global__ void __launch_bounds__(GC_BLOCK) k_spec_commit(GDev g, GLists L) {
+__global__ void __launch_bounds__(GC_BLOCK) k_spec_commit(GDev g, GLists L, int* big) {
     DevCtl* c = g.ctl;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int w = threadIdx.x / GC_WAVE;
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (long long)gridDim.x * blockDim.x) {
-        const int v = list[i];
-        const unsigned kv = g.k8[v];
-        if (gc_k8_state(kv) != GC_JP_IN) continue;
-        const int cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
-        gc_commit_colour(g, v, cc);
-        if (want_cround) g.cround[v] = round;
-        lmaxc = cc > lmaxc ? cc : lmaxc;
-        lacc++;
-        lsum += (ull)g.deg[v];
+    const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long i = sidx * GC_WAVE + gc_lane();
+        const int v = i < cnt ? list[i] : -1;
+        const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;
+        const bool win = v >= 0 && gc_k8_state(kv) == GC_JP_IN;
+        int cc = 0;
+        if (win) {
+            cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+            gc_commit_colour(g, v, cc);
+            if (want_cround) g.cround[v] = round;
+            lmaxc = cc > lmaxc ? cc : lmaxc;
+            lacc++;
+            lsum += (ull)g.deg[v];
+        }
+        // hub bitmaps (gc_hubs.hip): the winner's colour into every hub listing it
+        if (g.hbits_w) gc_hub_push_wave(g, win, v, cc, s_start[w], s_cc[w], big, &c->bigw_cnt);
     }
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
@@ -182,8 +194,15 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
 // Speculative first-fit rounds (gc_options.speculative = 1) under the current rank.
 int gc_color_speculative(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out, gc_stats* st) {
     const hipStream_t s = g->stream;
-    const GDev d = gc_view(g);
+    GDev d = gc_view(g);
     const GLists L = gc_lists(g);
+    // every uncoloured vertex proposes every round: hubs propose from pushed forbidden-colour
+    // bitmaps (gc_hubs.hip) instead of re-reading their rows; the one-shot resolution needs
+    // no hub JP
+    int rc0 = gc_hubs_prepare(g, d);
+    if (rc0) return rc0;
+    d.hub_w = 0;
+    d.tail_hmax = GC_TAIL_HMAX;
     DevCtl& h = *g->hctl;
     memset(&h, 0, sizeof(DevCtl));
     h.kbound = opt->num_colors;
@@ -228,7 +247,8 @@ int gc_color_speculative(gc_graph* g, const gc_options* opt, int32_t* colors_out
             break;
         }
         hipLaunchKernelGGL(k_spec_resolve, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
-        hipLaunchKernelGGL(k_spec_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
+        hipLaunchKernelGGL(k_spec_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, g->ulist);
+        if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         if ((rc = sync_ctl(g))) return rc;
         recs.push_back(RoundRec{U, U, maxmex, (long long)h.accepted, 0, 1});
     }

@@ -378,11 +378,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
 }
 
 
-// winners: admitted and never evicted, coloured (coloring_optimized.py:129-140).  With
-// hubs, a winner's colour goes into the bitmap of every hub listing it: a wave walks its
-// winners' hub lists as one flat range; lists longer than GC_B_PUSH are left to
-// k_b_push_big (a workgroup each) -- one thread per winner walked hub lists of thousands.
-#define GC_B_PUSH 256
+// winners: admitted and never evicted, coloured (coloring_optimized.py:129-140); with hub
+// bitmaps, pushed into the hubs listing them (gc_hub_push_wave)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev, int* big) {
     DevCtl* c = g.ctl;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
@@ -403,8 +400,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
         const int v = i < cnt ? list[i] : -1;
         const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;
         const bool win = v >= 0 && gc_k8_state(kv) == GC_JP_IN && ev[v] == GC_B_INF;
-        int cc = 0, hl = 0;
-        long long hs = 0;
+        int cc = 0;
         if (win) {
             cc = b_cand(g, v, kv);
             gc_commit_colour(g, v, cc);
@@ -412,28 +408,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
             lmaxc = cc > lmaxc ? cc : lmaxc;
             lacc++;
             lsum += (ull)g.deg[v];
-            if (g.hub_w) {
-                hs = g.hin_rp[v];
-                hl = (int)(g.hin_rp[v + 1] - hs);
-            }
         }
-        if (!g.hub_w) continue;  // wave-uniform
-        const bool far = hl > GC_B_PUSH;
-        gc_wave_append(far, v, big, &c->bigw_cnt);
-        if (far) hl = 0;
-        s_start[w][lane] = hs;
-        s_cc[w][lane] = cc;
-        const int incl = gc_wave_incl_scan(hl);
-        const int excl = incl - hl;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) gc_hub_mark(g, g.hin_col[s_start[w][o] + (e - eo)], s_cc[w][o]);
-        }
-        gc_wave_sync();
+        if (g.hbits_w) gc_hub_push_wave(g, win, v, cc, s_start[w], s_cc[w], big, &c->bigw_cnt);  // wave-uniform
     }
     __syncthreads();
     gc_block_max(&c->maxcolor, lmaxc, (long long*)scratch);
@@ -441,14 +417,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
-// the winners with long hub lists (k_b_commit): a workgroup each
-__global__ void __launch_bounds__(GC_BLOCK) k_b_push_big(GDev g, const int* big) {
-    const long long nb = (long long)g.ctl->bigw_cnt;
-    for (long long i = blockIdx.x; i < nb; i += gridDim.x) {
-        const int v = big[i];
-        gc_hub_mark_row(g, v, gc_colour(g, v), threadIdx.x, blockDim.x);  // committed: k8 was reset
-    }
-}
 
 struct RunB {
     gc_graph* g;
@@ -507,6 +475,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // hubs keep their forbidden colours as pushed bitmaps (every uncoloured vertex proposes
     // every round: without them k_propose_block re-reads every hub row each round)
     if ((rc = gc_hubs_prepare(g, R.d))) return rc;
+    R.d.hub_w = 0;  // bitmaps only: the fold has no hub JP
+    R.d.tail_hmax = GC_TAIL_HMAX;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
@@ -593,7 +563,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if ((rc = R.sync())) return rc;
         }
         hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
-        if (d.hub_w) hipLaunchKernelGGL(k_b_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, (const int*)g->ulist);
+        if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         prev_passes = passes;
         prevU = U;
         prev_maxmex = maxmex;

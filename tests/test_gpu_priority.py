@@ -92,3 +92,29 @@ def test_colour_counts_against_reference():
                 g = dg.color("A", priority=seed, speculative=spec)
                 assert g.ok and dg.validate() == (0, 0)
                 assert g.max_color + 1 <= ref + 2
+
+
+@pytest.mark.parametrize("hub_t,hub_w", [("0", "128"), ("64", "1"), ("off", "128")])
+@pytest.mark.parametrize("mode", MODES[:3], ids=MIDS[:3])
+def test_modes_with_hub_bitmaps(monkeypatch, hub_t, hub_w, mode):
+    """Seeded and speculative rounds propose hubs from pushed forbidden-colour bitmaps (no
+    hub JP): every threshold, a one-word bitmap (row-scan fallback past 32 colours) and
+    hubs off agree with the oracle; the reference path after them too (hub lists rebuilt
+    for the (deg, pos) partition)."""
+    monkeypatch.setenv("GC_HUB_T", hub_t)
+    monkeypatch.setenv("GC_HUB_W", hub_w)
+    with _dg().rmat(12, 16, seed=7) as dg:
+        rp, col = dg.export()
+        _check(dg, rp, col, *mode, bounded=False)
+        assert_same_run(dg.color("A"), oracle.c_color(*dg.export(), "A"))
+    n = 40 + 3000
+    adj = [[] for _ in range(n)]
+    for i in range(40):  # a clique of hubs (colours past a 1-word bitmap), each with leaves
+        adj[i] += [j for j in range(40) if j != i]
+    for leaf in range(40, n):
+        adj[leaf % 40].append(leaf)
+        adj[leaf].append(leaf % 40)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    with _dg().from_csr(rp, col) as dg:
+        _check(dg, rp, col, *mode)
