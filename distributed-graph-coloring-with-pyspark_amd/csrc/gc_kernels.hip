@@ -2486,6 +2486,10 @@ static int round_grid(const char* env, int dflt) {
 static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
 static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
+// the later JP sweeps: mostly short lists, where 1024 workgroups' start-up and end-of-kernel
+// reductions outweigh their reach (R-MAT-24 257 -> 238 ms, R-MAT-26 562 -> 521 ms at 384;
+// 256 within 1%; C2 and the mesh unchanged)
+static const int kGridS = round_grid("GC_GRID_S", 384);
 
 // per-slot stats -> DevCtl.sumdeg / nvert (one workgroup; before the host reads them)
 __global__ void k_stat_reduce(GDev g) {
@@ -2514,7 +2518,7 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_resolve, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L, i);
+    hipLaunchKernelGGL(k_sweep, dim3(kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
 }
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
