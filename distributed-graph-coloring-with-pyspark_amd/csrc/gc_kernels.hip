@@ -2486,6 +2486,8 @@ static int round_grid(const char* env, int dflt) {
 static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
 static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
+static const int kGridPB = round_grid("GC_GRID_PB", GC_BLOCK_GRID);  // k_propose_block
+static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit_big
 // the later JP sweeps: mostly short lists, where 1024 workgroups' start-up and end-of-kernel
 // reductions outweigh their reach (R-MAT-24 257 -> 238 ms, R-MAT-26 562 -> 521 ms at 384;
 // 256 within 1%; C2 and the mesh unchanged)
@@ -2512,7 +2514,7 @@ void gcl_propose(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose, dim3(kGridP), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose_block, dim3(GC_BLOCK_GRID), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
+    hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_resolve, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L);
@@ -2578,7 +2580,7 @@ void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream
     }
     hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        hipLaunchKernelGGL(k_commit_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
+        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
