@@ -84,6 +84,8 @@ struct gc_graph {
     uint64_t hub_seed = 0;
     bool bpart = false;        // low parts also split by degree (variant B: equal-degree entries last, neq counts them)
     int* neq = nullptr;
+    int* hpl = nullptr;        // hubs-off heavy JP pending lists (gc_alloc_heavy_pending), nnz + n ints
+    int* hplc = nullptr;
     uint64_t part_seed = 0;
 };
 
@@ -101,7 +103,8 @@ void gc_set_error(const char* fmt, ...);
 int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
-int gc_hubs_prepare(gc_graph* g, GDev& d);  // gc_hubs.hip: build (once) + reset; fills d's hub fields
+int gc_hubs_prepare(gc_graph* g, GDev& d);
+int gc_alloc_heavy_pending(gc_graph* g);  // gc_engine.hip: the hubs-off heavy JP's pending lists, on first use  // gc_hubs.hip: build (once) + reset; fills d's hub fields
 void gc_hubs_free(gc_graph* g);
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
                        gc_stats* st);  // gc_variant_b.hip

@@ -67,6 +67,8 @@ GDev gc_view(const gc_graph* g) {
     d.bigrow = getenv("GC_BIGROW") ? atoi(getenv("GC_BIGROW")) : GC_BIGROW;  // env: tests / tuning
     d.big_rows = !((g->flags & GC_GRAPH_SYMMETRIC) && 2 * g->maxdeg <= d.bigrow);
     d.claim_direct = getenv("GC_CLAIM_DIRECT") ? atoi(getenv("GC_CLAIM_DIRECT")) : 0;
+    d.hpl = g->hpl;
+    d.hplc = g->hplc;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hbits_w = 0;
@@ -126,6 +128,17 @@ static int dalloc(T** p, size_t count) {
 }
 
 static const long long kRoundCap = 4096;
+
+// The hubs-off heavy JP (a workgroup per heavy vertex, gc_jp_sweep) keeps, per round, the
+// entries of a heavy vertex's lower-rank part that can still block it (same candidate,
+// undecided) at hpl[rp[v] ..]: its later sweeps read those instead of the whole part
+// (R-MAT hubs: ~10^5 entries).  Only seeded ranks, shards and hubs-off runs take that path.
+int gc_alloc_heavy_pending(gc_graph* g) {
+    if (g->hpl) return GC_OK;
+    int st = dalloc(&g->hpl, (size_t)std::max<long long>(g->nnz, 1));
+    if (st == GC_OK) st = dalloc(&g->hplc, (size_t)std::max<long long>(g->n, 1));
+    return st;
+}
 
 int gc_alloc_run_state(gc_graph* g) {
     if (g->has_run_state) return GC_OK;
@@ -607,6 +620,11 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     if (opt->priority != GC_PRIORITY_REF) {
         run.d.hub_w = 0;
         run.d.tail_hmax = GC_TAIL_HMAX;
+    }
+    if (run.d.hub_w == 0 && g->maxdeg > run.d.heavy_t) {
+        if ((rc = gc_alloc_heavy_pending(g))) return rc;
+        run.d.hpl = g->hpl;
+        run.d.hplc = g->hplc;
     }
     run.init_loop();
     {

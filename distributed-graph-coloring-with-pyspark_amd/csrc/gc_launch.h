@@ -28,6 +28,8 @@ struct GDev {
     int big_rows;         // some in-row (+ hub row) may exceed bigrow: k_commit_big is needed
     int bigrow;           // heavy winners with longer in-rows (+ hub rows) go to k_commit_big (GC_BIGROW)
     int claim_direct;     // fused commit: claim with one atomic, no check-load first (GC_CLAIM_DIRECT)
+    int* hpl;             // hubs-off heavy JP (gc_jp_sweep): heavy v's pending entries at hpl[rp[v] ..], or null
+    int* hplc;            //   and their count (written by each sweep of v)
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
     // workgroup-per-vertex path; with hubs on (hub_w > 0) every such vertex is a hub that
     // keeps its forbidden colours as a bitmap and its per-round conflict candidates as a
@@ -101,8 +103,9 @@ void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                int* rwin, hipStream_t s);
-void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, hipStream_t s);
-void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, hipStream_t s);
+// big: winners whose hub lists are left to gcl_hub_push_big (counter DevCtl.list_cnt)
+void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, int* big, hipStream_t s);
+void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, int* big, hipStream_t s);
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
 void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, long long* send, long long cap,
                     hipStream_t s);

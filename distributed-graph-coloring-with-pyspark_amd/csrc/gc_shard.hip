@@ -28,7 +28,30 @@
 struct gc_shard {
     gc_graph v;  // borrowed CSR + own in-neighbour CSR + own run state
     long long lo = 0, hi = 0;
+    // Hub forbidden-colour bitmaps (gc_hubs.hip) for the proposals of the heavy vertices:
+    // the hub lists (hid, hin) are the parent graph's, built once at gc_shard_create; the
+    // bitmaps are this rank's replica, kept current by pushes from every winner, the rank's
+    // own (k_commit) and the others' (k_shard_list_commit / k_shard_scan_commit).  The
+    // resolution stays the row-scan JP (no hub JP in shards).
+    gc_graph* parent = nullptr;
+    unsigned* hbits = nullptr;
+    int hub_w = 0;
+    long long nhub = 0;
 };
+
+// the shard's kernel arguments: its own view plus the parent's hub lists and its bitmaps
+static GDev shard_view(gc_shard* sh) {
+    GDev d = gc_view(&sh->v);
+    const gc_graph* p = sh->parent;
+    if (sh->hbits && p && p->nhub == sh->nhub && p->hub_w == sh->hub_w) {
+        d.hbits_w = sh->hub_w;
+        d.hbits = sh->hbits;
+        d.hid = p->hid;
+        d.hin_rp = p->hin_rp;
+        d.hin_col = p->hin_col;
+    }
+    return d;
+}
 
 static int shard_sync(gc_shard* sh) {
     gc_graph* g = &sh->v;
@@ -76,7 +99,23 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     }
     int rc = gc_build_in_csr(&v, lo, hi);
     if (!rc) rc = gc_alloc_run_state(&v);
+    if (!rc && g->maxdeg > GC_HEAVY_T) rc = gc_alloc_heavy_pending(&v);  // shards resolve heavy vertices by row scans
+    if (!rc) {  // hub lists on the parent (once), a bitmap replica for this shard
+        GDev pd = gc_view(g);
+        rc = gc_hubs_prepare(g, pd);
+        if (!rc && g->nhub > 0 && v.maxdeg > GC_HEAVY_T) {  // heavy proposers (deg > GC_HEAVY_T) are hubs
+            sh->parent = g;
+            sh->hub_w = g->hub_w;
+            sh->nhub = g->nhub;
+            if (hipMalloc((void**)&sh->hbits, sizeof(unsigned) * (size_t)g->nhub * (size_t)g->hub_w) != hipSuccess) {
+                sh->hbits = nullptr;
+                gc_set_error("hipMalloc of the shard's hub bitmaps failed");
+                rc = GC_ENOMEM;
+            }
+        }
+    }
     if (rc) {
+        if (sh->hbits) hipFree(sh->hbits);
         std::string keep = gc_last_error();
         gc_free_all(&v);
         delete sh;
@@ -90,6 +129,7 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
 extern "C" void gc_shard_destroy(gc_shard* sh) {
     if (!sh) return;
     gc_free_all(&sh->v);
+    if (sh->hbits) hipFree(sh->hbits);
     delete sh;
 }
 
@@ -109,7 +149,9 @@ extern "C" int gc_shard_begin(gc_shard* sh, int64_t num_colors, int32_t track_ro
     h.fail_round = -1;
     h.want_cround = track_rounds ? 1 : 0;
     GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, g->stream));
-    const GDev d = gc_view(g);
+    if (sh->hbits)
+        GC_HIP(hipMemsetAsync(sh->hbits, 0, sizeof(unsigned) * (size_t)sh->nhub * (size_t)sh->hub_w, g->stream));
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
     gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), g->stream);
     gcl_seed_prep(d, g->seeds[0], g->seeds[1], g->stream);
@@ -128,7 +170,7 @@ extern "C" int gc_shard_propose(gc_shard* sh, int64_t round, int64_t* delta, int
     gc_graph* g = &sh->v;
     if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, delta);
     gcl_shard_reset(d, round, g->stream);
     gcl_fsort(d, L, g->fsum, g->stream);  // big rounds: the rank's frontier in vertex order
@@ -167,7 +209,7 @@ extern "C" int gc_shard_propose_async(gc_shard* sh, int64_t round, int64_t* delt
     gc_graph* g = &sh->v;
     if (cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, delta);
     gcl_shard_reset(d, round, g->stream);
     gcl_fsort(d, L, g->fsum, g->stream);
@@ -184,7 +226,7 @@ extern "C" int gc_shard_sweep_async(gc_shard* sh, int32_t i, int32_t count, int6
     gc_graph* g = &sh->v;
     if (delta && cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, delta);
     GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
     for (int j = i; j < i + count; ++j) {
@@ -204,7 +246,7 @@ extern "C" int gc_shard_pack(gc_shard* sh, int32_t kind, int32_t slot, const int
     if (!sh || !send || cap < 0 || slot < 0 || slot > 2) { gc_set_error("bad argument"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
-    gcl_shard_pack(gc_view(g), kind, slot, reinterpret_cast<const long long*>(delta),
+    gcl_shard_pack(shard_view(sh), kind, slot, reinterpret_cast<const long long*>(delta),
                    reinterpret_cast<long long*>(send), delta ? cap : 0, g->stream);
     GC_HIP(hipGetLastError());
     return GC_OK;
@@ -218,7 +260,7 @@ extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, i
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
     if (count > 0 && !recv) { gc_set_error("null delta buffer"); return GC_EINVAL; }
-    gcl_apply(gc_view(g), kind, reinterpret_cast<const long long*>(recv), count, sh->lo, sh->hi, (int)round + 1,
+    gcl_apply(shard_view(sh), kind, reinterpret_cast<const long long*>(recv), count, sh->lo, sh->hi, (int)round + 1,
               kind == GC_KIND_STATE ? g->parent : nullptr, g->stream);
     GC_HIP(hipGetLastError());
     return GC_OK;
@@ -234,7 +276,7 @@ extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int32_t count, int64_t* d
     gc_graph* g = &sh->v;
     if (delta && cap < sh->hi - sh->lo) { gc_set_error("delta capacity %lld < owned range", (long long)cap); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, delta);
     GC_HIP(hipMemsetAsync(&g->ctl->dcnt, 0, sizeof(ull), g->stream));
     for (int j = i; j < i + count; ++j) {
@@ -287,11 +329,12 @@ extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int32_t from_deltas,
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
     gcl_commit(d, L, GC_CM_SHARD, 0, g->stream);
-    if (from_deltas) gcl_shard_list_commit(d, L, g->parent, g->stream);
-    else gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->stream);
+    if (from_deltas) gcl_shard_list_commit(d, L, g->parent, g->ulist, g->stream);
+    else gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->ulist, g->stream);
+    if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->list_cnt, g->stream);  // the other ranks' winners
     gcl_shard_flip(d, g->stream);
     int rc = shard_sync(sh);
     if (rc) return rc;
@@ -307,7 +350,7 @@ extern "C" int gc_shard_reseed(gc_shard* sh, int64_t round, int64_t* nseeds, int
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
-    const GDev d = gc_view(g);
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
     gcl_shard_reset(d, round, g->stream);
     gcl_unc_compact(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, gc_grid_for_waves(g->n), g->stream);
@@ -330,7 +373,7 @@ extern "C" int gc_shard_colors(gc_shard* sh, int32_t* colors_out, int32_t* croun
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
-    gcl_finalize(gc_view(g), gc_grid_for_waves(g->n, 8192), g->stream);
+    gcl_finalize(shard_view(sh), gc_grid_for_waves(g->n, 8192), g->stream);
     if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, g->stream));
     if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, g->stream));
     return shard_sync(sh);

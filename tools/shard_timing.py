@@ -4,9 +4,10 @@ the seam exchanges and per-phase host syncs cost next to the single-GPU engine.
 
   python tools/shard_timing.py WORKLOAD [parts...]     WORKLOAD: rmat24 | mesh256 | uniform10M | rmat20
 
-Shard views run the row-scan engine (no hubs: their pushed state is not exchanged), so
-the single-GPU reference for the seam overhead is the engine with GC_HUB_T=off; the hub
-engine's time is printed beside it.  The P shards share one device and one stream, so
+Shard views resolve hubs by row scans (no hub JP: its pushed state is not exchanged) but
+propose them from hub bitmaps, so the engine with GC_HUB_T=off (no bitmaps either) is only
+an approximate single-GPU reference for the seam overhead; the hub engine's time is
+printed beside it.  The P shards share one device and one stream, so
 their kernels run one after another: the P-shard time is the sum of the shards' kernels
 plus the seams, and `seams` below is that time minus the P-way split of the engine's
 kernels (an estimate of what the exchange protocol costs per colouring)."""
