@@ -45,7 +45,9 @@ typedef unsigned long long ull;
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
 #define GC_ROUND_GRID 1024
+#ifndef GC_TAIL_MAX
 #define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
+#endif
 #define GC_LOOP_MAX 65536 // ... and over at most this many light vertices in k_sweep_loop
 #define GC_LOOP_HMAX 16384 //   (hubs)
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones

@@ -69,3 +69,44 @@ def test_mesh_like_rounds():
     o = oracle.c_color(rp, col, "A")
     with _dg().from_csr(rp, col) as dg:
         assert_same_run(dg.color("A"), o)
+
+
+PIPE_SETTINGS = [
+    {"GC_FUSE": "0"},                               # a k_propose launch every round
+    {"GC_TICKET_CLOSE": "0"},                       # a k_close launch every round
+    {"GC_FUSE": "0", "GC_TICKET_CLOSE": "0"},
+    {"GC_SNAP_COPY": "1"},                          # copy-engine snapshot of the control block
+    {"GC_CLAIM_DIRECT": "1"},                       # fused commit claims with one atomic
+    {"GC_BATCH_MAX": "1"},                          # a host wait after every round
+]
+
+
+@pytest.mark.parametrize("env", PIPE_SETTINGS, ids=["nofuse", "noticket", "nofuse_noticket", "snapcopy",
+                                                     "claimdirect", "batch1"])
+def test_pipeline_settings(monkeypatch, env):
+    """The fused commit (next round's proposals made by the commit), the commit that closes
+    its round, the pinned snapshot and their switched-off forms all match the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from gcolor_amd.generators import reference_csr
+    graphs = [_path_then_dense(120, 400, 10, 1), reference_csr(10000, 8, random.Random(3))]
+    w = 30
+    adj = [[] for _ in range(w * w)]
+    for y in range(w):
+        for x in range(w):
+            v = y * w + x
+            if x + 1 < w:
+                adj[v].append(v + 1)
+                adj[v + 1].append(v)
+            if y + 1 < w:
+                adj[v].append(v + w)
+                adj[v + w].append(v)
+    from gcolor_amd.graphio import csr_from_adjacency
+    graphs.append(csr_from_adjacency(adj))
+    for rp, col in graphs:
+        o = oracle.c_color(rp, col, "A")
+        with _dg().from_csr(rp, col) as dg:
+            assert_same_run(dg.color("A"), o)
+            top = int(o["max_color"])
+            for k in sorted({1, max(1, top)}):
+                assert_same_run(dg.color("A", num_colors=k), oracle.c_color(rp, col, "A", k=k))
