@@ -85,6 +85,7 @@ __device__ __forceinline__ void gc_st(T* p, T v) {
 // hubs (gc_hubs.hip): set colour cc in hub x's forbidden-colour bitmap (colours past the
 // bitmap are not tracked: such a hub scans its row when its mex could lie beyond it)
 __device__ __forceinline__ void gc_hub_mark(const GDev& g, int x, int cc) {
+    if (g.hseen && !g.hseen[x]) g.hseen[x] = 1;  // shards: the hub now belongs to a frontier
     if (cc >= 32 * g.hbits_w) return;
     unsigned* p = g.hbits + (long long)x * g.hbits_w + (cc >> 5);
     const unsigned bit = 1u << (cc & 31);
@@ -139,7 +140,7 @@ __device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.tail
 __device__ __forceinline__ bool gc_hub_gate(const GDev& g, const DevCtl* c, long long i, long long cl,
                                             const int*& hl, long long& ch, const GLists& L) {
     if (!g.hub_w || __hip_atomic_load(const_cast<long long*>(&c->hub_start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i) return false;
-    if (cl == 0) {
+    if (cl == 0 && !c->lights_hold) {  // shards: every rank's lights (gc_shard_release_hubs)
         hl = L.heavy;
         ch = (long long)c->heavy_cnt;
         return true;

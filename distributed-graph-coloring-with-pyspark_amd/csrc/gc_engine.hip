@@ -69,6 +69,11 @@ GDev gc_view(const gc_graph* g) {
     d.claim_direct = getenv("GC_CLAIM_DIRECT") ? atoi(getenv("GC_CLAIM_DIRECT")) : 0;
     d.hpl = g->hpl;
     d.hplc = g->hplc;
+    d.hub_repl = 0;
+    d.own_lo = 0;
+    d.own_hi = g->n;
+    d.hseen = nullptr;
+    d.nhub_repl = 0;
     d.heavy_t = GC_HEAVY_T;
     d.hub_w = 0;
     d.hbits_w = 0;

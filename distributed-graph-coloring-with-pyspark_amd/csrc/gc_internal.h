@@ -145,7 +145,9 @@ struct DevCtl {
     long long hub_start;    // hubs on: the sweep of this round that started the hubs' JP (the lights had converged)
     long long nx_maxmex;    // fused commit: next round's max candidate (k_close moves both into place)
     ull bcnt[9];            // variant B work lists: kind (0 light admission, 1 heavy admission, 2 eviction) x 3 rotating slots
-    ull pad4;
+    ull xhub_cnt;           // shards with replicated hubs: frontier hubs this rank does not own (not counted in F)
+    int lights_hold;        // shards: the hub JP waits for every rank's lights (cleared by gc_shard_release_hubs)
+    int pad4;
     int proposed;           // the current round's proposals were made by the last (fused) commit
     int pad3;
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)

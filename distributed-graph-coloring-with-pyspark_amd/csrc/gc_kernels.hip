@@ -49,7 +49,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_init(GDev g, int* seed_light) {
         const bool valid = v < g.n;
         const int d = valid ? g.deg[v] : 0;
         const bool iso = valid && d == 0;
-        const bool push0 = iso && g.trp[v + 1] > g.trp[v];
+        // (replicated hubs, gc_shard.hip: also when a hub lists it, so every rank marks that hub)
+        const bool push0 = iso && (g.trp[v + 1] > g.trp[v] || (g.hub_repl && g.hin_rp[v + 1] > g.hin_rp[v]));
         if (valid) {
             g.color[v] = iso ? 0 : -1;
             g.cround[v] = iso ? 0 : -1;
@@ -286,6 +287,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool isheavy = d > g.heavy_t;
         gc_wave_append(isheavy, v, L.heavy, &c->heavy_cnt);
+        if (g.hub_repl) {  // replicated hubs of other ranks: in this rank's lists, not in its F
+            const ull xm = __ballot(isheavy && (v < g.own_lo || v >= g.own_hi));
+            if (xm && gc_lane() == 0) atomicAdd(&c->xhub_cnt, (ull)__popcll(xm));
+        }
         const int de = isheavy ? 0 : d;
         s_mask[w][lane] = 0;
         s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
@@ -378,7 +383,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
                 }
                 gc_set_cand(g, v, mex);
                 lmax = mex > lmax ? mex : lmax;
-                if (kbound >= 0 && mex >= kbound) lfail++;
+                if (kbound >= 0 && mex >= kbound && (!g.hub_repl || (v >= g.own_lo && v < g.own_hi))) lfail++;
                 lsum += (ull)g.deg[v];
                 lnv++;
             }
@@ -433,7 +438,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
                 g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);
             }
             lmax = mex > lmax ? mex : lmax;
-            if (kbound >= 0 && mex >= kbound) lfail++;
+            if (kbound >= 0 && mex >= kbound && (!g.hub_repl || (v >= g.own_lo && v < g.own_hi))) lfail++;
             lsum += (ull)d;
             lnv++;
         }
@@ -872,6 +877,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     // heavy vertices first.  Hubs off: a workgroup each, undecided ones staged by wave 0
     __shared__ int s_hstage[GC_STAGE_CAP];
     GcStage hst{s_hstage, 0};
+    long long* const hdout = g.hub_repl ? nullptr : dout;  // replicated hubs (shards) are never sent
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
         // a wave's hubs are i = wid + j * waves; lane l loads the state of hub j0 + l, so a
         // hub's evaluation starts at its row read
@@ -901,7 +907,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             const long long left = (hcnt - i0 + waves - 1) / waves;
             const int nj = left < GC_WAVE ? (int)left : GC_WAVE;
             if (g.hub_scan) {
-                gc_hub_scan_groups(g, nj, pv, pkv, pcv, px, pkill, pp, st, ho, ho_cnt, lsum, lnv, dout, dcnt);
+                gc_hub_scan_groups(g, nj, pv, pkv, pcv, px, pkill, pp, st, ho, ho_cnt, lsum, lnv, hdout, dcnt);
                 continue;
             }
             for (int j = 0; j < nj; ++j) {
@@ -946,8 +952,8 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                     else if (!(f & 2u)) gc_set_state(g, v, kv, GC_JP_IN);
                     if (x >= 0 && ((f & 1u) || !(f & 2u)))  // hub mirror
                         g.hk[x] = gc_hk((unsigned)cv, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
-                    if (dout && ((f & 1u) || !(f & 2u)))
-                        dout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
+                    if (hdout && ((f & 1u) || !(f & 2u)))
+                        hdout[atomicAdd(dcnt, 1ull)] = gc_delta(v, (f & 1u) ? GC_JP_OUT : GC_JP_IN);
                     lsum += (ull)g.deg[v];
                     lnv++;
                 }
@@ -1951,6 +1957,19 @@ __global__ void __launch_bounds__(GC_BLOCK) k_delta_cand(GDev g, GLists L) {
     const int cur = c->cur;
     const long long cnt = (long long)c->fcnt[cur];
     const int* list = L.F[cur];
+    if (g.hub_repl) {  // every rank proposes every hub itself: the lights' deltas, compacted
+        const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
+        for (long long sidx = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE; sidx < steps;
+             sidx += (long long)gridDim.x * (blockDim.x / GC_WAVE)) {
+            const long long i = sidx * GC_WAVE + gc_lane();
+            const int v = i < cnt ? list[i] : -1;
+            const bool send = v >= 0 && g.hid[v] < 0;
+            const unsigned k = send ? g.k8[v] : 0u;
+            const long long dv = send ? gc_delta(v, gc_k8_cand(k) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(k)) : 0ll;
+            gc_wave_append64(send, dv, L.delta, const_cast<ull*>(&c->dcnt));
+        }
+        return;
+    }
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (long long)gridDim.x * blockDim.x) {
         const int v = list[i];
         const unsigned k = g.k8[v];
@@ -1978,7 +1997,17 @@ __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long
                 if (c6 == GC_K8_BIG) g.cand[v] = val;
                 g.k8[v] = gc_k8(c6, GC_JP_UND);
             } else if (kind == GC_KIND_STATE) {
-                g.k8[v] = (unsigned char)((g.k8[v] & ~3u) | (unsigned)val);
+                const unsigned kv = g.k8[v];
+                g.k8[v] = (unsigned char)((kv & ~3u) | (unsigned)val);
+                if (g.hub_repl && g.hub_w && val == GC_JP_IN && g.hid[v] < 0) {
+                    // another rank's light winner flags the hubs that list it and propose its
+                    // colour, as a local one does in its sweep (gc_jp_sweep)
+                    const int cv = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+                    for (long long e = g.hin_rp[v]; e < g.hin_rp[v + 1]; ++e) {
+                        const int hx = g.hin_col[e];
+                        if ((g.hk[hx] >> 2) == (unsigned)cv && !g.hkill[hx]) g.hkill[hx] = 1u;
+                    }
+                }
             } else {
                 gc_commit_colour(g, v, val);
                 if (want_cround) g.cround[v] = round;
@@ -2091,7 +2120,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
         for (int k = 0; k < 4; ++k) {
             const long long v = v0 + k;
             const unsigned b = (word >> (8 * k)) & 0xFFu;
-            const bool win = v < n && (v < lo || v >= hi) && gc_k8_state(b) == GC_JP_IN && gc_k8_cand(b) != GC_K8_NONE;
+            const bool win = v < n && (v < lo || v >= hi) && gc_k8_state(b) == GC_JP_IN && gc_k8_cand(b) != GC_K8_NONE &&
+                             !(g.hub_repl && g.hid[v] >= 0);  // replicated hubs: committed by k_commit
             if (!__ballot(win)) continue;
             long long tstart = 0;
             int din = 0, cc = 0;
@@ -2144,18 +2174,21 @@ __device__ __forceinline__ long long gc_hdr_word(long long x) {
 __global__ void __launch_bounds__(GC_BLOCK) k_shard_pack(GDev g, int kind, int slot, const long long* delta,
                                                          long long* send, long long cap) {
     const DevCtl* c = g.ctl;
-    const long long cnt = kind == GC_KIND_CAND ? (long long)c->fcnt[c->cur] : (long long)c->dcnt;
+    // (replicated hubs: the proposal deltas are compacted, k_delta_cand)
+    const long long cnt = kind == GC_KIND_CAND && !g.hub_repl ? (long long)c->fcnt[c->cur] : (long long)c->dcnt;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         long long h[GC_SEAM_HDR];
         if (kind == GC_KIND_CAND) {
-            h[0] = (long long)c->fcnt[c->cur];
+            h[0] = (long long)(c->fcnt[c->cur] - c->xhub_cnt);  // the rank's own frontier
             h[1] = c->maxmex;
             h[2] = (long long)c->failcnt;
             h[3] = cnt;
         } else {
-            h[0] = (long long)(c->und_cnt[slot] + c->undh_cnt[slot]);
+            // (+ hubs waiting for every rank's lights: gc_shard_start_hubs decides them)
+            h[0] = (long long)(c->und_cnt[slot] + c->undh_cnt[slot]) +
+                   (g.hub_w && c->hub_start == GC_HUB_NOT_STARTED ? (long long)c->heavy_cnt : 0ll);
             h[1] = cnt;
-            h[2] = 0;
+            h[2] = (long long)c->und_cnt[slot];  // undecided lights (every rank's 0: the hubs start)
             h[3] = cnt;
         }
         for (int i = 0; i < GC_SEAM_HDR; ++i) send[i] = gc_hdr_word(h[i]);
@@ -2183,9 +2216,55 @@ __global__ void k_shard_reset(GDev g, long long round) {
     c->list_cnt = 0;
     c->seed_cnt[0] = 0;
     c->seed_cnt[1] = 0;
+    c->xhub_cnt = 0;
+    c->lights_hold = g.hub_w ? 1 : 0;
+    c->hub_start = GC_HUB_NOT_STARTED;
     for (int k = 0; k < 3; ++k) {
         c->und_cnt[k] = 0;
         c->undh_cnt[k] = 0;
+    }
+}
+
+// Shards with replicated hubs: every uncoloured hub that a winner of any rank touched
+// (hseen, set by gc_hub_mark) joins this rank's frontier list `slot` (a hub is in the
+// frontier iff it has a coloured listed neighbour: coloring.py:86-95); the claim bitmap
+// keeps every hub listed once.
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_claim(GDev g, GLists L, int slot_next) {
+    DevCtl* c = g.ctl;
+    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    const int w = threadIdx.x / GC_WAVE;
+    const int slot = slot_next ? (c->cur ^ 1) : c->cur;
+    GcStage st{s_stage[w], 0};
+    const long long H = g.nhub_repl;
+    const long long steps = (H + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long x = sidx * GC_WAVE + gc_lane();
+        bool claim = false;
+        int v = 0;
+        if (x < H && g.hseen[x]) {
+            v = g.hub_v[x];
+            claim = g.c8[v] == GC_C8_NONE && gc_claim(g.inF, v);
+        }
+        gc_stage_push(st, claim, v, L.F[slot], &c->fcnt[slot]);
+    }
+    gc_stage_flush_block(st, L.F[slot], &c->fcnt[slot]);
+}
+
+// Replicated hubs after a slice seam moved light states without deltas: every other rank's
+// light winner flags the hubs listing it that propose its colour (what k_apply does for the
+// state deltas, and a local winner in its sweep).  Flags are idempotent.
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_flags(GDev g, long long lo, long long hi) {
+    const long long n = g.n;
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
+        if (v >= lo && v < hi) continue;
+        const unsigned kv = g.k8[v];
+        if (gc_k8_state(kv) != GC_JP_IN || gc_k8_cand(kv) == GC_K8_NONE || g.hid[v] >= 0) continue;
+        const int cv = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+        for (long long e = g.hin_rp[v]; e < g.hin_rp[v + 1]; ++e) {
+            const int hx = g.hin_col[e];
+            if ((g.hk[hx] >> 2) == (unsigned)cv && !g.hkill[hx]) g.hkill[hx] = 1u;
+        }
     }
 }
 
@@ -2575,6 +2654,14 @@ void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, l
 }
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
+}
+void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStream_t s) {
+    if (g.hub_repl && g.nhub_repl > 0)
+        hipLaunchKernelGGL(k_shard_hub_claim, dim3((int)std::min<long long>((g.nhub_repl + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, L, slot_next);
+}
+void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s) {
+    if (g.hub_repl && g.hub_w && g.n > 0)
+        hipLaunchKernelGGL(k_shard_hub_flags, dim3((int)std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, lo, hi);
 }
 void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
 // the winners gc_hub_push_wave left in `big`: a workgroup each walks its hub list

@@ -28,6 +28,12 @@ struct GDev {
     int big_rows;         // some in-row (+ hub row) may exceed bigrow: k_commit_big is needed
     int bigrow;           // heavy winners with longer in-rows (+ hub rows) go to k_commit_big (GC_BIGROW)
     int claim_direct;     // fused commit: claim with one atomic, no check-load first (GC_CLAIM_DIRECT)
+    // Shards with replicated hubs (gc_shard.hip): every rank runs the hub JP of every hub, so
+    // hubs never travel as deltas, and a rank claims the hubs its winners touched (hseen)
+    int hub_repl;
+    long long own_lo, own_hi;  // the rank's vertex range (hub_repl: failures counted by owners only)
+    int* hseen;               // hub x has a coloured listed neighbour (set by gc_hub_mark), or null
+    long long nhub_repl;      //   the number of hubs
     int* hpl;             // hubs-off heavy JP (gc_jp_sweep): heavy v's pending entries at hpl[rp[v] ..], or null
     int* hplc;            //   and their count (written by each sweep of v)
     // Hubs (variant A on one GPU; see gc_hubs.hip).  deg > heavy_t takes the
@@ -110,6 +116,11 @@ void gcl_shard_reset(const GDev& g, long long round, hipStream_t s);
 void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, long long* send, long long cap,
                     hipStream_t s);
 void gcl_shard_flip(const GDev& g, hipStream_t s);
+// replicated hubs: the uncoloured hubs a winner touched join the frontier (slot_next: the
+// next round's list, else the current one)
+void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStream_t s);
+// replicated hubs after a slice seam: the other ranks' light winners flag their hubs
+void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
 void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s);
 void gcl_partition_rows(const long long* rp, const int* col, const int* len, const int* split, int n, int* out,

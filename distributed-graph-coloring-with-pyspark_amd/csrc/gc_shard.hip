@@ -31,12 +31,21 @@ struct gc_shard {
     // Hub forbidden-colour bitmaps (gc_hubs.hip) for the proposals of the heavy vertices:
     // the hub lists (hid, hin) are the parent graph's, built once at gc_shard_create; the
     // bitmaps are this rank's replica, kept current by pushes from every winner, the rank's
-    // own (k_commit) and the others' (k_shard_list_commit / k_shard_scan_commit).  The
-    // resolution stays the row-scan JP (no hub JP in shards).
+    // own (k_commit) and the others' (k_shard_list_commit / k_shard_scan_commit).
     gc_graph* parent = nullptr;
     unsigned* hbits = nullptr;
     int hub_w = 0;
     long long nhub = 0;
+    // Replicated hubs (the default; GC_SHARD_HUBS=0 turns them off): every rank holds the
+    // hub JP state of EVERY hub (deg > the parent's hub threshold) and runs it on the
+    // replicated light states, so hubs are proposed, resolved and committed by every rank
+    // alike and never travel.  A rank lists every frontier hub (its own through its
+    // in-neighbour pushes, the others' through hseen, gc_shard_hub_claim); the hub JP starts
+    // once every rank's lights have converged (gc_shard_start_hubs) and runs to its end with
+    // no exchange, as the one-GPU engine's hub sweeps do (gc_hubs.hip).
+    bool repl = false;
+    unsigned *hk = nullptr, *hkill = nullptr;
+    int *hcur = nullptr, *hpc = nullptr, *hrow = nullptr, *hlen = nullptr, *hkcnt = nullptr, *hseen = nullptr;
 };
 
 // the shard's kernel arguments: its own view plus the parent's hub lists and its bitmaps
@@ -49,8 +58,62 @@ static GDev shard_view(gc_shard* sh) {
         d.hid = p->hid;
         d.hin_rp = p->hin_rp;
         d.hin_col = p->hin_col;
+        if (sh->repl) {  // the parent's read-only hub lists, this shard's hub JP state
+            d.heavy_t = p->hub_t;
+            d.hub_w = sh->hub_w;
+            d.hub_v = p->hub_v;
+            d.hlow_rp = p->hlow_rp;
+            d.hlow_col = p->hlow_col;
+            d.hlowb[0] = p->hlow_col;
+            d.hk = sh->hk;
+            d.hkill = sh->hkill;
+            d.hcur = sh->hcur;
+            d.hpc = sh->hpc;
+            d.hrow = sh->hrow;
+            d.hlen = sh->hlen;
+            d.hkcnt = sh->hkcnt;
+            d.hub_scan = 1;  // the resumable row scan (no per-round row copies to replicate)
+            d.hprep = 0;
+            d.hub_long = GC_HUB_LONG;
+            d.tail_hmax = GC_TAIL_HMAX_HUB;
+            d.hub_repl = 1;
+            d.own_lo = sh->lo;
+            d.own_hi = sh->hi;
+            d.hseen = sh->hseen;
+            d.nhub_repl = sh->nhub;
+        }
     }
     return d;
+}
+
+static void shard_free_hubs(gc_shard* sh) {
+    void* ptrs[] = {sh->hbits, sh->hk, sh->hkill, sh->hcur, sh->hpc, sh->hrow, sh->hlen, sh->hkcnt, sh->hseen};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    sh->hbits = sh->hk = sh->hkill = nullptr;
+    sh->hcur = sh->hpc = sh->hrow = sh->hlen = sh->hkcnt = sh->hseen = nullptr;
+    sh->repl = false;
+}
+
+// the shard's hub arrays: the bitmaps, and with replicated hubs the hub JP state
+static int shard_alloc_hubs(gc_shard* sh) {
+    const size_t H = (size_t)sh->nhub;
+    if (hipMalloc((void**)&sh->hbits, sizeof(unsigned) * H * (size_t)sh->hub_w) != hipSuccess) {
+        sh->hbits = nullptr;
+        gc_set_error("hipMalloc of the shard's hub bitmaps failed");
+        return GC_ENOMEM;
+    }
+    if (!sh->repl) return GC_OK;
+    void** arrs[] = {(void**)&sh->hk, (void**)&sh->hkill, (void**)&sh->hcur, (void**)&sh->hpc,
+                     (void**)&sh->hrow, (void**)&sh->hlen, (void**)&sh->hkcnt, (void**)&sh->hseen};
+    for (void** a : arrs) {
+        if (hipMalloc(a, 4 * H) != hipSuccess) {
+            *a = nullptr;
+            gc_set_error("hipMalloc of the shard's hub state failed");
+            return GC_ENOMEM;
+        }
+    }
+    return GC_OK;
 }
 
 static int shard_sync(gc_shard* sh) {
@@ -99,23 +162,29 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     }
     int rc = gc_build_in_csr(&v, lo, hi);
     if (!rc) rc = gc_alloc_run_state(&v);
-    if (!rc && g->maxdeg > GC_HEAVY_T) rc = gc_alloc_heavy_pending(&v);  // shards resolve heavy vertices by row scans
-    if (!rc) {  // hub lists on the parent (once), a bitmap replica for this shard
+    if (!rc) {  // hub lists on the parent (once), a bitmap replica (+ hub JP state) for this shard
         GDev pd = gc_view(g);
         rc = gc_hubs_prepare(g, pd);
-        if (!rc && g->nhub > 0 && v.maxdeg > GC_HEAVY_T) {  // heavy proposers (deg > GC_HEAVY_T) are hubs
+        const char* e = getenv("GC_SHARD_HUBS");
+        const bool want_repl = !(e && *e && atoi(e) == 0);
+        if (!rc && g->nhub > 0 && want_repl && g->hub_t >= 0) {  // every deg > hub_t vertex is a hub
             sh->parent = g;
             sh->hub_w = g->hub_w;
             sh->nhub = g->nhub;
-            if (hipMalloc((void**)&sh->hbits, sizeof(unsigned) * (size_t)g->nhub * (size_t)g->hub_w) != hipSuccess) {
-                sh->hbits = nullptr;
-                gc_set_error("hipMalloc of the shard's hub bitmaps failed");
-                rc = GC_ENOMEM;
-            }
+            sh->repl = true;
+            rc = shard_alloc_hubs(sh);
+        } else if (!rc && g->nhub > 0 && v.maxdeg > GC_HEAVY_T && g->hub_t <= GC_HEAVY_T) {
+            // bitmaps only: the heavy proposers (deg > GC_HEAVY_T) are hubs
+            sh->parent = g;
+            sh->hub_w = g->hub_w;
+            sh->nhub = g->nhub;
+            rc = shard_alloc_hubs(sh);
         }
     }
+    // without replicated hubs the shards resolve heavy vertices by row scans
+    if (!rc && !sh->repl && g->maxdeg > GC_HEAVY_T) rc = gc_alloc_heavy_pending(&v);
     if (rc) {
-        if (sh->hbits) hipFree(sh->hbits);
+        shard_free_hubs(sh);
         std::string keep = gc_last_error();
         gc_free_all(&v);
         delete sh;
@@ -129,7 +198,7 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
 extern "C" void gc_shard_destroy(gc_shard* sh) {
     if (!sh) return;
     gc_free_all(&sh->v);
-    if (sh->hbits) hipFree(sh->hbits);
+    shard_free_hubs(sh);
     delete sh;
 }
 
@@ -151,11 +220,17 @@ extern "C" int gc_shard_begin(gc_shard* sh, int64_t num_colors, int32_t track_ro
     GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, g->stream));
     if (sh->hbits)
         GC_HIP(hipMemsetAsync(sh->hbits, 0, sizeof(unsigned) * (size_t)sh->nhub * (size_t)sh->hub_w, g->stream));
+    if (sh->repl) {  // hk: k_init; hcur / hpc: every proposal
+        for (int* a : {sh->hrow, sh->hlen, sh->hkcnt, sh->hseen})
+            GC_HIP(hipMemsetAsync(a, 0, 4 * (size_t)sh->nhub, g->stream));
+        GC_HIP(hipMemsetAsync(sh->hkill, 0, 4 * (size_t)sh->nhub, g->stream));
+    }
     const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
     gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), g->stream);
     gcl_seed_prep(d, g->seeds[0], g->seeds[1], g->stream);
     gcl_commit(d, L, GC_CM_INIT, 0, g->stream);
+    gcl_shard_hub_claim(d, L, 0, g->stream);  // other ranks' hubs next to a seed
     int rc = shard_sync(sh);
     if (rc) return rc;
     if (U_out) *U_out = (int64_t)h.uncolored - (h.seedkey ? 1 : 0);
@@ -181,8 +256,8 @@ extern "C" int gc_shard_propose(gc_shard* sh, int64_t round, int64_t* delta, int
     int rc = shard_sync(sh);
     if (rc) return rc;
     const DevCtl& h = *g->hctl;
-    stats[0] = (int64_t)h.fcnt[h.cur];
-    stats[1] = (int64_t)h.fcnt[h.cur];
+    stats[0] = (int64_t)(sh->repl ? h.dcnt : h.fcnt[h.cur]);
+    stats[1] = (int64_t)(h.fcnt[h.cur] - h.xhub_cnt);
     stats[2] = h.maxmex;
     stats[3] = (int64_t)h.failcnt;
     return GC_OK;
@@ -288,7 +363,53 @@ extern "C" int gc_shard_sweep(gc_shard* sh, int32_t i, int32_t count, int64_t* d
     const DevCtl& h = *g->hctl;
     const int last = (i + count - 1) % 3;
     stats[0] = (int64_t)h.dcnt;
-    stats[1] = (int64_t)(h.und_cnt[last] + h.undh_cnt[last]);
+    stats[1] = (int64_t)(h.und_cnt[last] + h.undh_cnt[last]) +
+               (sh->repl && h.hub_start == GC_HUB_NOT_STARTED ? (int64_t)h.heavy_cnt : 0);
+    return GC_OK;
+}
+
+// Replicated hubs: the number of hubs (0: hubs, if any, are resolved through the exchange).
+extern "C" int gc_shard_hub_count(gc_shard* sh, int64_t* nhub) {
+    if (!sh || !nhub) { gc_set_error("null argument"); return GC_EINVAL; }
+    *nhub = sh->repl ? (int64_t)sh->nhub : 0;
+    return GC_OK;
+}
+
+// Replicated hubs, once every rank's lights are decided (every rank's sweep seam reported no
+// undecided light): start the hub JP at sweep i and run it to its end on this rank (every
+// rank runs the same sweeps on the same state, so no exchange).  from_slices: a slice seam
+// moved light states this round, so the other ranks' light winners flag their hubs here
+// (delta seams flagged them in gc_shard_apply).  sweeps_out: sweeps run (i, i+1, ...).
+extern "C" int gc_shard_start_hubs(gc_shard* sh, int32_t i, int32_t from_slices, int64_t* sweeps_out) {
+    if (!sh || i < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (sweeps_out) *sweeps_out = 0;
+    if (!sh->repl) return GC_OK;
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = shard_view(sh);
+    const GLists L = shard_lists(sh, nullptr);
+    if (from_slices) gcl_shard_hub_flags(d, sh->lo, sh->hi, g->stream);
+    GC_HIP(hipMemsetAsync(&g->ctl->lights_hold, 0, sizeof(int), g->stream));
+    const int batch = 8;  // sweeps past the end find no work and return at once
+    long long j = i;
+    for (;;) {
+        for (int k = 0; k < batch; ++k) gcl_sweep(d, L, (int)(j + k), g->stream);
+        j += batch;
+        int rc = shard_sync(sh);
+        if (rc) return rc;
+        const DevCtl& h = *g->hctl;
+        const int last = (int)((j - 1) % 3);
+        if ((h.und_cnt[last] | h.undh_cnt[last]) == 0 && h.hub_start != GC_HUB_NOT_STARTED) break;
+        if (j - i > 4 * (long long)sh->nhub + 64) {
+            gc_set_error("gc_shard_start_hubs: the hub sweeps did not converge");
+            return GC_EINVAL;
+        }
+    }
+    if (sweeps_out) {
+        const DevCtl& h = *g->hctl;
+        *sweeps_out = (int64_t)(j - i);
+        (void)h;
+    }
     return GC_OK;
 }
 
@@ -336,6 +457,7 @@ extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int32_t from_deltas,
     else gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->ulist, g->stream);
     if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->list_cnt, g->stream);  // the other ranks' winners
     gcl_shard_flip(d, g->stream);
+    gcl_shard_hub_claim(d, L, 0, g->stream);  // the other ranks' hubs next to this round's winners
     int rc = shard_sync(sh);
     if (rc) return rc;
     if (acc_out) *acc_out = (int64_t)g->hctl->accepted;
@@ -362,6 +484,7 @@ extern "C" int gc_shard_reseed(gc_shard* sh, int64_t round, int64_t* nseeds, int
     gcl_cc_seeds(d, g->ulist, &g->ctl->list_cnt, g->parent, g->best, g->seeds[0], g->seeds[1],
                  gc_grid_for_waves(Lc, 4096), g->stream);
     gcl_commit(d, L, GC_CM_RESEED, 0, g->stream);
+    gcl_shard_hub_claim(d, L, 0, g->stream);
     if ((rc = shard_sync(sh))) return rc;
     if (nseeds) *nseeds = (int64_t)(g->hctl->seed_cnt[0] + g->hctl->seed_cnt[1]);
     if (F_out) *F_out = (int64_t)g->hctl->fcnt[g->hctl->cur];

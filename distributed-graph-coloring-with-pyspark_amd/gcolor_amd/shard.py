@@ -255,6 +255,15 @@ class HipShard:
                                                              self.cap, self._st))
         return self._st[0], self._st[1]
 
+    def hub_count(self):
+        nat.check("gc_shard_hub_count", self._lib.gc_shard_hub_count(self._h, self._ct.byref(self._a)))
+        return self._a.value
+
+    def start_hubs(self, i, from_slices):
+        nat.check("gc_shard_start_hubs", self._lib.gc_shard_start_hubs(self._h, i, 1 if from_slices else 0,
+                                                                       self._ct.byref(self._a)))
+        return self._a.value
+
     def slice_buffer(self, stride):
         # one cached buffer per size (header + slice, or the bare slice of an overflow)
         if self._slice is None:
@@ -363,6 +372,8 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     lens = [int(x) for x in rng[:, 1] - rng[:, 0]]
     stride = max(max(lens), 1)
     C = max(int(inline), 0)
+    # replicated hubs (gc_shard_start_hubs): the same count on every rank
+    repl = getattr(ops, "hub_count", lambda: 0)() > 0
     hdr_bytes = 8 * HDR
 
     def rec(u, f, mm, acc, seeds):
@@ -445,6 +456,10 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             else:
                 any_dense |= finish_deltas(KIND_STATE, hdr, recv, r, True)
             if int(hdr[:, 0].sum()) == 0:
+                break
+            if repl and int(hdr[:, 2].sum()) == 0:
+                # every rank's lights are decided: each rank runs the hubs' sweeps alike
+                res.jp_sweeps += ops.start_hubs(i, any_dense)
                 break
             left = int(hdr[:, 0].max())
             res.jp_sweeps += 1

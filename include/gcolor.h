@@ -167,13 +167,22 @@ int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count
 int gc_shard_propose_async(gc_shard* s, int64_t round, int64_t* delta, int64_t cap);
 int gc_shard_sweep_async(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap);
 /* a seam's send buffer (device, 4 + cap int64): 4 header words -- propose: frontier, max
-   candidate, #candidates >= k, #deltas; sweep: undecided in list slot `slot`, #deltas, 0,
-   #deltas -- each encoded (0xFFFFFFFF << 32 | value) so appliers skip it as padding, then
+   candidate, #candidates >= k, #deltas; sweep: undecided in list slot `slot` (+ hubs
+   waiting for gc_shard_start_hubs), #deltas, undecided light vertices, #deltas -- each encoded (0xFFFFFFFF << 32 | value) so appliers skip it as padding, then
    up to cap deltas padded with -1 (delta == NULL: the header only)                      */
 int gc_shard_pack(gc_shard* s, int32_t kind, int32_t slot, const int64_t* delta, int64_t* send, int64_t cap);
 /* sweeps i .. i+count-1 (i = 0: first sweep over the frontier, then over the undecided);
    delta may be NULL (slice seam).  stats[2]: deltas written, still undecided here      */
 int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap, int64_t* stats);
+/* Replicated hubs (default; GC_SHARD_HUBS=0 at gc_shard_create turns them off): every rank
+   holds and runs the hub state of every high-degree vertex, so hubs never travel.
+   *nhub = the number of replicated hubs (0: none, hubs resolve through the seams).  Once a
+   sweep seam reports no undecided light vertex on any rank (header word 2 == 0 on every
+   rank) while vertices are still undecided (word 0), gc_shard_start_hubs runs the hubs'
+   sweeps i, i+1, ... to their end with no exchange (from_slices = 1: a slice seam moved
+   light states this round); *sweeps_out = sweeps run.                                  */
+int gc_shard_hub_count(gc_shard* s, int64_t* nhub);
+int gc_shard_start_hubs(gc_shard* s, int32_t i, int32_t from_slices, int64_t* sweeps_out);
 /* slice seam: the rank's slice [lo, hi) of the proposal bytes (cand6 << 2 | JP state)
    into dst (device, hi - lo bytes); put_slices copies the other ranks' slices back    */
 int gc_shard_get_slice(gc_shard* s, uint8_t* dst);

@@ -105,6 +105,43 @@ def test_uniform_and_mesh_sharded():
         assert r.max_color + 1 == 2
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_replicated_hubs_sharded(seed, monkeypatch):
+    """A low hub threshold makes most proposers replicated hubs: every rank proposes,
+    resolves (gc_shard_start_hubs, after every rank's lights) and commits all of them, and
+    claims the other ranks' hubs next to winners -- still bit-identical to one GPU, with
+    delta and slice seams, a colour bound, E1 re-seeds, and with the hubs sent as deltas
+    instead (GC_SHARD_HUBS=0)."""
+    from gcolor_amd.engine import DeviceGraph
+    from gcolor_amd import shard as sh
+    from gcolor_amd.generators import reference_csr
+    monkeypatch.setenv("GC_HUB_T", "8")
+    rp, col = _random_directed(3000, 15000, seed)
+    with DeviceGraph.from_csr(rp, col) as dg:
+        probe = sh.HipShard(dg, 0, dg.n)
+        assert probe.hub_count() > 100
+        probe.close()
+        r, one = same_as_single(dg, 3)
+        same_as_single(dg, 2, k=max(one.max_color, 1))
+        r, _ = same_as_single(dg, 3, dense=True)
+        assert r.dense_exchanges > 0
+        same_as_single(dg, 4, dense=False, local_sweeps=3)
+    with DeviceGraph.rmat(12, 16, seed=seed) as dg:
+        same_as_single(dg, 4)
+        same_as_single(dg, 2, dense=True)
+    monkeypatch.setenv("GC_HUB_T", "4")
+    rp, col = reference_csr(4000, 8, random.Random(1 + seed))
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        r, one = same_as_single(dg, 3)
+        assert r.reseeds == one.reseeds
+    monkeypatch.setenv("GC_SHARD_HUBS", "0")
+    with DeviceGraph.rmat(12, 16, seed=seed) as dg:
+        probe = sh.HipShard(dg, 0, dg.n)
+        assert probe.hub_count() == 0
+        probe.close()
+        same_as_single(dg, 3)
+
+
 def _gloo_gpu_worker(rank, world, port, out_dir):
     import torch.distributed as dist
     sys.path[:0] = [PKG_DIR, REPO]
