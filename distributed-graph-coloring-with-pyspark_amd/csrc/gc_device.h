@@ -151,20 +151,21 @@ __device__ __forceinline__ bool gc_hub_gate(const GDev& g, const DevCtl* c, long
 
 // Algorithmic-byte counters (stats only): a workgroup adds into slot blockIdx % GC_STAT_SLOTS
 // instead of every workgroup hitting the same two DevCtl words; k_stat_reduce sums them.
+template <int NW = GC_WAVES_PER_BLOCK>
 __device__ __forceinline__ void gc_stat_add(const GDev& g, int cls, ull lsum, ull lnv, ull* lds_scratch) {
     lsum = gc_wave_sum(lsum);
     lnv = gc_wave_sum(lnv);
     const int w = threadIdx.x / GC_WAVE;
     if (gc_lane() == 0) {
         lds_scratch[w] = lsum;
-        lds_scratch[GC_WAVES_PER_BLOCK + w] = lnv;
+        lds_scratch[NW + w] = lnv;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         ull a = 0, b = 0;
         for (int i = 0; i < (int)(blockDim.x / GC_WAVE); ++i) {
             a += lds_scratch[i];
-            b += lds_scratch[GC_WAVES_PER_BLOCK + i];
+            b += lds_scratch[NW + i];
         }
         ull* slot = g.bstat + (blockIdx.x % GC_STAT_SLOTS) * 16;
         if (a) atomicAdd(slot + cls, a);

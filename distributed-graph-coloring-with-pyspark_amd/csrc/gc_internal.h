@@ -46,11 +46,14 @@ typedef unsigned long long ull;
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)
 #define GC_ROUND_GRID 1024
 #ifndef GC_TAIL_MAX
-#define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail
+#define GC_TAIL_MAX 1024  // JP sweeps over at most this many light vertices run in k_sweep_tail (GDev.tail_lmax)
 #endif
 #define GC_LOOP_MAX 65536 // ... and over at most this many light vertices in k_sweep_loop
 #define GC_LOOP_HMAX 16384 //   (hubs)
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
+#ifndef GC_TAIL_WAVES
+#define GC_TAIL_WAVES 4   // waves of k_sweep_tail's one workgroup (4, 8 or 16; GDev.tail_nw)
+#endif
 #define GC_BLOCK_GRID 1024
 #define GC_STAT_SLOTS 256
 #define GC_ACC_SLOTS 256   // commit's winner count, summed by k_close  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
@@ -234,8 +237,9 @@ __device__ __forceinline__ void gc_stage_flush(GcStage& s, int* out, ull* out_cn
 // End-of-kernel flush for the whole workgroup (every thread calls): one global atomic per
 // workgroup instead of one per wave -- thousands of waves each returning a handful of
 // entries on one counter cost ~10 us per 1000 atomics.
+template <int NW = GC_WAVES_PER_BLOCK>
 __device__ __forceinline__ void gc_stage_flush_block(GcStage& s, int* out, ull* out_cnt) {
-    __shared__ int s_cnt[GC_WAVES_PER_BLOCK];
+    __shared__ int s_cnt[NW];
     __shared__ ull s_base;
     const int w = threadIdx.x / GC_WAVE;
     gc_wave_sync();
@@ -243,7 +247,7 @@ __device__ __forceinline__ void gc_stage_flush_block(GcStage& s, int* out, ull* 
     __syncthreads();
     if (threadIdx.x == 0) {
         int t = 0;
-        for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += s_cnt[i];
+        for (int i = 0; i < NW; ++i) t += s_cnt[i];
         s_base = t ? atomicAdd(out_cnt, (ull)t) : 0ull;
     }
     __syncthreads();

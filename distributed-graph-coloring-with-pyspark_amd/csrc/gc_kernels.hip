@@ -857,17 +857,18 @@ __device__ void gc_hub_first_long(GDev& g) {
 
 // One JP sweep over a light list (wave chunks) and a heavy list (workgroup per vertex);
 // undecided vertices are appended to (uo, uo_cnt) / (ho, ho_cnt).
+template <int NW = GC_WAVES_PER_BLOCK>
 __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ list, long long cnt, int skip_heavy,
                                             const int* hlist, long long hcnt, int* uo, ull* uo_cnt, int* ho,
                                             ull* ho_cnt, ull& lsum, ull& lnv, long long* dout, ull* dcnt,
                                             bool hub_first = false) {
-    __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_first[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ unsigned s_flag[NW][GC_WAVE];
+    __shared__ int s_first[NW][GC_WAVE];
+    __shared__ long long s_start[NW][GC_WAVE];
+    __shared__ unsigned s_c6[NW][GC_WAVE];
+    __shared__ int s_cv[NW][GC_WAVE];
     __shared__ unsigned s_f;
-    __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+    __shared__ int s_stage[NW][GC_STAGE_CAP];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const unsigned char* __restrict__ k8 = g.k8;
@@ -881,8 +882,8 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
         // a wave's hubs are i = wid + j * waves; lane l loads the state of hub j0 + l, so a
         // hub's evaluation starts at its row read
-        const long long waves = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
-        const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+        const long long waves = (long long)gridDim.x * NW;
+        const long long wid = (long long)blockIdx.x * NW + w;
         for (long long i0 = wid; i0 < hcnt; i0 += waves * GC_WAVE) {
             const long long il = i0 + (long long)lane * waves;
             int pv = -1, px = -1, pcv = 0;
@@ -1016,10 +1017,10 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         __syncthreads();
     }
     if (w == 0) gc_stage_flush(hst, ho, ho_cnt);
-    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    const int vpw = gc_vpw(cnt, (long long)gridDim.x * NW);
     const long long nch = gc_nchunks(cnt, vpw);
-    for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
-         ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+    for (long long ch = (long long)blockIdx.x * NW + w; ch < nch;
+         ch += (long long)gridDim.x * NW) {
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         // the vertex's words are loaded together (none waits on another: one memory trip)
@@ -1087,7 +1088,7 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                 });
         }
     }
-    gc_stage_flush_block(st, uo, uo_cnt);
+    gc_stage_flush_block<NW>(st, uo, uo_cnt);
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
@@ -1140,7 +1141,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
         c->und_cnt[z] = 0;
         c->undh_cnt[z] = 0;
         if (cl + ch > 0) c->sweeps += 1;
-        if (cl > GC_TAIL_MAX || ch > gc_tail_hmax(g)) c->bigsweeps = i;
+        if (cl > g.tail_lmax || ch > gc_tail_hmax(g)) c->bigsweeps = i;
         if (cl > GC_LOOP_MAX || ch > GC_LOOP_HMAX) c->hugesweeps = i;
         if (hub_start) c->hub_start = i;
     }
@@ -1207,7 +1208,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_loop(GDev g, GLists L, int S
         const int* hl = L.undH[in];
         const bool hub_start = gc_hub_gate(g, c, j + 1, cl, hl, ch, L);
         // empty, or small enough for the one-workgroup tail (k_sweep_tail takes it from here)
-        if (cl + ch == 0 || (cl <= GC_TAIL_MAX && ch <= gc_tail_hmax(g))) break;
+        if (cl + ch == 0 || (cl <= g.tail_lmax && ch <= gc_tail_hmax(g))) break;
         ++j;
         const int out = j % 3, z = (j + 1) % 3;
         __syncthreads();  // every workgroup has read hub_start before block 0 moves it
@@ -1235,14 +1236,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_loop(GDev g, GLists L, int S
 // deep end of a JP resolution is a chain of sweeps over a few hundred vertices each, which
 // as separate 2048-workgroup launches cost a launch gap apiece (and the sweeps enqueued
 // beyond the round's depth ran idle).  Here they run back to back, a workgroup barrier
-// apart, while the undecided lists stay within GC_TAIL_MAX / GC_TAIL_HMAX; a bigger list
+// apart, while the undecided lists stay within tail_lmax / tail_hmax; a bigger list
 // is left to full-grid sweeps (the commit then asks the host for them, GC_H_SWEEPS).
 // Counters are read with atomic RMWs and cleared with agent-scope stores; list entries and
 // states written before a barrier are visible to the whole workgroup after it.
-__global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S) {
+template <int NW>
+__global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, int S) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    __shared__ ull scratch[2 * NW];
     __shared__ long long s_cl, s_ch;
     int j = c->loop_last > S ? (int)c->loop_last : S;  // after k_sweep_loop's sweeps, if it ran
     ull lsum = 0, lnv = 0;
@@ -1257,7 +1259,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S
         long long ch = s_ch;
         const int* hl = L.undH[in];
         const bool hub_start = gc_hub_gate(g, c, j + 1, cl, hl, ch, L);
-        if (cl + ch == 0 || cl > GC_TAIL_MAX || ch > gc_tail_hmax(g)) break;
+        if (cl + ch == 0 || cl > g.tail_lmax || ch > gc_tail_hmax(g)) break;
         ++j;
         const int out = j % 3, z = (j + 1) % 3;  // out was cleared by the sweep before
         __syncthreads();  // every thread has read hub_start before thread 0 moves it
@@ -1267,12 +1269,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_tail(GDev g, GLists L, int S
             gc_st(&c->sweeps, c->sweeps + 1);
             if (hub_start) gc_st(&c->hub_start, (long long)j);
         }
-        gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
+        gc_jp_sweep<NW>(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                     &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt);
         __syncthreads();
     }
     if (threadIdx.x == 0) gc_st(&c->tail_last, (long long)j);
-    gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
+    gc_stat_add<NW>(g, GC_K_SWEEP, lsum, lnv, scratch);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2685,7 +2687,9 @@ void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t
     hipLaunchKernelGGL(k_sweep_loop, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S);
 }
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep_tail, dim3(1), dim3(GC_BLOCK), 0, s, g, L, S);
+    if (g.tail_nw == 16) hipLaunchKernelGGL(k_sweep_tail<16>, dim3(1), dim3(16 * GC_WAVE), 0, s, g, L, S);
+    else if (g.tail_nw == 8) hipLaunchKernelGGL(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
+    else hipLaunchKernelGGL(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
 }
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);

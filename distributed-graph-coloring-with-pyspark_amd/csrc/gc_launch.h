@@ -46,6 +46,8 @@ struct GDev {
                               //   commits' pushes (0 = none): == hub_w, or alone (seeded ranks,
                               //   speculative rounds, variant B, whose resolution has no hub JP)
     int tail_hmax;            // heavy entries the one-workgroup tail sweeps may take (GC_TAIL_HMAX[_HUB])
+    int tail_lmax;            // light entries the tail sweeps may take (GC_TAIL_MAX; env GC_TAIL_LMAX)
+    int tail_nw;              // waves of the tail's workgroup: 4, 8 or 16 (env GC_TAIL_WAVES)
     long long hub_long;       // hub-start sweep: hubs whose hlow row exceeds this are first-read by the whole grid
     const long long* hch_rp;  // static GC_HCH-entry chunks of the hlow rows (hub x: [hch_rp[x], hch_rp[x+1]))
     const int* hch_own;       //   chunk -> hub

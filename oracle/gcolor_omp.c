@@ -29,6 +29,7 @@
  * Every thread-shared byte is read and written with relaxed atomics.
  */
 #include <omp.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -382,7 +383,13 @@ int omp_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t symmetri
            are light) */
         const int32_t rr = (int32_t)r;
         int32_t *Li = L0, *Lo = L1;
+        /* GC_OMP_SWEEPLOG: per round, the JP list sizes (lights, then hubs) on stderr --
+           the shape of the dependency chains the GPU's sweeps walk (analysis only) */
+        static int slog = -1;
+        if (slog < 0) slog = getenv("GC_OMP_SWEEPLOG") != NULL;
+        if (slog) fprintf(stderr, "r %lld F %lld L", (long long)r, (long long)nF);
         while (nl > 0) {
+            if (slog) fprintf(stderr, " %lld", (long long)nl);
 #pragma omp parallel
             {
                 Buf* b = &bufs[omp_get_thread_num()];
@@ -423,7 +430,9 @@ int omp_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t symmetri
             }
             int32_t *Hi = H0, *Ho = H1;
             int64_t nh = nhp;
+            if (slog) fprintf(stderr, " H");
             while (nh > 0) {
+                if (slog) fprintf(stderr, " %lld", (long long)nh);
 #pragma omp parallel
                 {
                     Buf* b = &bufs[omp_get_thread_num()];
@@ -446,6 +455,7 @@ int omp_color(const int64_t* rp, const int32_t* col, int64_t n, int32_t symmetri
                 Ho = t;
             }
         }
+        if (slog) fprintf(stderr, "\n");
         /* commit (coloring.py:114-127) + push; losers stay in the frontier */
         int64_t acc = 0;
 #pragma omp parallel reduction(+ : acc)
