@@ -80,6 +80,9 @@ typedef unsigned long long ull;
 #define GC_CM_INIT 1
 #define GC_CM_RESEED 2
 #define GC_CM_SHARD 3   // sharded round: the rank's frontier, no halt / sweep checks
+// k_commit nsweeps in GC_CM_SHARD mode: the replicated hub JP ran asynchronously
+// (gc_shard_start_hubs_async): check that it converged first, else halt with GC_H_SWEEPS
+#define GC_SHARD_CHECK (-3)
 
 // kinds of exchanged deltas (sharded engine)
 #define GC_KIND_CAND 0
@@ -153,6 +156,7 @@ struct DevCtl {
     int pad4;
     int proposed;           // the current round's proposals were made by the last (fused) commit
     int pad3;
+    long long acc_last;     // shards: winners of the last finished round (k_shard_reset keeps them for the seam header)
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };

@@ -1523,7 +1523,8 @@ template <int FUSE>
 __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode, int nsweeps, int allow_big,
                                                      DevCtl* snap, int tclose) {
     DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) {
+    const bool shard_check = mode == GC_CM_SHARD && nsweeps == GC_SHARD_CHECK;
+    if ((mode == GC_CM_ROUND || shard_check) && c->halt) {
         if (snap && blockIdx.x == 0) gc_snap_copy(c, snap);
         return;
     }
@@ -1537,9 +1538,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     // k_sweep_tail ran before (nsweeps >= 0), else only the first sweep (k_resolve, slot 0) did
-    const long long last = mode == GC_CM_ROUND ? (nsweeps < 0 ? 0ll : c->tail_last) : nsweeps;
+    const long long last = mode == GC_CM_ROUND ? (nsweeps < 0 ? 0ll : c->tail_last) : (shard_check ? c->tail_last : nsweeps);
     const int last_slot = (int)(last % 3);
-    if (mode == GC_CM_ROUND &&
+    if ((mode == GC_CM_ROUND || shard_check) &&
         ((c->und_cnt[last_slot] | c->undh_cnt[last_slot]) || (g.hub_w && c->heavy_cnt && c->hub_start > last))) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             c->sweeps_enq = last;
@@ -1956,6 +1957,7 @@ __global__ void k_close(GDev g, GLists L, int mode, int allow_big, int fused, De
 // propose seam: (v, candidate) for every frontier entry of this rank
 __global__ void __launch_bounds__(GC_BLOCK) k_delta_cand(GDev g, GLists L) {
     const DevCtl* c = g.ctl;
+    if (c->halt) return;
     const int cur = c->cur;
     const long long cnt = (long long)c->fcnt[cur];
     const int* list = L.F[cur];
@@ -2025,6 +2027,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long
 // in-neighbours (owned targets only), O(winners) instead of k_shard_scan_commit's O(n).
 __global__ void __launch_bounds__(GC_BLOCK) k_shard_list_commit(GDev g, GLists L, const int* rwin, int* big) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;  // the hub JP did not converge (GC_SHARD_CHECK): the host adds sweeps
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -2091,6 +2094,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_list_commit(GDev g, GLists L
 // One 4-byte word of k8 per lane, 256 vertices per wave step.
 __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L, long long lo, long long hi, int* big) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -2166,10 +2170,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
 // A seam's send buffer, built on the device (no host round trip): HDR header words -- the
 // rank's round scalars, encoded as (0xFFFFFFFF << 32 | value) so every delta applier reads
 // them as padding -- then up to cap of the phase's deltas, padded with -1.
-//   kind GC_KIND_CAND  (propose seam): frontier, max candidate, #candidates >= k, #deltas
-//   kind GC_KIND_STATE (sweep seam):   undecided (lists of slot `slot`), #deltas, 0, #deltas
+//   kind GC_KIND_CAND  (propose seam): frontier, max candidate, #candidates >= k, #deltas,
+//                      winners of the last finished round (-halt code when it halted)
+//   kind GC_KIND_STATE (sweep seam):   undecided (lists of slot `slot`), #deltas, undecided lights, #deltas, 0
 // With delta == null only the header is written (the slice seams).
-#define GC_SEAM_HDR 4
+#define GC_SEAM_HDR 5
 __device__ __forceinline__ long long gc_hdr_word(long long x) {
     return (long long)((0xFFFFFFFFull << 32) | (ull)(unsigned)x);
 }
@@ -2185,6 +2190,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_pack(GDev g, int kind, int s
             h[1] = c->maxmex;
             h[2] = (long long)c->failcnt;
             h[3] = cnt;
+            h[4] = c->halt ? -(long long)c->halt : c->acc_last;
         } else {
             // (+ hubs waiting for every rank's lights: gc_shard_start_hubs decides them)
             h[0] = (long long)(c->und_cnt[slot] + c->undh_cnt[slot]) +
@@ -2192,6 +2198,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_pack(GDev g, int kind, int s
             h[1] = cnt;
             h[2] = (long long)c->und_cnt[slot];  // undecided lights (every rank's 0: the hubs start)
             h[3] = cnt;
+            h[4] = 0;
         }
         for (int i = 0; i < GC_SEAM_HDR; ++i) send[i] = gc_hdr_word(h[i]);
     }
@@ -2204,6 +2211,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_pack(GDev g, int kind, int s
 __global__ void k_shard_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
+    if (c->halt == GC_H_SWEEPS) return;  // the last finish halted: everything stays for gc_shard_resume_hubs
+    c->acc_last = (long long)c->accepted;
     c->halt = GC_RUN;
     c->round = round;
     c->heavy_cnt = 0;
@@ -2233,6 +2242,7 @@ __global__ void k_shard_reset(GDev g, long long round) {
 // keeps every hub listed once.
 __global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_claim(GDev g, GLists L, int slot_next) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
     const int slot = slot_next ? (c->cur ^ 1) : c->cur;
@@ -2274,6 +2284,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_flags(GDev g, long long 
 __global__ void k_shard_flip(GDev g) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     c->fcnt[c->cur] = 0;
     c->cur ^= 1;
 }

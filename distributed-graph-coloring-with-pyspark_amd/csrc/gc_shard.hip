@@ -44,6 +44,7 @@ struct gc_shard {
     // once every rank's lights have converged (gc_shard_start_hubs) and runs to its end with
     // no exchange, as the one-GPU engine's hub sweeps do (gc_hubs.hip).
     bool repl = false;
+    int tail_hmax = 4 * GC_TAIL_HMAX_HUB;  // hubs the one-workgroup tail sweeps take (GC_SHARD_TAIL_HMAX)
     unsigned *hk = nullptr, *hkill = nullptr;
     int *hcur = nullptr, *hpc = nullptr, *hrow = nullptr, *hlen = nullptr, *hkcnt = nullptr, *hseen = nullptr;
 };
@@ -75,7 +76,7 @@ static GDev shard_view(gc_shard* sh) {
             d.hub_scan = 1;  // the resumable row scan (no per-round row copies to replicate)
             d.hprep = 0;
             d.hub_long = GC_HUB_LONG;
-            d.tail_hmax = GC_TAIL_HMAX_HUB;
+            d.tail_hmax = sh->tail_hmax;  // the async hub JP (gc_shard_start_hubs_async) leans on the tail
             d.hub_repl = 1;
             d.own_lo = sh->lo;
             d.own_hi = sh->hi;
@@ -150,6 +151,7 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     v.nlow = g->nlow;
     sh->lo = lo;
     sh->hi = hi;
+    if (getenv("GC_SHARD_TAIL_HMAX")) sh->tail_hmax = std::max(0, atoi(getenv("GC_SHARD_TAIL_HMAX")));
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&v.ev0)) != hipSuccess || (e = hipEventCreate(&v.ev1)) != hipSuccess ||
@@ -375,6 +377,8 @@ extern "C" int gc_shard_hub_count(gc_shard* sh, int64_t* nhub) {
     return GC_OK;
 }
 
+static int hub_sweeps_to_end(gc_shard* sh, int j0, int64_t* sweeps_out);
+
 // Replicated hubs, once every rank's lights are decided (every rank's sweep seam reported no
 // undecided light): start the hub JP at sweep i and run it to its end on this rank (every
 // rank runs the same sweeps on the same state, so no exchange).  from_slices: a slice seam
@@ -387,9 +391,54 @@ extern "C" int gc_shard_start_hubs(gc_shard* sh, int32_t i, int32_t from_slices,
     if (!sh->repl) return GC_OK;
     GC_HIP(hipSetDevice(g->device));
     const GDev d = shard_view(sh);
+    if (from_slices) gcl_shard_hub_flags(d, sh->lo, sh->hi, g->stream);
+    GC_HIP(hipMemsetAsync(&g->ctl->lights_hold, 0, sizeof(int), g->stream));
+    return hub_sweeps_to_end(sh, i, sweeps_out);
+}
+
+// The asynchronous form: the hubs' first `grid` sweeps (i, i+1, ...) on the full grid, then
+// the one-workgroup tail (k_sweep_tail) runs the rest of the chain while the lists stay
+// within its limits.  Nothing waits: gc_shard_finish_async(check = 1) verifies on the device
+// that the hub JP converged (else the round halts with GC_H_SWEEPS, reported in the next
+// propose seam's header, and gc_shard_resume_hubs finishes it).  Every rank runs the same
+// sweeps on the same replicated state, so every rank halts alike.
+extern "C" int gc_shard_start_hubs_async(gc_shard* sh, int32_t i, int32_t from_slices, int32_t grid) {
+    if (!sh || i < 1 || grid < 1) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (!sh->repl) return GC_OK;
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
     if (from_slices) gcl_shard_hub_flags(d, sh->lo, sh->hi, g->stream);
     GC_HIP(hipMemsetAsync(&g->ctl->lights_hold, 0, sizeof(int), g->stream));
+    for (int k = 0; k < grid; ++k) gcl_sweep(d, L, i + k, g->stream);
+    gcl_sweep_tail(d, L, i + grid - 1, g->stream);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+// After a finish that halted (the previous propose seam's header carried -GC_H_SWEEPS on
+// every rank): clear the halt and run the hub sweeps from the first one not yet run to
+// their end (host-paced, as gc_shard_start_hubs); then the caller enqueues the finish again.
+extern "C" int gc_shard_resume_hubs(gc_shard* sh, int64_t* sweeps_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    if (sweeps_out) *sweeps_out = 0;
+    GC_HIP(hipSetDevice(g->device));
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    if (g->hctl->halt != GC_H_SWEEPS) { gc_set_error("gc_shard_resume_hubs: the shard is not halted for sweeps"); return GC_EINVAL; }
+    const long long j = g->hctl->sweeps_enq + 1;
+    GC_HIP(hipMemsetAsync(&g->ctl->halt, 0, sizeof(int), g->stream));
+    return hub_sweeps_to_end(sh, (int)j, sweeps_out);
+}
+
+// hub sweeps j0, j0+1, ... in batches, host-paced, until the lists are empty
+static int hub_sweeps_to_end(gc_shard* sh, int j0, int64_t* sweeps_out) {
+    gc_graph* g = &sh->v;
+    const GDev d = shard_view(sh);
+    const GLists L = shard_lists(sh, nullptr);
+    const int i = j0;
     const int batch = 8;  // sweeps past the end find no work and return at once
     long long j = i;
     for (;;) {
@@ -405,11 +454,9 @@ extern "C" int gc_shard_start_hubs(gc_shard* sh, int32_t i, int32_t from_slices,
             return GC_EINVAL;
         }
     }
-    if (sweeps_out) {
-        const DevCtl& h = *g->hctl;
-        *sweeps_out = (int64_t)(j - i);
-        (void)h;
-    }
+    if (sweeps_out) *sweeps_out = (int64_t)(j - i);
+    const long long tl = j - 1;  // the last sweep run: what a checked finish looks at
+    GC_HIP(hipMemcpy(&g->ctl->tail_last, &tl, sizeof(long long), hipMemcpyHostToDevice));
     return GC_OK;
 }
 
@@ -446,24 +493,40 @@ extern "C" int gc_shard_put_slices(gc_shard* sh, const uint8_t* src, int64_t str
 // replicated proposal bytes (a slice seam moved some states without deltas) -- push them
 // into this rank's in-neighbours and make that frontier current.
 // acc_out: winners of ALL ranks (the same on every rank); F_out: the rank's new frontier.
-extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int32_t from_deltas, int64_t* acc_out, int64_t* F_out) {
-    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+static int shard_finish_enqueue(gc_shard* sh, int32_t from_deltas, int32_t check) {
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
     const GDev d = shard_view(sh);
     const GLists L = shard_lists(sh, nullptr);
-    gcl_commit(d, L, GC_CM_SHARD, 0, g->stream);
+    gcl_commit(d, L, GC_CM_SHARD, check ? GC_SHARD_CHECK : 0, g->stream);
     if (from_deltas) gcl_shard_list_commit(d, L, g->parent, g->ulist, g->stream);
     else gcl_shard_scan_commit(d, L, sh->lo, sh->hi, g->ulist, g->stream);
     if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->list_cnt, g->stream);  // the other ranks' winners
     gcl_shard_flip(d, g->stream);
     gcl_shard_hub_claim(d, L, 0, g->stream);  // the other ranks' hubs next to this round's winners
-    int rc = shard_sync(sh);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+extern "C" int gc_shard_finish(gc_shard* sh, int64_t round, int32_t from_deltas, int64_t* acc_out, int64_t* F_out) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    int rc = shard_finish_enqueue(sh, from_deltas, 0);
+    if (!rc) rc = shard_sync(sh);
     if (rc) return rc;
     if (acc_out) *acc_out = (int64_t)g->hctl->accepted;
     if (F_out) *F_out = (int64_t)g->hctl->fcnt[g->hctl->cur];
     (void)round;
     return GC_OK;
+}
+
+// The same, only enqueued: the winners' count reaches the host in the next propose seam's
+// header (k_shard_pack, word 4).  check = 1: the hub JP ran asynchronously
+// (gc_shard_start_hubs_async); the commit first verifies on the device that it converged.
+extern "C" int gc_shard_finish_async(gc_shard* sh, int64_t round, int32_t from_deltas, int32_t check) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    (void)round;
+    return shard_finish_enqueue(sh, from_deltas, check);
 }
 
 // E1 on the replicated state (identical seeds on every rank), seeds pushed into the

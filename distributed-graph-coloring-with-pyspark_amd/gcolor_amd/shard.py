@@ -264,6 +264,21 @@ class HipShard:
                                                                        self._ct.byref(self._a)))
         return self._a.value
 
+    def start_hubs_async(self, i, from_slices, grid=3):
+        """the hub sweeps enqueued (``grid`` full-grid sweeps, then the one-workgroup tail);
+        a checked ``finish_async`` verifies on the device that they converged"""
+        nat.check("gc_shard_start_hubs_async", self._lib.gc_shard_start_hubs_async(
+            self._h, i, 1 if from_slices else 0, int(grid)))
+        return int(grid)
+
+    def resume_hubs(self):
+        nat.check("gc_shard_resume_hubs", self._lib.gc_shard_resume_hubs(self._h, self._ct.byref(self._a)))
+        return self._a.value
+
+    def finish_async(self, r, from_deltas=False, check=False):
+        nat.check("gc_shard_finish_async", self._lib.gc_shard_finish_async(self._h, r, 1 if from_deltas else 0,
+                                                                           1 if check else 0))
+
     def slice_buffer(self, stride):
         # one cached buffer per size (header + slice, or the bare slice of an overflow)
         if self._slice is None:
@@ -321,6 +336,7 @@ class ShardResult:
     jp_sweeps: int = 0
     exchanges: int = 0
     dense_exchanges: int = 0
+    hub_halts: int = 0  # checked finishes that found the asynchronous hub JP unfinished (some rank)
 
     @property
     def rounds(self):
@@ -332,7 +348,8 @@ class ShardResult:
 
 
 K8_BIG = 62  # candidates >= 62 do not fit the 6-bit proposal byte (gc_internal.h)
-HDR = 4      # header words carried in front of every seam's payload
+HDR = 5      # header words carried in front of every seam's payload (GC_SEAM_HDR)
+H_SWEEPS = 5  # halt code of a checked finish whose hub JP had not converged (GC_H_SWEEPS)
 
 
 def _hdr_words(vals):
@@ -348,7 +365,7 @@ def _hdr_values(words):
 
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
-                want_colors=True, inline=4096):
+                want_colors=True, inline=4096, deferred=True, hub_budget=3):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
@@ -361,7 +378,15 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     between two exchanges of the sweep seam (more than one pays where neighbours are
     mostly rank-local, e.g. meshes cut into slabs).  A round whose seams all moved deltas
     ends from the received IN states (O(winners)), otherwise from a scan of the proposal
-    bytes.  ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them)."""
+    bytes.  ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them).
+
+    With replicated hubs and an ``ops`` that has ``finish_async`` (``HipShard``), the hub
+    JP and the round's end are only enqueued: the winners' count comes back in word 4 of
+    the next propose seam's header, so a round costs the host one wait per seam and none
+    for the hubs or the commit.  A finish that found the hub JP unfinished halts on every
+    rank alike (word 4 < 0): the rest of the hub sweeps run, the finish is enqueued again
+    and the propose seam repeated.  ``deferred=False`` keeps the host-paced hub JP and
+    finish; ``hub_budget`` is the first round's full-grid hub sweeps (then adapted)."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -399,7 +424,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
 
     def finish_deltas(kind, hdr, recv, r, dense_ok):
         """after a delta seam: apply, or move what did not fit inline.  -> dense?"""
-        maxc = int(hdr[:, -1].max())
+        maxc = int(hdr[:, 3].max())
         if maxc > C and dense_ok and slice_for(maxc):
             res.exchanges += 1
             res.dense_exchanges += 1
@@ -410,20 +435,53 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
         ops.apply(kind, recv, int(recv.numel()), r)
         if maxc > C:
             res.exchanges += 1
-            own = int(hdr[comm.rank, -1])
+            own = int(hdr[comm.rank, 3])
             rest = comm.gather_deltas(ops.delta[C:], max(own - C, 0), maxc - C)
             ops.apply(kind, rest, int(rest.numel()), r)
         return False
 
     max_rounds = 4 * ops.n + 16
+    deferred = deferred and repl and hasattr(ops, "finish_async")
+    pending = None  # (round, U, F, maxmex, from_deltas) of a round whose finish is enqueued
+    acc_known = None  # its winners, from a rank whose finish completed (when another halted)
+    hub_grid, calm = max(int(hub_budget), 1), 0  # full-grid hub sweeps before the tail; rounds without a halt
     r = 0
     while True:
-        if U == 0:  # coloring.py:86-90
+        if U == 0 and pending is None:  # coloring.py:86-90
             rec(0, 0, -1, 0, 0)
             break
         if r > max_rounds:
             raise RuntimeError("round limit exceeded")
         hdr, recv = gather(ops.propose_seam(r, C))
+        if pending is not None:
+            st = hdr[:, 4]
+            if int(st.min()) < 0:
+                # Some rank's finish found its hub JP unfinished (the ranks list their hubs in
+                # different orders, so a sweep budget can suffice on one rank and not on
+                # another): those ranks run the rest and finish; every rank repeats the
+                # (idempotent) propose seam.  A finished rank's header holds the winners.
+                assert set(int(x) for x in st[st < 0]) == {-H_SWEEPS}, f"unexpected halt codes {st}"
+                if (st >= 0).any():
+                    acc_known = int(st[st >= 0][0])
+                if int(st[comm.rank]) < 0:
+                    res.jp_sweeps += ops.resume_hubs()
+                    ops.finish_async(pending[0], pending[4], check=True)
+                hub_grid = min(hub_grid + 1, 8)
+                calm = 0
+                res.hub_halts += 1
+                continue  # the propose seam again, after the finish
+            acc = acc_known if acc_known is not None else int(st[0])
+            acc_known = None
+            calm += 1
+            if calm >= 32 and hub_grid > min(2, int(hub_budget)):  # the budget has sufficed a while: trim it
+                hub_grid -= 1
+                calm = 0
+            rec(pending[1], pending[2], pending[3], acc, 0)
+            U -= acc
+            pending = None
+            if U == 0:
+                rec(0, 0, -1, 0, 0)
+                break
         F, maxmex, fails = int(hdr[:, 0].sum()), int(hdr[:, 1].max()), int(hdr[:, 2].sum())
         if F == 0:  # no proposer anywhere: the reference spins (coloring.py:93-95) -> E1
             if not e1:
@@ -444,7 +502,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
         finish_deltas(KIND_CAND, hdr, recv, r, maxmex < K8_BIG)
         # JP sweeps; a rank decides at most what it has left, so the seam's form is known
         # before the sweep runs (and a slice seam writes no deltas)
-        i, left, any_dense = 0, int(hdr[:, 0].max()), False
+        i, left, any_dense, hubs_async = 0, int(hdr[:, 0].max()), False, False
         while True:
             sl = slice_for(left)
             cnt = local_sweeps if i else 1
@@ -459,13 +517,21 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
                 break
             if repl and int(hdr[:, 2].sum()) == 0:
                 # every rank's lights are decided: each rank runs the hubs' sweeps alike
-                res.jp_sweeps += ops.start_hubs(i, any_dense)
+                if deferred:
+                    res.jp_sweeps += ops.start_hubs_async(i, any_dense, hub_grid)
+                    hubs_async = True
+                else:
+                    res.jp_sweeps += ops.start_hubs(i, any_dense)
                 break
             left = int(hdr[:, 0].max())
             res.jp_sweeps += 1
-        acc, _ = ops.finish(r, not any_dense)
-        rec(U, F, maxmex, acc, 0)
-        U -= acc
+        if deferred:
+            ops.finish_async(r, not any_dense, check=hubs_async)
+            pending = (r, U, F, maxmex, not any_dense)
+        else:
+            acc, _ = ops.finish(r, not any_dense)
+            rec(U, F, maxmex, acc, 0)
+            U -= acc
         r += 1
     res.colors, res.colored_round = ops.colors(track_rounds, want_colors)
     return res

@@ -166,9 +166,11 @@ int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count
    header, written on the device by gc_shard_pack                                        */
 int gc_shard_propose_async(gc_shard* s, int64_t round, int64_t* delta, int64_t cap);
 int gc_shard_sweep_async(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_t cap);
-/* a seam's send buffer (device, 4 + cap int64): 4 header words -- propose: frontier, max
-   candidate, #candidates >= k, #deltas; sweep: undecided in list slot `slot` (+ hubs
-   waiting for gc_shard_start_hubs), #deltas, undecided light vertices, #deltas -- each encoded (0xFFFFFFFF << 32 | value) so appliers skip it as padding, then
+/* a seam's send buffer (device, 5 + cap int64): 5 header words -- propose: frontier, max
+   candidate, #candidates >= k, #deltas, winners of the last finished round (or -halt code
+   when that finish halted: gc_shard_resume_hubs); sweep: undecided in list slot `slot`
+   (+ hubs waiting for gc_shard_start_hubs), #deltas, undecided light vertices, #deltas,
+   0 -- each encoded (0xFFFFFFFF << 32 | value) so appliers skip it as padding, then
    up to cap deltas padded with -1 (delta == NULL: the header only)                      */
 int gc_shard_pack(gc_shard* s, int32_t kind, int32_t slot, const int64_t* delta, int64_t* send, int64_t cap);
 /* sweeps i .. i+count-1 (i = 0: first sweep over the frontier, then over the undecided);
@@ -183,6 +185,13 @@ int gc_shard_sweep(gc_shard* s, int32_t i, int32_t count, int64_t* delta, int64_
    light states this round); *sweeps_out = sweeps run.                                  */
 int gc_shard_hub_count(gc_shard* s, int64_t* nhub);
 int gc_shard_start_hubs(gc_shard* s, int32_t i, int32_t from_slices, int64_t* sweeps_out);
+/* The same, only enqueued: `grid` full-grid hub sweeps from i, then the one-workgroup tail
+   (no host wait); gc_shard_finish_async(check = 1) verifies on the device that the hub JP
+   converged, else the round halts and the next propose seam's header word 4 reads
+   -GC_H_SWEEPS (5) on every rank: gc_shard_resume_hubs runs the rest, then the caller
+   enqueues the finish again and repeats the propose seam.                              */
+int gc_shard_start_hubs_async(gc_shard* s, int32_t i, int32_t from_slices, int32_t grid);
+int gc_shard_resume_hubs(gc_shard* s, int64_t* sweeps_out);
 /* slice seam: the rank's slice [lo, hi) of the proposal bytes (cand6 << 2 | JP state)
    into dst (device, hi - lo bytes); put_slices copies the other ranks' slices back    */
 int gc_shard_get_slice(gc_shard* s, uint8_t* dst);
@@ -193,6 +202,9 @@ int gc_shard_put_slices(gc_shard* s, const uint8_t* src, int64_t stride, const i
    bytes -- push them into the rank's in-neighbours; *acc_out = winners (global), *F_out =
    new frontier                                                                         */
 int gc_shard_finish(gc_shard* s, int64_t round, int32_t from_deltas, int64_t* acc_out, int64_t* F_out);
+/* the same, only enqueued (no wait): the winners' count arrives in the next propose seam's
+   header (word 4); check = 1 after gc_shard_start_hubs_async                            */
+int gc_shard_finish_async(gc_shard* s, int64_t round, int32_t from_deltas, int32_t check);
 /* run the shard's kernels on the caller's stream (a hipStream_t, e.g. torch's current one,
    where the collectives run): apply / get_slice / put_slices then only enqueue          */
 int gc_shard_set_stream(gc_shard* s, void* stream);

@@ -94,24 +94,25 @@ class NumpyShard:
         return [((0xFFFFFFFF << 32) | (int(x) & 0xFFFFFFFF)) - (1 << 64) for x in vals]
 
     def _pack(self, vals, cnt, C):
-        send = torch.full((4 + C,), -1, dtype=torch.int64)
-        send[:4] = torch.tensor(self._words(vals), dtype=torch.int64)
+        H = len(vals)
+        send = torch.full((H + C,), -1, dtype=torch.int64)
+        send[:H] = torch.tensor(self._words(vals), dtype=torch.int64)
         k = min(cnt, C)
         if k:
-            send[4:4 + k] = self.delta[:k]
+            send[H:H + k] = self.delta[:k]
         return send
 
     def propose_seam(self, r, C):
         cnt, f, mm, fails = self.propose(r)
-        return self._pack([f, mm, fails, cnt], cnt, C)
+        return self._pack([f, mm, fails, cnt, 0], cnt, C)
 
     def sweep_seam(self, i, count, C, emit, stride):
         cnt, und = self.sweep(i, count, emit)
         if emit:
-            return self._pack([und, cnt, 0, cnt], cnt, C)
-        buf = torch.zeros(32 + stride, dtype=torch.uint8)
-        buf[:32] = torch.tensor(self._words([und, 0, 0, 0]), dtype=torch.int64).view(torch.uint8)
-        self.get_slice(buf[32:])
+            return self._pack([und, cnt, 0, cnt, 0], cnt, C)
+        buf = torch.zeros(40 + stride, dtype=torch.uint8)
+        buf[:40] = torch.tensor(self._words([und, 0, 0, 0, 0]), dtype=torch.int64).view(torch.uint8)
+        self.get_slice(buf[40:])
         return buf
 
     def apply(self, kind, recv, tot, r):

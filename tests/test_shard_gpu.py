@@ -134,6 +134,16 @@ def test_replicated_hubs_sharded(seed, monkeypatch):
     with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
         r, one = same_as_single(dg, 3)
         assert r.reseeds == one.reseeds
+    # the asynchronous hub JP with no tail and one full-grid sweep: most checked finishes
+    # halt (on some ranks, not others) and resume; and the host-paced hub JP
+    monkeypatch.setenv("GC_HUB_T", "8")
+    monkeypatch.setenv("GC_SHARD_TAIL_HMAX", "0")
+    rp, col = _random_directed(3000, 15000, seed)
+    with DeviceGraph.from_csr(rp, col) as dg:
+        r, _ = same_as_single(dg, 3, hub_budget=1)
+        assert r.hub_halts > 0
+        same_as_single(dg, 2, deferred=False)
+    monkeypatch.delenv("GC_SHARD_TAIL_HMAX")
     monkeypatch.setenv("GC_SHARD_HUBS", "0")
     with DeviceGraph.rmat(12, 16, seed=seed) as dg:
         probe = sh.HipShard(dg, 0, dg.n)
