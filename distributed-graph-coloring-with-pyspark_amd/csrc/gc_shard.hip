@@ -162,7 +162,7 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
         delete sh;
         return GC_ENOMEM;
     }
-    int rc = gc_build_in_csr(&v, lo, hi);
+    int rc = (g->flags & GC_GRAPH_SYMMETRIC) ? gc_build_in_csr_sym(&v, lo, hi) : gc_build_in_csr(&v, lo, hi);
     if (!rc) rc = gc_alloc_run_state(&v);
     if (!rc) {  // hub lists on the parent (once), a bitmap replica (+ hub JP state) for this shard
         GDev pd = gc_view(g);
