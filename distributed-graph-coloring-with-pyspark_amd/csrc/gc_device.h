@@ -151,10 +151,22 @@ __device__ __forceinline__ bool gc_hub_gate(const GDev& g, const DevCtl* c, long
 
 // Algorithmic-byte counters (stats only): a workgroup adds into slot blockIdx % GC_STAT_SLOTS
 // instead of every workgroup hitting the same two DevCtl words; k_stat_reduce sums them.
+#ifndef GC_STAT_WAVE
+#define GC_STAT_WAVE 1  // measured: R-MAT-24 226 vs 228 ms with the per-workgroup reduction
+#endif
 template <int NW = GC_WAVES_PER_BLOCK>
 __device__ __forceinline__ void gc_stat_add(const GDev& g, int cls, ull lsum, ull lnv, ull* lds_scratch) {
     lsum = gc_wave_sum(lsum);
     lnv = gc_wave_sum(lnv);
+#if GC_STAT_WAVE  // each wave adds its own sums (no workgroup barriers at the kernel's end)
+    (void)lds_scratch;
+    if (gc_lane() == 0) {
+        ull* slot = g.bstat + ((blockIdx.x * NW + threadIdx.x / GC_WAVE) % GC_STAT_SLOTS) * 16;
+        if (lsum) atomicAdd(slot + cls, lsum);
+        if (lnv) atomicAdd(slot + 8 + cls, lnv);
+    }
+    return;
+#endif
     const int w = threadIdx.x / GC_WAVE;
     if (gc_lane() == 0) {
         lds_scratch[w] = lsum;

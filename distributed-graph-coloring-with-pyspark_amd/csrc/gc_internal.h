@@ -51,6 +51,10 @@ typedef unsigned long long ull;
 #define GC_LOOP_MAX 65536 // ... and over at most this many light vertices in k_sweep_loop
 #define GC_LOOP_HMAX 16384 //   (hubs)
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
+#ifndef GC_SWEEP_STATS
+#define GC_SWEEP_STATS 0  // sumdeg / nvert counters of the JP sweeps (no §8d credit, diagnostics only):
+                          // their end-of-kernel reduction cost R-MAT-24 236 -> 228 ms
+#endif
 #ifndef GC_TAIL_WAVES
 #define GC_TAIL_WAVES 4   // waves of k_sweep_tail's one workgroup (4, 8 or 16; GDev.tail_nw)
 #endif

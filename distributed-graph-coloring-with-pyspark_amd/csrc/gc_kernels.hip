@@ -1149,8 +1149,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     ull lsum = 0, lnv = 0;
     gc_jp_sweep(g, L.undL[in], cl, 0, hl, ch, L.undL[out], &c->und_cnt[out], L.undH[out],
                 &c->undh_cnt[out], lsum, lnv, L.delta, &c->dcnt, hub_start && g.hprep);
+#if GC_SWEEP_STATS  // the sweeps carry no §8d credit (their counts are only diagnostics)
     __syncthreads();
     gc_stat_add(g, GC_K_SWEEP, lsum, lnv, scratch);
+#endif
 }
 
 // Grid barrier of k_sweep_loop (cdna_hip_programming.md §6 G16): every wave drains its
@@ -1274,7 +1276,9 @@ __global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, i
         __syncthreads();
     }
     if (threadIdx.x == 0) gc_st(&c->tail_last, (long long)j);
+#if GC_SWEEP_STATS
     gc_stat_add<NW>(g, GC_K_SWEEP, lsum, lnv, scratch);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
