@@ -1088,7 +1088,11 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
                 });
         }
     }
-    gc_stage_flush_block<NW>(st, uo, uo_cnt);
+#ifndef GC_WAVE_FLUSH_MAX
+#define GC_WAVE_FLUSH_MAX 0
+#endif
+    if (cnt <= GC_WAVE_FLUSH_MAX) gc_stage_flush(st, uo, uo_cnt);  // short lists: few waves append, no barriers
+    else gc_stage_flush_block<NW>(st, uo, uo_cnt);
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
