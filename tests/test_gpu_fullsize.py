@@ -10,6 +10,8 @@
   mesh), 1531 rounds (3 * (512 - 2) + 1, the last one empty), bit-exact
   against the multi-core restatement.
 * north star (R-MAT scale 26): valid, rounds / colours pinned.
+* C5's graph on one GPU (R-MAT scale 28, past 2^32 adjacency entries): valid, pinned; and
+  R-MAT-27 (the 8-GPU weak-scaling graph) as one shard against the engine.
 """
 import os
 import sys
@@ -96,3 +98,30 @@ def test_north_star_rmat26_valid():
         g = dg.color("A", want_rounds=False, want_colors=False)
         assert dg.validate() == (0, 0)
         assert (g.rounds, g.max_color + 1) == (1355, 1350)
+
+
+def test_c5_rmat28_on_one_gpu_valid():
+    """C5's graph (R-MAT scale 28, ~8.5e9 adjacency entries, past int32 edge offsets) held
+    by ONE MI355X: valid, rounds / colours pinned."""
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(28, 16, seed=1) as dg:
+        assert dg.nnz > 1 << 32
+        g = dg.color("A", want_rounds=False, want_colors=False)
+        assert dg.validate() == (0, 0)
+        assert (g.rounds, g.max_color + 1) == (2052, 2047)
+
+
+def test_rmat27_one_shard_matches_engine():
+    """The weak-scaling bench colours R-MAT-27 (4.2e9 entries) at 8 GPUs: one shard of it
+    (the whole vertex range, replicated hubs, enqueued hub JP and finish) is the engine's
+    colouring, round for round."""
+    from gcolor_amd import shard as sh
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(27, 16, seed=1) as dg:
+        one = dg.color("A", want_rounds=True)
+        assert (one.rounds, one.max_color + 1) == (1667, 1663)
+        ops = sh.HipShard(dg, 0, dg.n)
+        res = sh.shard_color(ops, sh.ThreadTransport(sh.ThreadHub(1), 0))
+        ops.close()
+        assert np.array_equal(res.colors, one.colors)
+        assert list(res.round_U) == list(one.round_U) and list(res.round_accepted) == list(one.round_accepted)
