@@ -78,6 +78,8 @@ typedef unsigned long long ull;
 #define GC_H_RESEED 4   // zero proposers with uncoloured vertices left: host runs E1
 #define GC_H_SWEEPS 5   // JP not finished after the enqueued sweeps: host adds sweeps
 #define GC_H_ROUNDCAP 6 // per-round record buffer full
+#define GC_H_SEAM 7     // shards: a fused propose seam was not applied (a rank halted, or its deltas overflowed)
+#define GC_SEAM_HDR 5   // header words in front of a shard seam's payload (k_shard_pack)
 
 // commit modes (bookkeeping done by the last workgroup)
 #define GC_CM_ROUND 0

@@ -1993,8 +1993,26 @@ __global__ void __launch_bounds__(GC_BLOCK) k_delta_cand(GDev g, GLists L) {
 // them).  Entries with v < 0 are padding (and the exchange headers, gcolor_amd/shard.py).
 // rwin != null: IN states -- other ranks' winners of the round -- are also listed there, so
 // the round's end colours them from the list instead of scanning every proposal byte.
+// hdr_stride > 0 (a fused propose seam, shard.py): recv is every rank's send buffer of
+// hdr_stride words (GC_SEAM_HDR header words + inline deltas); if some rank's finish halted
+// (word 4 < 0) or its deltas did not fit inline (word 3 > hdr_stride - GC_SEAM_HDR), nothing
+// is applied and the shard halts with GC_H_SEAM (the host takes the unfused path).
+__device__ __forceinline__ int gc_hdr_value(long long w) { return (int)(unsigned)(w & 0xFFFFFFFFll); }
 __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long long* recv, long long count,
-                                                    long long lo, long long hi, int round, int* rwin) {
+                                                    long long lo, long long hi, int round, int* rwin,
+                                                    long long hdr_stride) {
+    if (g.ctl->halt) return;
+    if (hdr_stride > 0) {
+        bool bad = false;
+        for (long long p = 0; p * hdr_stride < count; ++p) {
+            const long long* h = recv + p * hdr_stride;
+            bad |= gc_hdr_value(h[4]) < 0 || (long long)gc_hdr_value(h[3]) > hdr_stride - GC_SEAM_HDR;
+        }
+        if (bad) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->halt = GC_H_SEAM;
+            return;
+        }
+    }
     const bool want_cround = g.ctl->want_cround != 0;
     const int lane = gc_lane();
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -2182,7 +2200,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
 //                      winners of the last finished round (-halt code when it halted)
 //   kind GC_KIND_STATE (sweep seam):   undecided (lists of slot `slot`), #deltas, undecided lights, #deltas, 0
 // With delta == null only the header is written (the slice seams).
-#define GC_SEAM_HDR 5
 __device__ __forceinline__ long long gc_hdr_word(long long x) {
     return (long long)((0xFFFFFFFFull << 32) | (ull)(unsigned)x);
 }
@@ -2658,9 +2675,16 @@ void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
-               int* rwin, hipStream_t s) {
+               int* rwin, hipStream_t s, long long hdr_stride) {
     if (count <= 0) return;
-    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round, rwin);
+    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round, rwin,
+                       hdr_stride);
+}
+__global__ void k_shard_clear_halt(GDev g, int code) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g.ctl->halt == code) g.ctl->halt = GC_RUN;
+}
+void gcl_shard_clear_halt(const GDev& g, int code, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_clear_halt, dim3(1), dim3(64), 0, s, g, code);
 }
 void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, int* big, hipStream_t s) {
     hipLaunchKernelGGL(k_shard_list_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, rwin, big);

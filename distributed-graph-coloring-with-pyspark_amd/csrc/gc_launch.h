@@ -110,7 +110,8 @@ void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allo
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s);  // see gc_hub_push_wave
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
-               int* rwin, hipStream_t s);
+               int* rwin, hipStream_t s, long long hdr_stride = 0);
+void gcl_shard_clear_halt(const GDev& g, int code, hipStream_t s);  // halt := GC_RUN if it is `code`
 // big: winners whose hub lists are left to gcl_hub_push_big (counter DevCtl.list_cnt)
 void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, int* big, hipStream_t s);
 void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, int* big, hipStream_t s);

@@ -343,6 +343,29 @@ extern "C" int gc_shard_apply(gc_shard* sh, int32_t kind, const int64_t* recv, i
     return GC_OK;
 }
 
+// A fused propose seam's apply (the first JP sweep is enqueued behind it before the host has
+// read any header): applied only if every rank's header allows it, else the shard halts with
+// GC_H_SEAM, so the sweep behind it does nothing; gc_shard_clear_halt(GC_H_SEAM) undoes it.
+extern "C" int gc_shard_apply_checked(gc_shard* sh, int32_t kind, const int64_t* recv, int64_t count, int64_t round,
+                                      int64_t hdr_stride) {
+    if (!sh || hdr_stride <= GC_SEAM_HDR || (count > 0 && !recv)) { gc_set_error("bad argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    gcl_apply(shard_view(sh), kind, reinterpret_cast<const long long*>(recv), count, sh->lo, sh->hi, (int)round + 1,
+              kind == GC_KIND_STATE ? g->parent : nullptr, g->stream, hdr_stride);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+extern "C" int gc_shard_clear_halt(gc_shard* sh, int32_t code) {
+    if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    gcl_shard_clear_halt(shard_view(sh), code, g->stream);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
 // JP sweeps i, i+1, ..., i+count-1 over the rank's lists (i = 0 is the first sweep over
 // the frontier; later sweeps run over the undecided); the rank's later sweeps can decide
 // vertices whose lower-rank neighbours are its own, so several run between two

@@ -34,6 +34,7 @@ EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", 
            "gc_shard_propose_async", "gc_shard_sweep_async", "gc_shard_pack",
            "gc_shard_get_slice", "gc_shard_put_slices", "gc_shard_hub_count", "gc_shard_start_hubs",
            "gc_shard_start_hubs_async", "gc_shard_resume_hubs", "gc_shard_finish_async",
+           "gc_shard_apply_checked", "gc_shard_clear_halt",
            "gc_json_read_graph", "gc_json_write_coloring", "gc_json_write_graph", "gc_csr_write", "gc_csr_read",
            "gc_csr_free"]
 
@@ -125,6 +126,8 @@ def load():
         "gc_shard_start_hubs_async": ([P, I32, I32, I32], ctypes.c_int),
         "gc_shard_resume_hubs": ([P, _I64P], ctypes.c_int),
         "gc_shard_finish_async": ([P, I64, I32, I32], ctypes.c_int),
+        "gc_shard_apply_checked": ([P, I32, P, I64, I64, I64], ctypes.c_int),
+        "gc_shard_clear_halt": ([P, I32], ctypes.c_int),
         "gc_json_read_graph": ([ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(GcCsr))], ctypes.c_int),
         "gc_json_write_coloring": ([ctypes.c_char_p, P, P, I64], ctypes.c_int),
         "gc_json_write_graph": ([ctypes.c_char_p, P, P, P, I64, P], ctypes.c_int),

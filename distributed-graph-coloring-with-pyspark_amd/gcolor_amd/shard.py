@@ -275,6 +275,13 @@ class HipShard:
         nat.check("gc_shard_resume_hubs", self._lib.gc_shard_resume_hubs(self._h, self._ct.byref(self._a)))
         return self._a.value
 
+    def apply_checked(self, kind, recv, r, hdr_stride):
+        nat.check("gc_shard_apply_checked", self._lib.gc_shard_apply_checked(self._h, kind, _p(recv), int(recv.numel()),
+                                                                             r, int(hdr_stride)))
+
+    def clear_halt(self, code):
+        nat.check("gc_shard_clear_halt", self._lib.gc_shard_clear_halt(self._h, int(code)))
+
     def finish_async(self, r, from_deltas=False, check=False):
         nat.check("gc_shard_finish_async", self._lib.gc_shard_finish_async(self._h, r, 1 if from_deltas else 0,
                                                                            1 if check else 0))
@@ -337,6 +344,7 @@ class ShardResult:
     exchanges: int = 0
     dense_exchanges: int = 0
     hub_halts: int = 0  # checked finishes that found the asynchronous hub JP unfinished (some rank)
+    fused_misses: int = 0  # fused propose seams that could not be applied (the unfused path followed)
 
     @property
     def rounds(self):
@@ -350,6 +358,7 @@ class ShardResult:
 K8_BIG = 62  # candidates >= 62 do not fit the 6-bit proposal byte (gc_internal.h)
 HDR = 5      # header words carried in front of every seam's payload (GC_SEAM_HDR)
 H_SWEEPS = 5  # halt code of a checked finish whose hub JP had not converged (GC_H_SWEEPS)
+H_SEAM = 7    # halt code of a fused propose seam that could not be applied (GC_H_SEAM)
 
 
 def _hdr_words(vals):
@@ -365,7 +374,7 @@ def _hdr_values(words):
 
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
-                want_colors=True, inline=4096, deferred=True, hub_budget=3):
+                want_colors=True, inline=4096, deferred=True, hub_budget=3, fuse=True):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
@@ -380,13 +389,19 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     ends from the received IN states (O(winners)), otherwise from a scan of the proposal
     bytes.  ``want_colors=False`` leaves the colours in HBM (``ops.colors`` fetches them).
 
-    With replicated hubs and an ``ops`` that has ``finish_async`` (``HipShard``), the hub
-    JP and the round's end are only enqueued: the winners' count comes back in word 4 of
+    With an ``ops`` that has ``finish_async`` (``HipShard``), the round's end (and with
+    replicated hubs their JP) is only enqueued: the winners' count comes back in word 4 of
     the next propose seam's header, so a round costs the host one wait per seam and none
     for the hubs or the commit.  A finish that found the hub JP unfinished halts on every
     rank alike (word 4 < 0): the rest of the hub sweeps run, the finish is enqueued again
     and the propose seam repeated.  ``deferred=False`` keeps the host-paced hub JP and
-    finish; ``hub_budget`` is the first round's full-grid hub sweeps (then adapted)."""
+    finish; ``hub_budget`` is the first round's full-grid hub sweeps (then adapted).
+
+    ``fuse``: when the last round's frontiers fit the inline deltas, the propose seam's
+    all-gather, its apply and the first JP sweep seam are enqueued together, with ONE host
+    wait for both headers.  The apply checks every rank's header on the device and, when
+    some rank halted or overflowed, applies nothing and halts the shard (GC_H_SEAM), so the
+    sweep behind it does nothing; the host clears that halt and takes the unfused path."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -441,10 +456,12 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
         return False
 
     max_rounds = 4 * ops.n + 16
-    deferred = deferred and repl and hasattr(ops, "finish_async")
+    deferred = deferred and hasattr(ops, "finish_async")
     pending = None  # (round, U, F, maxmex, from_deltas) of a round whose finish is enqueued
     acc_known = None  # its winners, from a rank whose finish completed (when another halted)
     hub_grid, calm = max(int(hub_budget), 1), 0  # full-grid hub sweeps before the tail; rounds without a halt
+    fuse_on = fuse and deferred and dense is not True and C > 0
+    last_fmax = None  # largest per-rank frontier of the last propose seam (does the next one fit inline?)
     r = 0
     while True:
         if U == 0 and pending is None:  # coloring.py:86-90
@@ -452,7 +469,20 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             break
         if r > max_rounds:
             raise RuntimeError("round limit exceeded")
-        hdr, recv = gather(ops.propose_seam(r, C))
+        fused = fuse_on and last_fmax is not None and last_fmax <= C
+        pre = None  # the first sweep seam's (headers, received), when fused with the propose seam
+        if fused:
+            res.exchanges += 1
+            recv = comm.allgather(ops.propose_seam(r, C))
+            ops.apply_checked(KIND_CAND, recv, r, HDR + C)
+            pre = gather(ops.sweep_seam(0, 1, C, True, stride))  # the one host wait
+            hdr = _hdr_values(recv.view(P, -1)[:, :HDR].cpu().numpy())
+            if int(hdr[:, 4].min()) < 0 or int(hdr[:, 3].max()) > C:  # not applied anywhere
+                ops.clear_halt(H_SEAM)  # (a rank halted by its finish keeps that halt)
+                pre = None
+                res.fused_misses += 1
+        else:
+            hdr, recv = gather(ops.propose_seam(r, C))
         if pending is not None:
             st = hdr[:, 4]
             if int(st.min()) < 0:
@@ -483,6 +513,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
                 rec(0, 0, -1, 0, 0)
                 break
         F, maxmex, fails = int(hdr[:, 0].sum()), int(hdr[:, 1].max()), int(hdr[:, 2].sum())
+        last_fmax = int(hdr[:, 0].max())
         if F == 0:  # no proposer anywhere: the reference spins (coloring.py:93-95) -> E1
             if not e1:
                 rec(U, 0, -1, 0, 0)
@@ -499,14 +530,19 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             res.status, res.fail_round, res.fail_count = FAILED, r, fails
             break
         # candidates >= 62 live in cand[], outside the proposal bytes: deltas only
-        finish_deltas(KIND_CAND, hdr, recv, r, maxmex < K8_BIG)
+        if pre is None:  # (a fused seam was applied on the device)
+            finish_deltas(KIND_CAND, hdr, recv, r, maxmex < K8_BIG)
         # JP sweeps; a rank decides at most what it has left, so the seam's form is known
         # before the sweep runs (and a slice seam writes no deltas)
         i, left, any_dense, hubs_async = 0, int(hdr[:, 0].max()), False, False
         while True:
-            sl = slice_for(left)
-            cnt = local_sweeps if i else 1
-            hdr, recv = gather(ops.sweep_seam(i, cnt, C, not sl, stride))
+            if pre is not None:  # the first sweep seam ran fused with the propose seam
+                sl, cnt = False, 1
+                (hdr, recv), pre = pre, None
+            else:
+                sl = slice_for(left)
+                cnt = local_sweeps if i else 1
+                hdr, recv = gather(ops.sweep_seam(i, cnt, C, not sl, stride))
             i += cnt
             if sl:
                 ops.put_slices(recv[hdr_bytes:], hdr_bytes + stride, starts, lens)

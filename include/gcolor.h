@@ -162,6 +162,14 @@ int gc_shard_begin(gc_shard* s, int64_t num_colors, int32_t track_rounds, int64_
 /* stats[4]: deltas written, frontier size, max candidate (-1 none), #candidates >= k    */
 int gc_shard_propose(gc_shard* s, int64_t round, int64_t* delta, int64_t cap, int64_t* stats);
 int gc_shard_apply(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round);  /* enqueued */
+/* Fused propose seam (the first JP sweep enqueued behind it, no host wait between): recv is
+   every rank's send buffer of hdr_stride words; nothing is applied and the shard halts
+   (GC_H_SEAM = 7: its kernels do nothing) when some rank's header shows a halted finish or
+   more deltas than fit inline -- the caller then clears it (gc_shard_clear_halt) and takes
+   the unfused path.                                                                       */
+int gc_shard_apply_checked(gc_shard* s, int32_t kind, const int64_t* recv, int64_t count, int64_t round,
+                           int64_t hdr_stride);
+int gc_shard_clear_halt(gc_shard* s, int32_t code);  /* halt := run if it is `code` (enqueued) */
 /* the same phases, only enqueued (no wait, no stats): their counts travel in the seam's
    header, written on the device by gc_shard_pack                                        */
 int gc_shard_propose_async(gc_shard* s, int64_t round, int64_t* delta, int64_t cap);

@@ -103,6 +103,7 @@ def test_uniform_and_mesh_sharded():
     with DeviceGraph.mesh(20, 16, 12) as dg:
         r, _ = same_as_single(dg, 3)
         assert r.max_color + 1 == 2
+        same_as_single(dg, 2, deferred=False)
 
 
 @pytest.mark.parametrize("seed", range(2))
@@ -143,6 +144,9 @@ def test_replicated_hubs_sharded(seed, monkeypatch):
         r, _ = same_as_single(dg, 3, hub_budget=1)
         assert r.hub_halts > 0
         same_as_single(dg, 2, deferred=False)
+        same_as_single(dg, 3, fuse=False)
+        r, _ = same_as_single(dg, 2, inline=64)  # fused propose seams that overflow: the unfused path
+        assert r.fused_misses > 0
     monkeypatch.delenv("GC_SHARD_TAIL_HMAX")
     monkeypatch.setenv("GC_SHARD_HUBS", "0")
     with DeviceGraph.rmat(12, 16, seed=seed) as dg:
