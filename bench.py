@@ -223,7 +223,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
             "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": desc, "n": dg.n, "m_undirected": m, "nnz": dg.nnz, "max_degree": dg.max_degree,
                        "variant": "A (coloring.py)",
-                       "parallelism": f"{world} vertex-range shards (balanced by deg+1), round seams over RCCL",
+                       "parallelism": f"{world} vertex-range shards (balanced by deg+1), round seams over "
+                                      f"{'RCCL' if comm.backend == 'nccl' else comm.backend}",
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
                        "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2)},
