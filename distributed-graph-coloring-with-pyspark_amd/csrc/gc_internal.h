@@ -40,7 +40,7 @@ typedef unsigned long long ull;
 #endif
 #define GC_HUB_NOT_STARTED (1ll << 40)
 #define GC_TAIL_HMAX_HUB 128
-#define GC_BIGROW 4096       // a winner with longer in-rows is walked by the whole grid (k_commit_big)  // tail sweeps may take this many hubs (their sweeps read short lists)
+#define GC_BIGROW 2048       // a winner with longer in-rows (+ hub pushes) is walked by the whole grid (k_commit_big); 4096 -> 2048: R-MAT-24 224 -> 217 ms
 // per-wave LDS staging capacity for list appends
 #define GC_STAGE_CAP 512
 // fixed grid of the device-predicated round kernels (grid-stride over device counts)

@@ -1343,8 +1343,14 @@ __device__ __forceinline__ void gc_precheck(const GLists& L, DevCtl* c, long lon
 // stores; the next kernel reads them after the launch boundary).
 // A fused commit (k_commit<1>) made the next round's proposals: their failure count and
 // max candidate move from the nx_ slots into place (else the nx_ slots hold 0 / -1).
-__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode, int fused) {
-    const long long acc = (long long)gc_aread(&c->accepted);
+// pre (gc_close_body): the counters it needs, read by separate lanes in one memory trip
+struct GcClosePre {
+    ull accepted, nx_failcnt, uncolored, fnext;
+    long long nx_maxmex;
+};
+__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode, int fused,
+                                                        const GcClosePre& pre) {
+    const long long acc = (long long)pre.accepted;
     long long U = c->U;
     int cur = c->cur;
     if (mode == GC_CM_ROUND) {
@@ -1363,7 +1369,7 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
         cur ^= 1;
         gc_st(&c->cur, cur);
     } else if (mode == GC_CM_INIT) {
-        U = (long long)gc_aread(&c->uncolored) - (c->seedkey ? 1 : 0);
+        U = (long long)pre.uncolored - (c->seedkey ? 1 : 0);
     } else {  // GC_CM_RESEED: the E1 round record (no proposers, `acc` seeds planted)
         gc_record(L, c, U, 0, -1, 0, acc, 0);
         U -= acc;
@@ -1371,9 +1377,9 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->U, U);
     gc_st(&c->heavy_cnt, 0ull);
     gc_st(&c->wide_cnt, 0ull);
-    gc_st(&c->failcnt, gc_aread(&c->nx_failcnt));
+    gc_st(&c->failcnt, pre.nx_failcnt);
     gc_st(&c->accepted, 0ull);
-    gc_st(&c->maxmex, (long long)gc_aread(reinterpret_cast<ull*>(&c->nx_maxmex)));
+    gc_st(&c->maxmex, pre.nx_maxmex);
     gc_st(&c->nx_failcnt, 0ull);
     gc_st(&c->nx_maxmex, -1ll);
     gc_st(&c->proposed, mode == GC_CM_ROUND && fused ? 1 : 0);
@@ -1388,19 +1394,34 @@ __device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl
     gc_st(&c->bigw_cnt, 0ull);
     gc_st(&c->use_c4, 0);  // k_pack_c4 (when the host enqueues it) turns it on for its round
     gc_st(&c->seed_cnt[1], 0ull);
-    gc_precheck(L, c, U, (long long)gc_aread(&c->fcnt[cur]));
+    gc_precheck(L, c, U, (long long)pre.fnext);
 }
 
 __device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big, int fused) {
-    if (g.accs && threadIdx.x < GC_WAVE) {  // the commit's slotted winner counts
-        ull a = 0;
-        for (int k = threadIdx.x; k < GC_ACC_SLOTS; k += GC_WAVE) a += atomicExch(&g.accs[k], 0ull);
-        a = gc_wave_sum(a);
-        if (threadIdx.x == 0 && a) atomicAdd(&c->accepted, a);
-    }
-    if (threadIdx.x == 0) {
+    if (threadIdx.x >= GC_WAVE) return;
+    const int lane = threadIdx.x;
+    ull a = 0;  // the commit's slotted winner counts
+    if (g.accs)
+        for (int k = lane; k < GC_ACC_SLOTS; k += GC_WAVE) a += atomicExch(&g.accs[k], 0ull);
+    a = gc_wave_sum(a);
+    // the counters the close reads, one lane each, in one memory trip (they were one
+    // returning atomic after another: ~1 us each on the round's critical path)
+    const int cur = c->cur;
+    ull x = 0;
+    if (lane == 1) x = gc_aread(&c->accepted);
+    else if (lane == 2) x = gc_aread(&c->nx_failcnt);
+    else if (lane == 3) x = gc_aread(reinterpret_cast<ull*>(&c->nx_maxmex));
+    else if (lane == 4) x = gc_aread(&c->uncolored);
+    else if (lane == 5) x = gc_aread(&c->fcnt[mode == GC_CM_ROUND ? cur ^ 1 : cur]);  // the next frontier
+    GcClosePre pre;
+    pre.accepted = (ull)__shfl((long long)x, 1, GC_WAVE) + a;
+    pre.nx_failcnt = (ull)__shfl((long long)x, 2, GC_WAVE);
+    pre.nx_maxmex = __shfl((long long)x, 3, GC_WAVE);
+    pre.uncolored = (ull)__shfl((long long)x, 4, GC_WAVE);
+    pre.fnext = (ull)__shfl((long long)x, 5, GC_WAVE);
+    if (lane == 0) {
         c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
-        gc_close_round(L, c, mode, fused);
+        gc_close_round(L, c, mode, fused, pre);
     }
 }
 
