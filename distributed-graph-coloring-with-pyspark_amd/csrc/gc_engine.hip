@@ -386,7 +386,7 @@ struct Run {
             kt.end();
         }
         kt.begin(GC_K_PROPOSE);
-        gcl_propose(d, L, s);
+        gcl_propose(d, L, s, resort_hint ? 0 : 1);
         kt.end();
         if (need_pblock()) {  // heavy (deg > heavy_t) or wide (mex >= 64, so deg >= 64) proposers possible
             kt.begin(GC_K_PROPOSE);

@@ -2654,6 +2654,9 @@ static int round_grid(const char* env, int dflt) {
     return v > 0 ? v : dflt;
 }
 static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
+// k_propose when the last snapshot's frontier was small (< n/256): 512 workgroups (R-MAT-24
+// 216 -> 210 ms with the later sweeps on 256; the full grid stays for C2's big rounds)
+static const int kGridPS = round_grid("GC_GRID_PS", 512);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
 static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
 static const int kGridPB = round_grid("GC_GRID_PB", GC_BLOCK_GRID);  // k_propose_block
@@ -2661,7 +2664,7 @@ static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit
 // the later JP sweeps: mostly short lists, where 1024 workgroups' start-up and end-of-kernel
 // reductions outweigh their reach (R-MAT-24 257 -> 238 ms, R-MAT-26 562 -> 521 ms at 384;
 // 256 within 1%; C2 and the mesh unchanged)
-static const int kGridS = round_grid("GC_GRID_S", 384);
+static const int kGridS = round_grid("GC_GRID_S", 256);
 
 // per-slot stats -> DevCtl.sumdeg / nvert (one workgroup; before the host reads them)
 __global__ void k_stat_reduce(GDev g) {
@@ -2680,8 +2683,8 @@ void gcl_stat_reduce(const GDev& g, hipStream_t s) {
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
 }
-void gcl_propose(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose, dim3(kGridP), dim3(GC_BLOCK), 0, s, g, L);
+void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small) {
+    hipLaunchKernelGGL(k_propose, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
