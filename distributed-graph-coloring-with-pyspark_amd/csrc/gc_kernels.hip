@@ -2665,6 +2665,9 @@ static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit
 // reductions outweigh their reach (R-MAT-24 257 -> 238 ms, R-MAT-26 562 -> 521 ms at 384;
 // 256 within 1%; C2 and the mesh unchanged)
 static const int kGridS = round_grid("GC_GRID_S", 256);
+// ... when heavy vertices are resolved a workgroup each (no hub JP: seeded ranks, hubs off):
+// seeded R-MAT-24 1520 ms on 256 workgroups, 1265 on 384, 938 on 1024
+static const int kGridSH = round_grid("GC_GRID_SH", 1024);
 
 // per-slot stats -> DevCtl.sumdeg / nvert (one workgroup; before the host reads them)
 __global__ void k_stat_reduce(GDev g) {
@@ -2693,7 +2696,7 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_resolve, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep, dim3(kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
+    hipLaunchKernelGGL(k_sweep, dim3(g.hub_w ? kGridS : kGridSH), dim3(GC_BLOCK), 0, s, g, L, i);
 }
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
