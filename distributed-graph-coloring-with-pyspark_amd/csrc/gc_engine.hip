@@ -82,6 +82,7 @@ GDev gc_view(const gc_graph* g) {
     d.tail_lmax = getenv("GC_TAIL_LMAX") ? atoi(getenv("GC_TAIL_LMAX")) : GC_TAIL_MAX;
     d.tail_nw = getenv("GC_TAIL_WAVES") ? atoi(getenv("GC_TAIL_WAVES")) : GC_TAIL_WAVES;
     d.tail_nw = d.tail_nw >= 16 ? 16 : (d.tail_nw >= 8 ? 8 : 4);
+    d.heavy_wg = 0;
     d.hch_rp = nullptr;
     d.hch_own = nullptr;
     d.hkcnt = nullptr;
@@ -630,6 +631,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         run.d.tail_hmax = GC_TAIL_HMAX;
     }
     if (run.d.hub_w == 0 && g->maxdeg > run.d.heavy_t) {
+        run.d.heavy_wg = 1;
         if ((rc = gc_alloc_heavy_pending(g))) return rc;
         run.d.hpl = g->hpl;
         run.d.hplc = g->hplc;

@@ -2668,6 +2668,8 @@ static const int kGridS = round_grid("GC_GRID_S", 256);
 // ... when heavy vertices are resolved a workgroup each (no hub JP: seeded ranks, hubs off):
 // seeded R-MAT-24 1520 ms on 256 workgroups, 1265 on 384, 938 on 1024
 static const int kGridSH = round_grid("GC_GRID_SH", 1024);
+// ... and the first sweep (k_resolve) then: seeded R-MAT-24 935 ms on 1024, 879 on 2048, 862 on 4096
+static const int kGridRH = round_grid("GC_GRID_RH", 4096);
 
 // per-slot stats -> DevCtl.sumdeg / nvert (one workgroup; before the host reads them)
 __global__ void k_stat_reduce(GDev g) {
@@ -2693,10 +2695,10 @@ void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve, dim3(kGridR), dim3(GC_BLOCK), 0, s, g, L);
+    hipLaunchKernelGGL(k_resolve, dim3(g.heavy_wg ? kGridRH : kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep, dim3(g.hub_w ? kGridS : kGridSH), dim3(GC_BLOCK), 0, s, g, L, i);
+    hipLaunchKernelGGL(k_sweep, dim3(g.heavy_wg ? kGridSH : kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
 }
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);

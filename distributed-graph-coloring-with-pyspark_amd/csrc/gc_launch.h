@@ -48,6 +48,8 @@ struct GDev {
     int tail_hmax;            // heavy entries the one-workgroup tail sweeps may take (GC_TAIL_HMAX[_HUB])
     int tail_lmax;            // light entries the tail sweeps may take (GC_TAIL_MAX; env GC_TAIL_LMAX)
     int tail_nw;              // waves of the tail's workgroup: 4, 8 or 16 (env GC_TAIL_WAVES)
+    int heavy_wg;             // heavy vertices are resolved a workgroup each (no hub JP, some deg > heavy_t):
+                              //   the JP sweeps run on the larger grids (GC_GRID_RH / GC_GRID_SH)
     long long hub_long;       // hub-start sweep: hubs whose hlow row exceeds this are first-read by the whole grid
     const long long* hch_rp;  // static GC_HCH-entry chunks of the hlow rows (hub x: [hch_rp[x], hch_rp[x+1]))
     const int* hch_own;       //   chunk -> hub
