@@ -215,6 +215,7 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
         assert unc == 0 and conf == 0, f"invalid colouring: {unc} uncoloured, {conf} conflicts"
         one = dg.color("A", want_rounds=False, want_colors=True)  # reference run (outside timing)
         assert np.array_equal(one.colors, res.colors), "sharded colouring differs from the 1-GPU engine"
+        t1 = min(dg.color("A", want_rounds=False, want_colors=False).device_ms for _ in range(2))  # the same graph on ONE GPU
         balg = one.balg_bytes + 20.0 * dg.n + 8.0 * dg.nnz
         achieved = balg / world / t / 1e9
         line = {
@@ -227,7 +228,9 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
                                       f"{'RCCL' if comm.backend == 'nccl' else comm.backend}",
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
-                       "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2)},
+                       "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2),
+                       # the same graph coloured by the single-GPU engine on rank 0's GPU (best of 2)
+                       "single_gpu_ms": round(t1, 2), "speedup_vs_single_gpu": round(t1 / (t * 1e3), 3)},
             "colors_used": res.max_color + 1,
             "roofline": {"bound": "hbm", "kernel": "whole colouring per GPU (sharded), §8d algorithmic bytes",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
