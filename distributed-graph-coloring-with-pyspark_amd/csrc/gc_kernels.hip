@@ -1135,7 +1135,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resolve(GDev g, GLists L) {
 __global__ void __launch_bounds__(GC_BLOCK) k_sweep(GDev g, GLists L, int i) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
+#if GC_SWEEP_STATS
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+#endif
     const int in = (i - 1) % 3, out = i % 3, z = (i + 1) % 3;
     const long long cl = (long long)c->und_cnt[in];
     long long ch = (long long)c->undh_cnt[in];
@@ -1250,7 +1252,9 @@ template <int NW>
 __global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, int S) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
+#if GC_SWEEP_STATS
     __shared__ ull scratch[2 * NW];
+#endif
     __shared__ long long s_cl, s_ch;
     int j = c->loop_last > S ? (int)c->loop_last : S;  // after k_sweep_loop's sweeps, if it ran
     ull lsum = 0, lnv = 0;
