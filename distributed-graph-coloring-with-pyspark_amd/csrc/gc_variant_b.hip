@@ -480,6 +480,12 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
+    // fold pass grids (env GC_GRID_BE / GC_GRID_BA: eviction / admission passes).  Heavy
+    // admissions take a workgroup each: with vertices that can be heavy, 2048 workgroups
+    // (R-MAT-24 891 -> 824 ms; 4096: 928, 512: 1134); C2 keeps 1024 (4096: 18.4 -> 22.0 ms)
+    const int grid_ev = getenv("GC_GRID_BE") && atoi(getenv("GC_GRID_BE")) > 0 ? atoi(getenv("GC_GRID_BE")) : GC_ROUND_GRID;
+    const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
+                         : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
     DevCtl& h = *g->hctl;
     memset(&h, 0, sizeof(DevCtl));
     h.kbound = opt->num_colors;
@@ -532,8 +538,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         auto enqueue_passes = [&](long long k) {
             for (long long j = 0; j < k; ++j, ++passes) {
                 const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
-                hipLaunchKernelGGL(k_b_ev, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
-                hipLaunchKernelGGL(k_b_adm, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
+                hipLaunchKernelGGL(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+                hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
         };
         enqueue_passes(std::max(2ll, std::min(prev_passes, 24ll)));
