@@ -68,9 +68,45 @@ __global__ void k_spec_reset(GDev g, long long round) {
 
 // one-shot resolution: v keeps its proposal iff no lower-rank listed entry (the nlow head
 // of its row) proposed the same colour; every uncoloured vertex proposes, and candidates
-// do not change during the pass, so the states written here never feed another decision
+// do not change during the pass, so the states written here never feed another decision.
+// Heavy proposers (the heavy list k_propose built: deg > heavy_t) take a workgroup each and
+// stop at their first same-candidate entry: a wave whose chunk held one walked its whole
+// lower-rank part alone, the pass's long pole on R-MAT.
 __global__ void __launch_bounds__(GC_BLOCK) k_spec_resolve(GDev g, GLists L) {
     DevCtl* c = g.ctl;
+    {
+        __shared__ unsigned s_hit;
+        const long long hcnt = (long long)c->heavy_cnt;
+        for (long long i = blockIdx.x; i < hcnt; i += gridDim.x) {
+            const int v = L.heavy[i];
+            const unsigned kv = g.k8[v];
+            const unsigned c6 = gc_k8_cand(kv);
+            const int cv = c6 == GC_K8_BIG ? g.cand[v] : (int)c6;
+            const long long start = g.rp[v];
+            const int dl = g.nlow[v];
+            if (threadIdx.x == 0) s_hit = 0u;
+            __syncthreads();
+            for (int e0 = 0; e0 < dl; e0 += GC_SLOTS * GC_BLOCK) {
+                unsigned hit = 0u;
+#pragma unroll
+                for (int k = 0; k < GC_SLOTS; ++k) {
+                    const int e = e0 + k * GC_BLOCK + (int)threadIdx.x;
+                    if (e < dl) {
+                        const int u = g.col[start + e];
+                        const unsigned ku = g.k8[u];
+                        if (gc_k8_cand(ku) == c6 && (c6 != GC_K8_BIG || g.cand[u] == cv)) hit = 1u;
+                    }
+                }
+                if (hit) s_hit = 1u;
+                __syncthreads();
+                const bool done = s_hit != 0u;
+                __syncthreads();
+                if (done) break;
+            }
+            if (threadIdx.x == 0) g.k8[v] = (unsigned char)((kv & ~3u) | (s_hit ? GC_JP_OUT : GC_JP_IN));
+            __syncthreads();
+        }
+    }
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -85,7 +121,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_spec_resolve(GDev g, GLists L) {
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long idx = ch * vpw + lane;
-        const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+        int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+        if (v >= 0 && g.deg[v] > g.heavy_t) v = -1;  // in the heavy list (above)
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0u;
         const unsigned c6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
         const int dl = v >= 0 ? g.nlow[v] : 0;
