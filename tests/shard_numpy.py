@@ -190,3 +190,42 @@ class NumpyShard:
         if not fetch:
             return None, None
         return self.c.astype(np.int32), (self.cround.astype(np.int32) if track else None)
+
+
+class DeferredNumpyShard(NumpyShard):
+    """The stand-in with HipShard's enqueue-only round end and fused propose seam
+    (gcolor_amd.shard.shard_color with finish_async): the round's winners travel in word 4
+    of the next propose seam's header, and a fused seam's apply checks every rank's header
+    first -- when one cannot be applied (a rank's deltas overflowed the inline part) the
+    shard 'halts' (GC_H_SEAM): the sweep behind it does nothing until the host clears it."""
+
+    HDR = 5
+
+    def begin(self, k, track):
+        self.acc_last, self.halted = 0, False
+        return super().begin(k, track)
+
+    def finish_async(self, r, from_deltas=False, check=False):
+        self.acc_last, _ = self.finish(r, from_deltas)
+
+    def propose_seam(self, r, C):
+        cnt, f, mm, fails = self.propose(r)
+        return self._pack([f, mm, fails, cnt, self.acc_last], cnt, C)
+
+    def apply_checked(self, kind, recv, r, hdr_stride):
+        if self.halted:
+            return
+        words = recv.view(-1, hdr_stride)[:, :self.HDR].numpy() & 0xFFFFFFFF
+        vals = np.where(words >= 1 << 31, words - (1 << 32), words)
+        if (vals[:, 4] < 0).any() or (vals[:, 3] > hdr_stride - self.HDR).any():
+            self.halted = True
+            return
+        self.apply(kind, recv, int(recv.numel()), r)
+
+    def clear_halt(self, code):
+        self.halted = False
+
+    def sweep_seam(self, i, count, C, emit, stride):
+        if self.halted:  # the sweep does nothing; its header is ignored by the host
+            return self._pack([0, 0, 0, 0, 0], 0, C)
+        return super().sweep_seam(i, count, C, emit, stride)

@@ -19,7 +19,7 @@ from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
 
 sys.path.insert(0, REPO)
 from oracle import oracle  # noqa: E402
-from shard_numpy import NumpyShard  # noqa: E402
+from shard_numpy import DeferredNumpyShard, NumpyShard  # noqa: E402
 
 from gcolor_amd import shard as sh  # noqa: E402
 
@@ -33,14 +33,14 @@ def _random_directed(n, m, seed):
     return np.cumsum(rp), dst.astype(np.int32)
 
 
-def run_threads(rp, col, parts, k=None, e1=True, **kw):
+def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, **kw):
     ranges = sh.balanced_ranges(rp, parts)
     hub = sh.ThreadHub(parts)
     out, err = [None] * parts, []
 
     def go(i):
         try:
-            ops = NumpyShard(rp, col, *ranges[i])
+            ops = (DeferredNumpyShard if deferred_ops else NumpyShard)(rp, col, *ranges[i])
             out[i] = sh.shard_color(ops, sh.ThreadTransport(hub, i), k, e1, track_rounds=True, **kw)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
@@ -107,25 +107,38 @@ def test_threads_directed_selfloops_bounded_and_stalled(seed):
     assert r.status == s["status"] and np.array_equal(r.colors, s["colors"])
 
 
+@pytest.mark.parametrize("deferred_ops", [False, True])
 @pytest.mark.parametrize("dense", [True, False, None])
 @pytest.mark.parametrize("local_sweeps", [1, 3])
 @pytest.mark.parametrize("inline", [4096, 5, 0])
-def test_dense_seams_and_local_sweeps(dense, local_sweeps, inline):
+def test_dense_seams_and_local_sweeps(dense, local_sweeps, inline, deferred_ops):
     """Slices of the proposal bytes instead of deltas, several JP sweeps between
     exchanges, and deltas that overflow the inline part of a seam's all-gather (a second
-    exchange: the rest of the deltas, or slices) leave the result unchanged."""
+    exchange: the rest of the deltas, or slices) leave the result unchanged; so do the
+    enqueue-only round end and the fused propose seam (deferred_ops), its misses included."""
     for seed in range(3):
         rp, col = _random_directed(400, 2000, 10 + seed)
         o = oracle.c_color(rp, col, "A")
-        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps, inline=inline)
+        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps, inline=inline, deferred_ops=deferred_ops)
         assert_matches_oracle(res[seed % 3], o)
         if dense:
             assert res[0].dense_exchanges > 0
         elif dense is False:
             assert res[0].dense_exchanges == 0
     ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
-    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps, inline=inline)[1],
-                          oracle.c_color(rp, col, "A"))
+    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps, inline=inline,
+                                      deferred_ops=deferred_ops)[1], oracle.c_color(rp, col, "A"))
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_fused_propose_seam_misses(parts):
+    """A fused propose seam whose deltas overflow the inline part on some rank is applied
+    nowhere (GC_H_SEAM); the host clears the halt and takes the unfused path."""
+    ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
+    res = run_threads(rp, col, parts, inline=8, deferred_ops=True)
+    assert max(r.fused_misses for r in res) > 0
+    for r in res:
+        assert_matches_oracle(r, oracle.c_color(rp, col, "A"))
 
 
 def test_more_ranks_than_vertices():
@@ -136,10 +149,11 @@ def test_more_ranks_than_vertices():
 
 
 # ---- two processes over torch.distributed (gloo), the transport the GPU ranks use -------
-def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096):
+def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096, deferred_ops=False):
     import torch.distributed as dist
     sys.path[:0] = [PKG_DIR, REPO, os.path.dirname(os.path.abspath(__file__))]
-    from shard_numpy import NumpyShard as NS
+    from shard_numpy import DeferredNumpyShard, NumpyShard
+    NS = DeferredNumpyShard if deferred_ops else NumpyShard
     from gcolor_amd import shard as shm
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     d = np.load(path)
@@ -155,16 +169,17 @@ def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,dense,inline", [("gen_1000_8_s1", None, 4096), ("gen_1000_8_s1", True, 4096),
-                                               ("asymmetric", None, 4096), ("gen_1000_8_s1", None, 3),
-                                               ("gen_1000_8_s1", False, 0)])
-def test_gloo_world_size_2(case, dense, inline, tmp_path):
+@pytest.mark.parametrize("case,dense,inline,deferred_ops", [
+    ("gen_1000_8_s1", None, 4096, False), ("gen_1000_8_s1", True, 4096, False), ("asymmetric", None, 4096, False),
+    ("gen_1000_8_s1", None, 3, False), ("gen_1000_8_s1", False, 0, False),
+    ("gen_1000_8_s1", None, 4096, True), ("asymmetric", None, 3, True)])
+def test_gloo_world_size_2(case, dense, inline, deferred_ops, tmp_path):
     ids, adj, rp, col = fixture_csr(load_golden(case))
     path = str(tmp_path / "g.npz")
     np.savez(path, rp=rp, col=col)
     port = 29500 + random.randint(0, 2000)
-    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path), dense, inline), nprocs=2,
-                                join=True)
+    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path), dense, inline, deferred_ops),
+                                nprocs=2, join=True)
     o = oracle.c_color(rp, col, "A")
     for r in range(2):
         got = json.load(open(tmp_path / f"r{r}.json"))
