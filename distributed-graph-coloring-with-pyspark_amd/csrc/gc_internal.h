@@ -218,10 +218,13 @@ __device__ __forceinline__ int gc_owner(int excl, int e) {
 // Vertices per wave chunk for a list of cnt entries spread over `waves` waves: 64 for
 // big lists (bandwidth), down to 1 for short ones (one vertex per wave, its edges over
 // the lanes: a tail sweep costs one dependent gather instead of ceil(64*deg/64)).
+#ifndef GC_VPW_MAX
+#define GC_VPW_MAX 64
+#endif
 __device__ __forceinline__ int gc_vpw(long long cnt, long long waves) {
     long long per = (cnt + waves - 1) / waves;
     int v = 1;
-    while (v < 64 && v < per) v <<= 1;
+    while (v < GC_VPW_MAX && v < per) v <<= 1;
     return v;
 }
 
