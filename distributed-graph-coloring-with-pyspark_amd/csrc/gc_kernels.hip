@@ -2662,7 +2662,7 @@ static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 // 216 -> 210 ms with the later sweeps on 256; the full grid stays for C2's big rounds)
 static const int kGridPS = round_grid("GC_GRID_PS", 512);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
-static const int kGridC = round_grid("GC_GRID_C", GC_ROUND_GRID);
+static const int kGridC = round_grid("GC_GRID_C", 768);  // mesh 512^3 111 -> 106 ms (1024 -> 768; 1536: 158), R-MAT and C2 alike
 static const int kGridPB = round_grid("GC_GRID_PB", GC_BLOCK_GRID);  // k_propose_block
 static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit_big
 // the later JP sweeps: mostly short lists, where 1024 workgroups' start-up and end-of-kernel
