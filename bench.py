@@ -199,11 +199,13 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
         dist.barrier()
 
     for _ in range(max(args.warmup, 1)):
-        res = sh.shard_color(ops, comm, want_colors=False)
+        res = sh.shard_color(ops, comm, want_colors=False, ahead=args.seam_ahead,
+                             inline_max=args.seam_inline_max)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):  # colours stay in HBM, as in the 1-GPU step
-        res = sh.shard_color(ops, comm, want_colors=False)
+        res = sh.shard_color(ops, comm, want_colors=False, ahead=args.seam_ahead,
+                             inline_max=args.seam_inline_max)
     barrier()
     t = (time.perf_counter() - t0) / args.steps
     tt = torch.tensor([t], dtype=torch.float64, device="cuda")
@@ -229,6 +231,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
                        "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2),
+                       "seam_ahead": args.seam_ahead, "seam_inline_max": args.seam_inline_max, "sweep_seams_run_ahead": res.ahead_seams,
+                       "fused_misses": res.fused_misses,
                        # the same graph coloured by the single-GPU engine on rank 0's GPU (best of 2)
                        "single_gpu_ms": round(t1, 2), "speedup_vs_single_gpu": round(t1 / (t * 1e3), 3)},
             "colors_used": res.max_color + 1,
@@ -264,6 +268,13 @@ def main():
                     help="north_star mode N1: JP rounds ranked by prio_hash(seed, v) instead of (deg, pos)")
     ap.add_argument("--speculative", action="store_true",
                     help="north_star mode N1: speculative first-fit rounds with one-shot resolution")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the sharded engine even at N=1 (one-rank RCCL group): the multi-GPU protocol's "
+                         "own cost on one GPU, against the single-GPU engine on the same graph")
+    ap.add_argument("--seam-ahead", type=int, default=4,
+                    help="sharded runs: JP sweep seams a fused round runs ahead of the host (gcolor_amd.shard)")
+    ap.add_argument("--seam-inline-max", type=int, default=1 << 16,
+                    help="sharded runs: largest inline delta part of a seam (gcolor_amd.shard)")
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
@@ -273,7 +284,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    if world == 1 and args.sharded:  # a one-rank group without a launcher
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.sharded:
         import torch.distributed as dist
         # GC_BENCH_DEVICE pins every rank to one GPU (rehearsal of the multi-rank path on a
         # 1-GPU box, with GC_BENCH_BACKEND=gloo); the driver's runs use one GPU per rank
@@ -285,7 +301,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-        if not args.replicas:
+        if args.sharded or not args.replicas:
             return run_sharded(args, world, rank, local_rank, dist, torch)
     else:
         torch.cuda.set_device(0)

@@ -345,6 +345,8 @@ class ShardResult:
     dense_exchanges: int = 0
     hub_halts: int = 0  # checked finishes that found the asynchronous hub JP unfinished (some rank)
     fused_misses: int = 0  # fused propose seams that could not be applied (the unfused path followed)
+    ahead_misses: int = 0  # sweep seams run ahead that overflowed (the host moved their deltas)
+    ahead_seams: int = 0  # sweep seams run ahead of the host
 
     @property
     def rounds(self):
@@ -374,7 +376,8 @@ def _hdr_values(words):
 
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
-                want_colors=True, inline=4096, deferred=True, hub_budget=3, fuse=True):
+                want_colors=True, inline=4096, deferred=True, hub_budget=3, fuse=True, ahead=4,
+                inline_max=1 << 16):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
@@ -401,7 +404,18 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     all-gather, its apply and the first JP sweep seam are enqueued together, with ONE host
     wait for both headers.  The apply checks every rank's header on the device and, when
     some rank halted or overflowed, applies nothing and halts the shard (GC_H_SEAM), so the
-    sweep behind it does nothing; the host clears that halt and takes the unfused path."""
+    sweep behind it does nothing; the host clears that halt and takes the unfused path.
+
+    ``ahead``: a fused round enqueues up to that many JP sweep seams behind the propose seam
+    (as many as the last round needed), each applied on the device with the same check, and
+    the host reads all their headers in its one wait.  A seam whose deltas overflowed on some
+    rank halts the shard there: the host clears the halt, moves that seam's deltas itself and
+    runs the sweeps behind it again.  Seams past the JP's end sweep empty lists.
+
+    The inline part follows the frontiers: a round's is the last round's largest per-rank
+    frontier rounded up to a power of two, between ``inline`` and ``inline_max`` (every rank
+    derives it from the same headers), so a round whose frontier did not outgrow the last
+    one's moves its deltas in one all-gather per seam and runs fused."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -411,7 +425,8 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     starts = [int(x) for x in rng[:, 0]]
     lens = [int(x) for x in rng[:, 1] - rng[:, 0]]
     stride = max(max(lens), 1)
-    C = max(int(inline), 0)
+    C0 = C = max(int(inline), 0)
+    Cmax = max(int(inline_max), C0)
     # replicated hubs (gc_shard_start_hubs): the same count on every rank
     repl = getattr(ops, "hub_count", lambda: 0)() > 0
     hdr_bytes = 8 * HDR
@@ -460,8 +475,9 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     pending = None  # (round, U, F, maxmex, from_deltas) of a round whose finish is enqueued
     acc_known = None  # its winners, from a rank whose finish completed (when another halted)
     hub_grid, calm = max(int(hub_budget), 1), 0  # full-grid hub sweeps before the tail; rounds without a halt
-    fuse_on = fuse and deferred and dense is not True and C > 0
+    fuse_on = fuse and deferred and dense is not True and C0 > 0
     last_fmax = None  # largest per-rank frontier of the last propose seam (does the next one fit inline?)
+    last_seams = 1  # sweep seams the last round needed (how many a fused round runs ahead)
     r = 0
     while True:
         if U == 0 and pending is None:  # coloring.py:86-90
@@ -469,17 +485,28 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             break
         if r > max_rounds:
             raise RuntimeError("round limit exceeded")
+        if last_fmax is not None and C0 > 0:
+            C = min(Cmax, max(C0, 1 << max(int(last_fmax) - 1, 0).bit_length()))
         fused = fuse_on and last_fmax is not None and last_fmax <= C
-        pre = None  # the first sweep seam's (headers, received), when fused with the propose seam
+        pre = []  # sweep seams run ahead of the host: (headers, received), applied on the device
+        cand_applied = False  # the propose seam's deltas were applied on the device
         if fused:
             res.exchanges += 1
             recv = comm.allgather(ops.propose_seam(r, C))
             ops.apply_checked(KIND_CAND, recv, r, HDR + C)
-            pre = gather(ops.sweep_seam(0, 1, C, True, stride))  # the one host wait
-            hdr = _hdr_values(recv.view(P, -1)[:, :HDR].cpu().numpy())
-            if int(hdr[:, 4].min()) < 0 or int(hdr[:, 3].max()) > C:  # not applied anywhere
+            recvs = [recv]
+            for j in range(max(1, min(int(ahead), last_seams))):
+                res.exchanges += 1
+                res.ahead_seams += 1
+                recvs.append(comm.allgather(ops.sweep_seam(j, 1, C, True, stride)))
+                ops.apply_checked(KIND_STATE, recvs[-1], r, HDR + C)
+            words = torch.stack([x.view(P, -1)[:, :HDR] for x in recvs]).cpu().numpy()  # the one host wait
+            hdr = _hdr_values(words[0])
+            pre = [(_hdr_values(words[j]), recvs[j]) for j in range(1, len(recvs))]
+            cand_applied = int(hdr[:, 4].min()) >= 0 and int(hdr[:, 3].max()) <= C
+            if not cand_applied:  # applied nowhere, and the sweep seams behind it did nothing
                 ops.clear_halt(H_SEAM)  # (a rank halted by its finish keeps that halt)
-                pre = None
+                pre = []
                 res.fused_misses += 1
         else:
             hdr, recv = gather(ops.propose_seam(r, C))
@@ -530,29 +557,39 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             res.status, res.fail_round, res.fail_count = FAILED, r, fails
             break
         # candidates >= 62 live in cand[], outside the proposal bytes: deltas only
-        if pre is None:  # (a fused seam was applied on the device)
+        if not cand_applied:
             finish_deltas(KIND_CAND, hdr, recv, r, maxmex < K8_BIG)
         # JP sweeps; a rank decides at most what it has left, so the seam's form is known
         # before the sweep runs (and a slice seam writes no deltas)
-        i, left, any_dense, hubs_async = 0, int(hdr[:, 0].max()), False, False
+        i, left, any_dense, hubs_async, seams = 0, int(hdr[:, 0].max()), False, False, 0
         while True:
-            if pre is not None:  # the first sweep seam ran fused with the propose seam
+            if pre:  # a sweep seam run ahead (fused with the propose seam)
                 sl, cnt = False, 1
-                (hdr, recv), pre = pre, None
+                hdr, recv = pre.pop(0)
+                if int(hdr[:, 3].max()) > C:
+                    # some rank's deltas overflowed: applied nowhere, the shard halted there and
+                    # the seams behind it did nothing (their sweeps run again from i + 1)
+                    ops.clear_halt(H_SEAM)
+                    pre = []
+                    res.ahead_misses += 1
+                    any_dense |= finish_deltas(KIND_STATE, hdr, recv, r, True)
+                i += 1
             else:
                 sl = slice_for(left)
                 cnt = local_sweeps if i else 1
                 hdr, recv = gather(ops.sweep_seam(i, cnt, C, not sl, stride))
-            i += cnt
-            if sl:
-                ops.put_slices(recv[hdr_bytes:], hdr_bytes + stride, starts, lens)
-                any_dense = True
-            else:
-                any_dense |= finish_deltas(KIND_STATE, hdr, recv, r, True)
+                i += cnt
+                if sl:
+                    ops.put_slices(recv[hdr_bytes:], hdr_bytes + stride, starts, lens)
+                    any_dense = True
+                else:
+                    any_dense |= finish_deltas(KIND_STATE, hdr, recv, r, True)
+            seams += 1
             if int(hdr[:, 0].sum()) == 0:
                 break
             if repl and int(hdr[:, 2].sum()) == 0:
                 # every rank's lights are decided: each rank runs the hubs' sweeps alike
+                i += len(pre)  # (sweeps run ahead past the lights' end swept empty lists)
                 if deferred:
                     res.jp_sweeps += ops.start_hubs_async(i, any_dense, hub_grid)
                     hubs_async = True
@@ -561,6 +598,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
                 break
             left = int(hdr[:, 0].max())
             res.jp_sweeps += 1
+        last_seams = seams
         if deferred:
             ops.finish_async(r, not any_dense, check=hubs_async)
             pending = (r, U, F, maxmex, not any_dense)

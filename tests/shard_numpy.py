@@ -229,3 +229,24 @@ class DeferredNumpyShard(NumpyShard):
         if self.halted:  # the sweep does nothing; its header is ignored by the host
             return self._pack([0, 0, 0, 0, 0], 0, C)
         return super().sweep_seam(i, count, C, emit, stride)
+
+
+class InflatedShard(DeferredNumpyShard):
+    """DeferredNumpyShard whose sweep seams carry every delta three times (applying a state
+    twice changes nothing): their counts can overflow the inline part while the propose
+    seam's fit, which exercises the host's recovery of a sweep seam run ahead."""
+
+    def __init__(self, rp, col, lo, hi):
+        super().__init__(rp, col, lo, hi)
+        self.delta = torch.empty(3 * max(self.hi - self.lo, 1), dtype=torch.int64)
+        self._x3 = False
+
+    def _emit(self, pairs):
+        return super()._emit(pairs * 3 if self._x3 else pairs)
+
+    def sweep(self, i, count=1, emit=True):
+        self._x3 = True
+        try:
+            return super().sweep(i, count, emit)
+        finally:
+            self._x3 = False

@@ -19,7 +19,7 @@ from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
 
 sys.path.insert(0, REPO)
 from oracle import oracle  # noqa: E402
-from shard_numpy import DeferredNumpyShard, NumpyShard  # noqa: E402
+from shard_numpy import DeferredNumpyShard, InflatedShard, NumpyShard  # noqa: E402
 
 from gcolor_amd import shard as sh  # noqa: E402
 
@@ -33,14 +33,15 @@ def _random_directed(n, m, seed):
     return np.cumsum(rp), dst.astype(np.int32)
 
 
-def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, **kw):
+def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, shard_cls=None, **kw):
     ranges = sh.balanced_ranges(rp, parts)
     hub = sh.ThreadHub(parts)
     out, err = [None] * parts, []
 
     def go(i):
         try:
-            ops = (DeferredNumpyShard if deferred_ops else NumpyShard)(rp, col, *ranges[i])
+            cls = shard_cls or (DeferredNumpyShard if deferred_ops else NumpyShard)
+            ops = cls(rp, col, *ranges[i])
             out[i] = sh.shard_color(ops, sh.ThreadTransport(hub, i), k, e1, track_rounds=True, **kw)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
@@ -119,24 +120,42 @@ def test_dense_seams_and_local_sweeps(dense, local_sweeps, inline, deferred_ops)
     for seed in range(3):
         rp, col = _random_directed(400, 2000, 10 + seed)
         o = oracle.c_color(rp, col, "A")
-        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps, inline=inline, deferred_ops=deferred_ops)
+        res = run_threads(rp, col, 3, dense=dense, local_sweeps=local_sweeps, inline=inline, inline_max=inline,
+                          deferred_ops=deferred_ops)
         assert_matches_oracle(res[seed % 3], o)
         if dense:
             assert res[0].dense_exchanges > 0
         elif dense is False:
             assert res[0].dense_exchanges == 0
     ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
-    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps, inline=inline,
+    assert_matches_oracle(run_threads(rp, col, 2, dense=dense, local_sweeps=local_sweeps, inline=inline, inline_max=inline,
                                       deferred_ops=deferred_ops)[1], oracle.c_color(rp, col, "A"))
 
 
 @pytest.mark.parametrize("parts", [2, 3])
-def test_fused_propose_seam_misses(parts):
+@pytest.mark.parametrize("ahead", [1, 2, 4])
+@pytest.mark.parametrize("inline,inline_max", [(8, 8), (24, 24), (8, 64)])
+def test_fused_propose_seam_misses(parts, ahead, inline, inline_max):
     """A fused propose seam whose deltas overflow the inline part on some rank is applied
-    nowhere (GC_H_SEAM); the host clears the halt and takes the unfused path."""
+    nowhere (GC_H_SEAM); the host clears the halt and takes the unfused path.  Sweep seams
+    run ahead of the host (``ahead``) halt the same way at the first overflow: the host
+    moves that seam's deltas and runs the sweeps behind it again.  (8, 64): the inline part
+    follows the frontiers, and a round whose frontier outgrew the last one's misses."""
     ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
-    res = run_threads(rp, col, parts, inline=8, deferred_ops=True)
+    res = run_threads(rp, col, parts, inline=inline, inline_max=inline_max, deferred_ops=True, ahead=ahead)
     assert max(r.fused_misses for r in res) > 0
+    for r in res:
+        assert_matches_oracle(r, oracle.c_color(rp, col, "A"))
+
+
+@pytest.mark.parametrize("ahead", [2, 4])
+def test_sweep_seams_ahead_overflow(ahead):
+    """Sweep seams run ahead of the host whose deltas overflow the inline part (the stand-in
+    sends every sweep delta three times): the first such seam halts every rank, the host
+    moves its deltas and runs the sweeps behind it again; the result is unchanged."""
+    ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
+    res = run_threads(rp, col, 2, inline=48, inline_max=48, shard_cls=InflatedShard, ahead=ahead)
+    assert max(r.ahead_misses for r in res) > 0 and min(r.ahead_seams for r in res) > 0
     for r in res:
         assert_matches_oracle(r, oracle.c_color(rp, col, "A"))
 
@@ -160,7 +179,7 @@ def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096, defe
     rp, col = d["rp"], d["col"]
     lo, hi = shm.balanced_ranges(rp, world)[rank]
     res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, track_rounds=True, dense=dense,
-                          inline=inline)
+                          inline=inline, inline_max=inline)
     out = {"status": res.status, "colors": res.colors.tolist(), "cround": res.colored_round.tolist(),
            "U": res.round_U, "F": res.round_F, "maxmex": res.round_maxmex, "acc": res.round_accepted,
            "seeds": res.round_seeds}

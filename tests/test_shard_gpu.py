@@ -145,8 +145,12 @@ def test_replicated_hubs_sharded(seed, monkeypatch):
         assert r.hub_halts > 0
         same_as_single(dg, 2, deferred=False)
         same_as_single(dg, 3, fuse=False)
-        r, _ = same_as_single(dg, 2, inline=64)  # fused propose seams that overflow: the unfused path
+        r, _ = same_as_single(dg, 2, inline=64, inline_max=64)  # fused seams that overflow: the unfused path
         assert r.fused_misses > 0
+        same_as_single(dg, 3, inline=64, inline_max=1024)  # the inline part follows the frontiers
+        same_as_single(dg, 3, ahead=1)  # one sweep seam fused with the propose seam
+        r, _ = same_as_single(dg, 2, ahead=2)
+        assert r.ahead_seams > 0
     monkeypatch.delenv("GC_SHARD_TAIL_HMAX")
     monkeypatch.setenv("GC_SHARD_HUBS", "0")
     with DeviceGraph.rmat(12, 16, seed=seed) as dg:
