@@ -292,7 +292,9 @@ extern "C" int gc_shard_propose_async(gc_shard* sh, int64_t round, int64_t* delt
     gcl_fsort(d, L, g->fsum, g->stream);
     gcl_pack_c4(d, g->stream);
     gcl_propose(d, L, g->stream);
-    gcl_propose_block(d, L, g->stream);
+    // no heavy (deg > heavy_t) or wide (mex >= 64, so deg >= 64) proposer possible: no
+    // k_propose_block launch (meshes: one launch of host time per round, as in gc_color)
+    if (g->maxdeg > d.heavy_t || g->maxdeg >= 64) gcl_propose_block(d, L, g->stream);
     gcl_delta_cand(d, L, g->stream);
     GC_HIP(hipGetLastError());
     return GC_OK;
