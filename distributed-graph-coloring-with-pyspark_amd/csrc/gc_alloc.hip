@@ -1,0 +1,117 @@
+// gc_alloc.hip -- the library's device / pinned-host allocator: a per-device cache of
+// freed blocks, keyed by exact size.
+//
+// A colouring from a resident CSR (rank partition, hub index, rounds,
+// validation) allocates ~60 buffers per graph handle; hipMalloc of a large buffer costs
+// tens of microseconds to milliseconds and hipFree synchronises the device.  Handles that
+// are created and destroyed repeatedly (bench.py's timed step, the CLI's two runs, the
+// tests) therefore get their buffers back from this cache: a freed block is parked under
+// (device, size) and handed to the next request of exactly that size.  The cache is
+// released on a failed allocation (then retried) and by gc_release_cache().
+//
+// Callers free a block only when no queued work still uses it (every free site follows a
+// stream synchronisation), so a parked block is idle by construction.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <unordered_map>
+
+#include "gc_engine.h"
+
+namespace {
+
+struct Block {
+    size_t bytes;
+    int device;
+    bool host;
+};
+
+struct Cache {
+    std::mutex mu;
+    std::unordered_map<void*, Block> live;                   // handed out
+    std::multimap<std::pair<long long, size_t>, void*> idle;  // (device or -1 for host, bytes) -> block
+    size_t idle_bytes = 0;
+};
+
+Cache& cache() {
+    static Cache* c = new Cache();  // never destroyed: frees at process exit would race the runtime's teardown
+    return *c;
+}
+
+void release_locked(Cache& c) {
+    int dev0 = 0;
+    hipGetDevice(&dev0);
+    for (auto& kv : c.idle) {
+        if (kv.first.first < 0) {
+            hipHostFree(kv.second);
+        } else {
+            hipSetDevice((int)kv.first.first);
+            hipFree(kv.second);
+        }
+    }
+    c.idle.clear();
+    c.idle_bytes = 0;
+    hipSetDevice(dev0);
+}
+
+hipError_t alloc(void** p, size_t bytes, bool host) {
+    if (bytes == 0) bytes = 1;
+    int dev = 0;
+    hipGetDevice(&dev);
+    const long long key = host ? -1 : dev;
+    Cache& c = cache();
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto it = c.idle.find({key, bytes});
+        if (it != c.idle.end()) {
+            *p = it->second;
+            c.idle.erase(it);
+            c.idle_bytes -= bytes;
+            c.live[*p] = Block{bytes, dev, host};
+            return hipSuccess;
+        }
+    }
+    hipError_t e = host ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+    if (e != hipSuccess) {  // the cache may hold what is missing: give it back and retry once
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> lk(c.mu);
+        release_locked(c);
+        e = host ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+        if (e != hipSuccess) return e;
+    }
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.live[*p] = Block{bytes, dev, host};
+    return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t gc_dmalloc(void** p, size_t bytes) { return alloc(p, bytes, false); }
+hipError_t gc_hmalloc(void** p, size_t bytes) { return alloc(p, bytes, true); }
+
+hipError_t gc_dfree(void* p) {
+    if (!p) return hipSuccess;
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return hipFree(p);  // not ours (never expected)
+    const Block b = it->second;
+    c.live.erase(it);
+    c.idle.insert({{b.host ? -1 : b.device, b.bytes}, p});
+    c.idle_bytes += b.bytes;
+    return hipSuccess;
+}
+
+extern "C" int gc_release_cache(void) {
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    release_locked(c);
+    return GC_OK;
+}
+
+size_t gc_cache_idle_bytes(void) {
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return c.idle_bytes;
+}

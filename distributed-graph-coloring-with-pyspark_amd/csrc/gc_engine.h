@@ -87,7 +87,38 @@ struct gc_graph {
     int* hpl = nullptr;        // hubs-off heavy JP pending lists (gc_alloc_heavy_pending), nnz + n ints
     int* hplc = nullptr;
     uint64_t part_seed = 0;
+    // edge-balanced tiling of the CSR (gc_prep.hip): whole-row tiles of <= GC_TW rows +
+    // entries, rows longer than GC_TH split into GC_SEG-entry segments
+    unsigned char* kb = nullptr;  // min(deg, 255): the rank key's byte the partition gathers first
+    int* tile_r0 = nullptr;       // [ntiles + 1] first row of each tile
+    long long ntiles = 0;
+    int* seg_row = nullptr;       // heavy segments: row, index within the row
+    int* seg_j = nullptr;
+    ull* seg_aux = nullptr;       // per segment: packed class counts of the last two-pass kernel
+    unsigned* seg_cls = nullptr;  // per segment and thread: 16 x 2-bit classes
+    long long* seg_base = nullptr;  // [ntiles + 1] exclusive scan of the tiles' segment counts; [ntiles] = total
+    long long nseg_cap = 0;
+    unsigned* hubmap = nullptr;   // bit per vertex: hid >= 0 (symmetric hub transpose)
 };
+
+// caching allocator (gc_alloc.hip): every device / pinned-host buffer of the library
+hipError_t gc_dmalloc(void** p, size_t bytes);
+hipError_t gc_hmalloc(void** p, size_t bytes);
+hipError_t gc_dfree(void* p);
+size_t gc_cache_idle_bytes(void);  // parked bytes (count as free memory)
+
+// gc_prep.hip: tiling, rank partition, validation and hub-transpose passes
+int gc_build_tiling(gc_graph* g);
+// rank partition of rows (rp, src) into dst (!= src): per row [class 0 | class 1 | class 2]
+// with class 0 = lower key, 1 = equal key and earlier position (both lower rank), 2 =
+// higher rank; nlow = c0 + c1, neq = c1 (neq may be null).  prio 0: key = deg (coloring.py:64),
+// 1: key = prio_hash(seed, v).  *bad (device) counts entries outside [0, n).
+int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad);
+int gc_validate_tiles(gc_graph* g, const int* colors);  // -> ctl->uncolored, ctl->conflicts
+// symmetric graphs: hub transpose (hin_rp / hin_col: the hubs listed in each row) and the
+// lower-rank hubs of every hub row (hlow counts -> klow[x]); hubmap / hid / hub_v ready
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow);
+int gc_hub_transpose_fill(gc_graph* g, long long H);
 
 void gc_set_error(const char* fmt, ...);
 
@@ -100,7 +131,7 @@ void gc_set_error(const char* fmt, ...);
         }                                                                                     \
     } while (0)
 
-int gc_alloc_graph_common(gc_graph* g);  // deg, maxdeg, transpose (gc_graph.hip)
+int gc_alloc_graph_common(gc_graph* g, const int* src);  // deg, maxdeg, rank partition of src, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi);  // the same, symmetric graphs (no atomics)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip

@@ -128,9 +128,9 @@ GLists gc_lists(const gc_graph* g) {
 template <typename T>
 static int dalloc(T** p, size_t count) {
     if (count == 0) count = 1;
-    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    hipError_t e = gc_dmalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) {
-        gc_set_error("hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
+        gc_set_error("gc_dmalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
         return GC_ENOMEM;
     }
     return GC_OK;
@@ -182,7 +182,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->rec, (size_t)kRoundCap);
     A(g->fsum, (size_t)gcl_fsort_blocks(g->n) + 1);
 #undef A
-    GC_HIP(hipHostMalloc((void**)&g->hsnap, 2 * sizeof(DevCtl), hipHostMallocDefault));
+    GC_HIP(gc_hmalloc((void**)&g->hsnap, 2 * sizeof(DevCtl)));
     GC_HIP(hipHostGetDevicePointer((void**)&g->hsnap_dev, g->hsnap, 0));
     GC_HIP(hipEventCreateWithFlags(&g->evsnap[0], hipEventDisableTiming));
     GC_HIP(hipEventCreateWithFlags(&g->evsnap[1], hipEventDisableTiming));
@@ -659,8 +659,7 @@ extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolore
     }
     GC_HIP(hipMemsetAsync(&g->ctl->uncolored, 0, sizeof(ull), g->stream));
     GC_HIP(hipMemsetAsync(&g->ctl->conflicts, 0, sizeof(ull), g->stream));
-    gcl_validate(gc_view(g), src, g->heavy, gc_grid_for_waves(g->n), g->stream);
-    GC_HIP(hipGetLastError());
+    if ((rc = gc_validate_tiles(g, src))) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));
     if (uncolored) *uncolored = (int64_t)g->hctl->uncolored;

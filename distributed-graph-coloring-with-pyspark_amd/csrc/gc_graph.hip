@@ -16,16 +16,6 @@
 // ------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------
-__global__ void k_check_cols(const int* col, long long nnz, int n, ull* bad) {
-    ull b = 0;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (long long)gridDim.x * blockDim.x) {
-        const int u = col[e];
-        b += (u < 0 || u >= n);
-    }
-    b = gc_wave_sum(b);
-    if (gc_lane() == 0 && b) atomicAdd(bad, b);
-}
-
 // in-neighbour CSR of the rows [lo, hi): for every target u, the rows in range listing u
 __global__ void k_count_targets(const long long* rp, const int* col, long long lo, long long hi, ull* cnt) {
     for (long long v = lo + (long long)blockIdx.x * blockDim.x + threadIdx.x; v < hi; v += (long long)gridDim.x * blockDim.x)
@@ -165,10 +155,10 @@ static int exclusive_scan_ll(const long long* in, long long* out, long long coun
     size_t bytes = 0;
     GC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s));
     void* tmp = nullptr;
-    GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+    GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
     hipStreamSynchronize(s);
-    hipFree(tmp);
+    gc_dfree(tmp);
     GC_HIP(e);
     return GC_OK;
 }
@@ -176,8 +166,14 @@ static int exclusive_scan_ll(const long long* in, long long* out, long long coun
 void gc_free_all(gc_graph* g) {
     if (!g) return;
     hipSetDevice(g->device);
-    if (g->trp && g->trp != g->rp) hipFree(g->trp);
-    if (g->tcol && g->tcol != g->col) hipFree(g->tcol);
+    if (g->stream) hipStreamSynchronize(g->stream);  // parked blocks are idle (gc_alloc.hip)
+    {
+        void* prep[] = {g->kb, g->tile_r0, g->seg_row, g->seg_j, g->seg_aux, g->seg_cls, g->seg_base, g->hubmap};
+        for (void* p : prep)
+            if (p) gc_dfree(p);
+    }
+    if (g->trp && g->trp != g->rp) gc_dfree(g->trp);
+    if (g->tcol && g->tcol != g->col) gc_dfree(g->tcol);
     gc_hubs_free(g);
     if (g->borrowed) {  // a shard's view: the CSR belongs to the replicated graph handle
         g->rp = nullptr;
@@ -189,9 +185,9 @@ void gc_free_all(gc_graph* g) {
                     g->F[1], g->heavy, g->wide, g->undL[0], g->undL[1], g->undL[2], g->undH[0], g->undH[1],
                     g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->lcur, g->neq, g->hpl, g->hplc, g->bstat, g->accs, g->bigw, g->rec, g->fsum, g->ctl};
     for (void* p : ptrs)
-        if (p) hipFree(p);
-    if (g->hctl) hipHostFree(g->hctl);
-    if (g->hsnap) hipHostFree(g->hsnap);
+        if (p) gc_dfree(p);
+    if (g->hctl) gc_dfree(g->hctl);
+    if (g->hsnap) gc_dfree(g->hsnap);
     for (auto e : g->evsnap)
         if (e) hipEventDestroy(e);
     for (auto e : g->evpool) hipEventDestroy(e);
@@ -215,11 +211,11 @@ static int new_graph(gc_graph** out, long long n, long long nnz, uint32_t flags,
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&g->ev0)) != hipSuccess || (e = hipEventCreate(&g->ev1)) != hipSuccess ||
-        (e = hipMalloc((void**)&g->ctl, sizeof(DevCtl))) != hipSuccess ||
-        (e = hipHostMalloc((void**)&g->hctl, sizeof(DevCtl), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipMalloc((void**)&g->rp, sizeof(long long) * (size_t)(n + 1))) != hipSuccess ||
-        (e = hipMalloc((void**)&g->col, sizeof(int) * (size_t)std::max<long long>(nnz, 1))) != hipSuccess ||
-        (e = hipMalloc((void**)&g->deg, sizeof(int) * (size_t)std::max<long long>(n, 1))) != hipSuccess) {
+        (e = gc_dmalloc((void**)&g->ctl, sizeof(DevCtl))) != hipSuccess ||
+        (e = gc_hmalloc((void**)&g->hctl, sizeof(DevCtl))) != hipSuccess ||
+        (e = gc_dmalloc((void**)&g->rp, sizeof(long long) * (size_t)(n + 1))) != hipSuccess ||
+        (e = gc_dmalloc((void**)&g->col, sizeof(int) * (size_t)std::max<long long>(nnz, 1))) != hipSuccess ||
+        (e = gc_dmalloc((void**)&g->deg, sizeof(int) * (size_t)std::max<long long>(n, 1))) != hipSuccess) {
         gc_set_error("graph allocation failed: %s", hipGetErrorString(e));
         gc_free_all(g);
         delete g;
@@ -229,55 +225,37 @@ static int new_graph(gc_graph** out, long long n, long long nnz, uint32_t flags,
     return GC_OK;
 }
 
-// Rank is static -- (deg, pos), coloring.py:64 -- so every row is stored with its
-// lower-rank neighbours first and nlow[v] counts them: a Jones-Plassmann sweep then
-// reads only those entries (every other listed neighbour cannot block v).  Mark the
-// entries (k_rank_flags), then stable-partition each row on the mark into a new column
-// array (k_partition_rows).  Order inside a row is irrelevant to every phase (mex, LFMIS,
-// push and validation all work on sets).
-static int partition_rows(gc_graph* g) {
+// deg, kb, maxdeg and the rp checks; the rank partition of the input rows `src` (device,
+// file order) into g->col (rows lower-rank first, coloring.py:64: see gc_prep.hip) with
+// the column range check folded in; the transpose unless symmetric.
+int gc_alloc_graph_common(gc_graph* g, const int* src) {
     hipStream_t s = g->stream;
-    GC_HIP(hipMalloc((void**)&g->nlow, sizeof(int) * (size_t)std::max<long long>(g->n, 1)));
-    if (g->n == 0) return GC_OK;
-    if (g->nnz == 0) {
-        GC_HIP(hipMemsetAsync(g->nlow, 0, sizeof(int) * (size_t)g->n, s));
-        GC_HIP(hipStreamSynchronize(s));
-        return GC_OK;
-    }
-    int* out = nullptr;
-    GC_HIP(hipMalloc((void**)&out, sizeof(int) * (size_t)g->nnz));
-    const int grid = gc_grid_for_waves(g->n, 8192);
-    gcl_rank_flags(g->rp, g->col, reinterpret_cast<const unsigned*>(g->deg), (int)g->n, g->nlow, grid, s);
-    gcl_partition_rows(g->rp, g->col, g->deg, g->nlow, (int)g->n, out, grid, s);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-        hipFree(out);
-        gc_set_error("row partition failed");
-        return GC_EHIP;
-    }
-    hipFree(g->col);
-    g->col = out;
-    return GC_OK;
-}
-
-// deg, maxdeg, column range check, row partition by rank, transpose (unless symmetric)
-int gc_alloc_graph_common(gc_graph* g) {
-    hipStream_t s = g->stream;
+    const size_t n1 = (size_t)std::max<long long>(g->n, 1);
+    GC_HIP(gc_dmalloc((void**)&g->nlow, sizeof(int) * n1));
+    GC_HIP(gc_dmalloc((void**)&g->neq, sizeof(int) * n1));
+    GC_HIP(gc_dmalloc((void**)&g->kb, n1));
     GC_HIP(hipMemsetAsync(g->ctl, 0, sizeof(DevCtl), s));
-    if (g->n > 0) gcl_degrees(g->rp, (int)g->n, g->deg, &g->ctl->seedkey, grid_for(g->n), s);
-    if (g->nnz > 0)
-        hipLaunchKernelGGL(k_check_cols, dim3(grid_for(g->nnz)), dim3(GC_BLOCK), 0, s, g->col, g->nnz, (int)g->n,
-                           &g->ctl->conflicts);
+    if (g->n > 0)
+        gcl_degrees(g->rp, (int)g->n, g->nnz, g->deg, g->kb, &g->ctl->seedkey, &g->ctl->list_cnt, grid_for(g->n), s);
     GC_HIP(hipGetLastError());
+    GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
+    GC_HIP(hipStreamSynchronize(s));
+    if (g->hctl->list_cnt) {
+        gc_set_error("row_ptr is not a CSR offset array (rp[0] != 0, rp[n] != nnz or decreasing)");
+        return GC_EINVAL;
+    }
+    g->maxdeg = (long long)g->hctl->seedkey;
+    if (g->maxdeg >= (1ll << 31)) { gc_set_error("degree too large"); return GC_EINVAL; }
+    int rc = gc_partition(g, src, g->col, GC_PRIORITY_REF, 0, &g->ctl->conflicts);
+    if (rc) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
     GC_HIP(hipStreamSynchronize(s));
     if (g->hctl->conflicts) {
         gc_set_error("%llu adjacency entries are outside [0, n)", (unsigned long long)g->hctl->conflicts);
         return GC_EINVAL;
     }
-    g->maxdeg = (long long)g->hctl->seedkey;
-    if (g->maxdeg >= (1ll << 31)) { gc_set_error("degree too large"); return GC_EINVAL; }
-    int rc0 = partition_rows(g);
-    if (rc0) return rc0;
+    g->part_prio = GC_PRIORITY_REF;
+    g->bpart = true;  // the reference partition splits every low part by degree too (variant B)
     if (g->flags & GC_GRAPH_SYMMETRIC) {
         g->trp = g->rp;
         g->tcol = g->col;
@@ -296,22 +274,22 @@ int gc_build_in_csr(gc_graph* g, long long lo, long long hi) {
     GC_HIP(hipMemcpy(&e0, g->rp + lo, sizeof(long long), hipMemcpyDeviceToHost));
     GC_HIP(hipMemcpy(&e1, g->rp + hi, sizeof(long long), hipMemcpyDeviceToHost));
     long long* cnt = nullptr;
-    GC_HIP(hipMalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
-    GC_HIP(hipMalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
-    GC_HIP(hipMalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e1 - e0, 1)));
+    GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e1 - e0, 1)));
     GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
     if (hi > lo)
         hipLaunchKernelGGL(k_count_targets, dim3(grid_for(hi - lo)), dim3(GC_BLOCK), 0, s, g->rp, g->col, lo, hi,
                            (ull*)cnt);
     int rc = exclusive_scan_ll(cnt, g->trp, g->n + 1, s);
-    if (rc) { hipFree(cnt); return rc; }
+    if (rc) { gc_dfree(cnt); return rc; }
     GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
     if (hi > lo)
         hipLaunchKernelGGL(k_fill_transpose, dim3(grid_for(hi - lo)), dim3(GC_BLOCK), 0, s, g->rp, g->col, lo, hi,
                            g->trp, (ull*)cnt, g->tcol);
     GC_HIP(hipGetLastError());
     GC_HIP(hipStreamSynchronize(s));
-    hipFree(cnt);
+    gc_dfree(cnt);
     return GC_OK;
 }
 
@@ -319,17 +297,17 @@ int gc_build_in_csr(gc_graph* g, long long lo, long long hi) {
 int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi) {
     hipStream_t s = g->stream;
     long long* cnt = nullptr;
-    GC_HIP(hipMalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
-    GC_HIP(hipMalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
+    GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
     GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
     const int grid = gc_grid_for_waves(std::max<long long>(g->n, 1) * GC_WAVE, 8192);
     if (g->n > 0) hipLaunchKernelGGL(k_filter_count, dim3(grid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->n, lo, hi, cnt);
     int rc = exclusive_scan_ll(cnt, g->trp, g->n + 1, s);
-    hipFree(cnt);
+    gc_dfree(cnt);
     if (rc) return rc;
     long long e = 0;
     GC_HIP(hipMemcpy(&e, g->trp + g->n, sizeof(long long), hipMemcpyDeviceToHost));
-    GC_HIP(hipMalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e, 1)));
     if (g->n > 0)
         hipLaunchKernelGGL(k_filter_fill, dim3(grid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->n, lo, hi, g->trp, g->tcol);
     GC_HIP(hipGetLastError());
@@ -337,8 +315,13 @@ int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi) {
     return GC_OK;
 }
 
-static int finish_create(gc_graph* g, gc_graph** out) {
-    int rc = gc_alloc_graph_common(g);
+// src: the input rows (device, file order); scratch: a library buffer holding them, freed here
+static int finish_create(gc_graph* g, gc_graph** out, const int* src, int* scratch) {
+    int rc = gc_alloc_graph_common(g, src);
+    if (scratch) {
+        hipStreamSynchronize(g->stream);
+        gc_dfree(scratch);
+    }
     if (rc) {
         std::string keep = gc_last_error();
         gc_free_all(g);
@@ -350,40 +333,56 @@ static int finish_create(gc_graph* g, gc_graph** out) {
     return GC_OK;
 }
 
+static int alloc_scratch(gc_graph* g, int** p) {
+    if (gc_dmalloc((void**)p, sizeof(int) * (size_t)std::max<long long>(g->nnz, 1)) != hipSuccess) {
+        gc_free_all(g);
+        delete g;
+        gc_set_error("allocation of the input rows (%lld entries) failed", g->nnz);
+        return GC_ENOMEM;
+    }
+    return GC_OK;
+}
+
 extern "C" int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t nnz, uint32_t flags,
                                gc_graph** out) {
     if (!row_ptr || (nnz > 0 && !col)) { gc_set_error("gc_graph_create: null input"); return GC_EINVAL; }
-    if (row_ptr[0] != 0 || row_ptr[n] != nnz) { gc_set_error("gc_graph_create: row_ptr[0] != 0 or row_ptr[n] != nnz"); return GC_EINVAL; }
+    if (n < 0 || row_ptr[0] != 0 || row_ptr[n] != nnz) { gc_set_error("gc_graph_create: row_ptr[0] != 0 or row_ptr[n] != nnz"); return GC_EINVAL; }
     for (int64_t v = 0; v < n; ++v)
         if (row_ptr[v + 1] < row_ptr[v]) { gc_set_error("gc_graph_create: row_ptr not monotone at %lld", (long long)v); return GC_EINVAL; }
     gc_graph* g;
     int rc = new_graph(out, n, nnz, flags, &g);
     if (rc) return rc;
+    int* raw = nullptr;
+    if ((rc = alloc_scratch(g, &raw))) return rc;
     hipError_t e1 = hipMemcpy(g->rp, row_ptr, sizeof(long long) * (size_t)(n + 1), hipMemcpyHostToDevice);
-    hipError_t e2 = nnz ? hipMemcpy(g->col, col, sizeof(int) * (size_t)nnz, hipMemcpyHostToDevice) : hipSuccess;
+    hipError_t e2 = nnz ? hipMemcpy(raw, col, sizeof(int) * (size_t)nnz, hipMemcpyHostToDevice) : hipSuccess;
     if (e1 != hipSuccess || e2 != hipSuccess) {
         gc_set_error("H2D copy failed");
+        gc_dfree(raw);
         gc_free_all(g);
         delete g;
         return GC_EHIP;
     }
-    return finish_create(g, out);
+    return finish_create(g, out, raw, raw);
 }
 
+// The caller's device CSR is read in place (rp copied, col partitioned straight into the
+// graph's own array): no device-to-device copy of the rows.  The caller's buffers must stay
+// valid for the duration of the call only.
 extern "C" int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                                       uint32_t flags, gc_graph** out) {
+    if (!d_row_ptr || (nnz > 0 && !d_col)) { gc_set_error("gc_graph_create_device: null input"); return GC_EINVAL; }
     gc_graph* g;
     int rc = new_graph(out, n, nnz, flags, &g);
     if (rc) return rc;
-    hipError_t e1 = hipMemcpy(g->rp, d_row_ptr, sizeof(long long) * (size_t)(n + 1), hipMemcpyDeviceToDevice);
-    hipError_t e2 = nnz ? hipMemcpy(g->col, d_col, sizeof(int) * (size_t)nnz, hipMemcpyDeviceToDevice) : hipSuccess;
-    if (e1 != hipSuccess || e2 != hipSuccess) {
+    if (hipMemcpyAsync(g->rp, d_row_ptr, sizeof(long long) * (size_t)(n + 1), hipMemcpyDeviceToDevice, g->stream) !=
+        hipSuccess) {
         gc_set_error("D2D copy failed");
         gc_free_all(g);
         delete g;
         return GC_EHIP;
     }
-    return finish_create(g, out);
+    return finish_create(g, out, d_col, nullptr);
 }
 
 extern "C" int gc_graph_create_mesh(int64_t nx, int64_t ny, int64_t nz, gc_graph** out) {
@@ -393,19 +392,22 @@ extern "C" int gc_graph_create_mesh(int64_t nx, int64_t ny, int64_t nz, gc_graph
     gc_graph* g;
     int rc = new_graph(out, n, nnz, GC_GRAPH_SYMMETRIC, &g);
     if (rc) return rc;
+    int* raw = nullptr;
+    if ((rc = alloc_scratch(g, &raw))) return rc;
     long long* cnt = nullptr;
     if (hipMalloc((void**)&cnt, sizeof(long long) * (size_t)(n + 1)) != hipSuccess) {
-        gc_free_all(g); delete g; gc_set_error("mesh alloc failed"); return GC_ENOMEM;
+        gc_dfree(raw); gc_free_all(g); delete g; gc_set_error("mesh alloc failed"); return GC_ENOMEM;
     }
     hipLaunchKernelGGL(k_mesh_deg, dim3(grid_for(n)), dim3(GC_BLOCK), 0, g->stream, nx, ny, nz, cnt);
     rc = exclusive_scan_ll(cnt, g->rp, n + 1, g->stream);
     hipFree(cnt);
-    if (rc) { gc_free_all(g); delete g; return rc; }
-    hipLaunchKernelGGL(k_mesh_fill, dim3(grid_for(n)), dim3(GC_BLOCK), 0, g->stream, nx, ny, nz, g->rp, g->col);
-    if (hipStreamSynchronize(g->stream) != hipSuccess) { gc_free_all(g); delete g; gc_set_error("mesh fill failed"); return GC_EHIP; }
-    return finish_create(g, out);
+    if (rc) { gc_dfree(raw); gc_free_all(g); delete g; return rc; }
+    hipLaunchKernelGGL(k_mesh_fill, dim3(grid_for(n)), dim3(GC_BLOCK), 0, g->stream, nx, ny, nz, g->rp, raw);
+    if (hipStreamSynchronize(g->stream) != hipSuccess) { gc_dfree(raw); gc_free_all(g); delete g; gc_set_error("mesh fill failed"); return GC_EHIP; }
+    return finish_create(g, out, raw, raw);
 }
 
+// (the generator's key buffers are one-off: plain hipMalloc / hipFree, not the cache)
 extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a, double b, double c, uint64_t seed,
                                     gc_graph** out) {
     if (scale < 1 || scale > 30 || edge_factor < 1 || a < 0 || b < 0 || c < 0 || a + b + c > 1.0) {
@@ -422,6 +424,7 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
     ull *k0 = nullptr, *k1 = nullptr;
     size_t* d_count = nullptr;
     void* tmp = nullptr;
+    int* raw = nullptr;
     int rc = GC_OK;
     long long nuniq = 0, nnz = 0;
     gc_graph* g = nullptr;
@@ -462,7 +465,12 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
         tmp = nullptr;
         hipSetDevice(dev);
         if ((rc = new_graph(out, n, nnz, GC_GRAPH_SYMMETRIC, &g))) break;
-        hipLaunchKernelGGL(k_keys_to_csr, dim3(grid_for(nnz, 65536)), dim3(GC_BLOCK), 0, s, k0, nnz, (int)scale, g->col);
+        if (hipMalloc((void**)&raw, sizeof(int) * (size_t)std::max<long long>(nnz, 1)) != hipSuccess) {
+            gc_set_error("R-MAT rows (%lld entries) do not fit", nnz);
+            rc = GC_ENOMEM;
+            break;
+        }
+        hipLaunchKernelGGL(k_keys_to_csr, dim3(grid_for(nnz, 65536)), dim3(GC_BLOCK), 0, s, k0, nnz, (int)scale, raw);
         hipLaunchKernelGGL(k_row_bounds, dim3(grid_for(n + 1, 65536)), dim3(GC_BLOCK), 0, s, k0, nnz, (int)scale, n,
                            g->rp);
         if (hipStreamSynchronize(s) != hipSuccess) { gc_set_error("R-MAT CSR build failed"); rc = GC_EHIP; break; }
@@ -473,10 +481,13 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
     if (d_count) hipFree(d_count);
     hipStreamDestroy(s);
     if (rc) {
+        if (raw) hipFree(raw);
         if (g) { gc_free_all(g); delete g; }
         return rc;
     }
-    return finish_create(g, out);
+    rc = finish_create(g, out, raw, nullptr);
+    hipFree(raw);
+    return rc;
 }
 
 extern "C" void gc_graph_destroy(gc_graph* g) {
@@ -499,6 +510,17 @@ extern "C" int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col
     GC_HIP(hipSetDevice(g->device));
     if (row_ptr) GC_HIP(hipMemcpy(row_ptr, g->rp, sizeof(long long) * (size_t)(g->n + 1), hipMemcpyDeviceToHost));
     if (col && g->nnz) GC_HIP(hipMemcpy(col, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToHost));
+    return GC_OK;
+}
+
+extern "C" int gc_graph_export_device(const gc_graph* g, int64_t* d_row_ptr, int32_t* d_col) {
+    if (!g) { gc_set_error("null graph"); return GC_EINVAL; }
+    GC_HIP(hipSetDevice(g->device));
+    if (d_row_ptr)
+        GC_HIP(hipMemcpyAsync(d_row_ptr, g->rp, sizeof(long long) * (size_t)(g->n + 1), hipMemcpyDeviceToDevice, g->stream));
+    if (d_col && g->nnz)
+        GC_HIP(hipMemcpyAsync(d_col, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, g->stream));
+    GC_HIP(hipStreamSynchronize(g->stream));
     return GC_OK;
 }
 

@@ -134,10 +134,10 @@ int scan_ll(const long long* in, long long* out, long long count, hipStream_t s)
     size_t bytes = 0;
     GC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s));
     void* tmp = nullptr;
-    GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+    GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
     hipStreamSynchronize(s);
-    hipFree(tmp);
+    gc_dfree(tmp);
     GC_HIP(e);
     return GC_OK;
 }
@@ -159,15 +159,15 @@ int build(gc_graph* g, int T, int W) {
     hipStream_t s = g->stream;
     const long long n = g->n;
     long long *pos = nullptr, *flag = nullptr;
-    GC_HIP(hipMalloc((void**)&pos, sizeof(long long) * (size_t)(n + 1)));
-    GC_HIP(hipMalloc((void**)&flag, sizeof(long long) * (size_t)(n + 1)));
+    GC_HIP(gc_dmalloc((void**)&pos, sizeof(long long) * (size_t)(n + 1)));
+    GC_HIP(gc_dmalloc((void**)&flag, sizeof(long long) * (size_t)(n + 1)));
     hipLaunchKernelGGL(k_hub_flag, dim3(grid_of(n + 1)), dim3(GC_BLOCK), 0, s, g->deg, n, T, flag);
     int rc = scan_ll(flag, pos, n + 1, s);
-    hipFree(flag);
+    gc_dfree(flag);
     long long H = 0;
     if (!rc && hipMemcpy(&H, pos + n, sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess) rc = GC_EHIP;
     if (rc || H == 0) {
-        hipFree(pos);
+        gc_dfree(pos);
         g->hub_t = T;
         g->nhub = 0;
         return rc;
@@ -175,103 +175,123 @@ int build(gc_graph* g, int T, int W) {
     // memory: hid/hub_v, the hub transpose (one entry per hub-row entry), bitmaps, blockers
     size_t freeb = 0, totalb = 0;
     hipMemGetInfo(&freeb, &totalb);
+    freeb += gc_cache_idle_bytes();
     const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (28.0 + 4.0 * W) * (double)H;
     if (need > 0.5 * (double)freeb) {  // no room: row scans as before
-        hipFree(pos);
+        gc_dfree(pos);
         g->hub_t = T;
         g->nhub = 0;
         return GC_OK;
     }
     g->nhub = H;
-    GC_HIP(hipMalloc((void**)&g->hid, sizeof(int) * (size_t)std::max<long long>(n, 1)));
-    GC_HIP(hipMalloc((void**)&g->hub_v, sizeof(int) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hid, sizeof(int) * (size_t)std::max<long long>(n, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hub_v, sizeof(int) * (size_t)H));
     hipLaunchKernelGGL(k_hub_ids, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, g->deg, n, T, pos, g->hid, g->hub_v);
     {  // re-index the hubs in rank order
         ull *k0 = nullptr, *k1 = nullptr;
-        GC_HIP(hipMalloc((void**)&k0, sizeof(ull) * (size_t)H));
-        GC_HIP(hipMalloc((void**)&k1, sizeof(ull) * (size_t)H));
+        GC_HIP(gc_dmalloc((void**)&k0, sizeof(ull) * (size_t)H));
+        GC_HIP(gc_dmalloc((void**)&k1, sizeof(ull) * (size_t)H));
         hipLaunchKernelGGL(k_hub_keys, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, g->deg, g->hub_v, H, k0);
         size_t bytes = 0;
         GC_HIP(rocprim::radix_sort_keys(nullptr, bytes, k0, k1, (size_t)H, 0, 64, s));
         void* tmp = nullptr;
-        GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+        GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
         const hipError_t e = rocprim::radix_sort_keys(tmp, bytes, k0, k1, (size_t)H, 0, 64, s);
         if (e == hipSuccess)
             hipLaunchKernelGGL(k_hub_reindex, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const ull*)k1, H, g->hid, g->hub_v);
         hipStreamSynchronize(s);
-        hipFree(tmp);
-        hipFree(k0);
-        hipFree(k1);
+        gc_dfree(tmp);
+        gc_dfree(k0);
+        gc_dfree(k1);
         GC_HIP(e);
     }
-    // hub transpose: reuse pos as the per-target counter
-    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
     const int hgrid = (int)std::max<long long>(1, std::min<long long>((H + 3) / 4, 8192));
-    hipLaunchKernelGGL(k_hub_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, (ull*)pos);
-    GC_HIP(hipMalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
-    if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { hipFree(pos); return rc; }
-    long long E = 0;
+    long long E = 0, EL = 0;
+    const bool sym = (g->flags & GC_GRAPH_SYMMETRIC) != 0;
+    long long* klow = nullptr;
+    if (sym) {
+        // symmetric: every row filtered for its hub entries (gc_prep.hip, edge-balanced tiles):
+        // hin counts into pos, each hub row's lower-rank hubs (a prefix of its hin row) into klow
+        GC_HIP(gc_dmalloc((void**)&klow, sizeof(long long) * (size_t)(H + 1)));
+        if ((rc = gc_hub_transpose_sym(g, H, pos, klow))) { gc_dfree(pos); gc_dfree(klow); return rc; }
+    } else {
+        // hub transpose: reuse pos as the per-target counter
+        GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
+        hipLaunchKernelGGL(k_hub_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, (ull*)pos);
+    }
+    GC_HIP(gc_dmalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
+    if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { gc_dfree(pos); gc_dfree(klow); return rc; }
     GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
     hipMemGetInfo(&freeb, &totalb);
+    freeb += gc_cache_idle_bytes();
     const double need2 = 24.0 * (double)E + (28.0 + 4.0 * W) * (double)H;  // hin + hlow copies <= 5 E
     if (need2 > 0.6 * (double)freeb) {
-        hipFree(pos);
+        gc_dfree(pos);
+        gc_dfree(klow);
         gc_hubs_free(g);
         g->hub_t = T;
         g->nhub = 0;
         return GC_OK;
     }
-    GC_HIP(hipMalloc((void**)&g->hin_col, sizeof(int) * (size_t)std::max<long long>(E, 1)));
-    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
-    hipLaunchKernelGGL(k_hub_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, g->hin_rp,
-                       (ull*)pos, g->hin_col);
-    GC_HIP(hipMalloc((void**)&g->hbits, sizeof(unsigned) * (size_t)H * W));
-    GC_HIP(hipMalloc((void**)&g->hkill, sizeof(unsigned) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hcur, sizeof(int) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hpc, sizeof(int) * (size_t)H));
-
-    // lower-rank hubs of each hub row (pos reused: H + 1 counts)
-    GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
-    hipLaunchKernelGGL(k_hlow_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
-                       pos);
-    GC_HIP(hipMalloc((void**)&g->hlow_rp, sizeof(long long) * (size_t)(H + 1)));
-    if ((rc = scan_ll(pos, g->hlow_rp, H + 1, s))) { hipFree(pos); return rc; }
-    long long EL = 0;
+    GC_HIP(gc_dmalloc((void**)&g->hin_col, sizeof(int) * (size_t)std::max<long long>(E, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hbits, sizeof(unsigned) * (size_t)H * W));
+    GC_HIP(gc_dmalloc((void**)&g->hkill, sizeof(unsigned) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hcur, sizeof(int) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hpc, sizeof(int) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hlow_rp, sizeof(long long) * (size_t)(H + 1)));
+    if (sym) {
+        rc = scan_ll(klow, g->hlow_rp, H + 1, s);
+        gc_dfree(klow);
+        if (rc) { gc_dfree(pos); return rc; }
+    } else {
+        GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
+        hipLaunchKernelGGL(k_hub_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, g->hin_rp,
+                           (ull*)pos, g->hin_col);
+        // lower-rank hubs of each hub row (pos reused: H + 1 counts)
+        GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
+        hipLaunchKernelGGL(k_hlow_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v,
+                           H, pos);
+        if ((rc = scan_ll(pos, g->hlow_rp, H + 1, s))) { gc_dfree(pos); return rc; }
+    }
     GC_HIP(hipMemcpy(&EL, g->hlow_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
-    GC_HIP(hipMalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
-    GC_HIP(hipMalloc((void**)&g->hpend[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
-    GC_HIP(hipMalloc((void**)&g->hpend[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
-    GC_HIP(hipMalloc((void**)&g->hlow2[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
-    GC_HIP(hipMalloc((void**)&g->hlow2[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
-    GC_HIP(hipMalloc((void**)&g->hrow, sizeof(int) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hlen, sizeof(int) * (size_t)H));
-    hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v, H,
-                       g->hlow_rp, g->hlow_col);
+    GC_HIP(gc_dmalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hpend[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hpend[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hlow2[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hlow2[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hrow, sizeof(int) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hlen, sizeof(int) * (size_t)H));
+    if (sym) {
+        if ((rc = gc_hub_transpose_fill(g, H))) { gc_dfree(pos); return rc; }
+    } else {
+        hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v,
+                           H, g->hlow_rp, g->hlow_col);
+    }
     if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
         size_t bytes = 0;
         GC_HIP(rocprim::segmented_radix_sort_keys(nullptr, bytes, g->hlow_col, g->hpend[0], (unsigned)EL, (unsigned)H,
                                                   g->hlow_rp, g->hlow_rp + 1, 0, 32, s));
         void* tmp = nullptr;
-        GC_HIP(hipMalloc(&tmp, bytes ? bytes : 1));
+        GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
         const hipError_t e = rocprim::segmented_radix_sort_keys(tmp, bytes, g->hlow_col, g->hpend[0], (unsigned)EL,
                                                                 (unsigned)H, g->hlow_rp, g->hlow_rp + 1, 0, 32, s);
         hipStreamSynchronize(s);
-        hipFree(tmp);
+        gc_dfree(tmp);
         GC_HIP(e);
         std::swap(g->hlow_col, g->hpend[0]);  // the unsorted copy becomes working memory
     }
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
     hipLaunchKernelGGL(k_hch_count, dim3(grid_of(H + 1)), dim3(GC_BLOCK), 0, s, g->hlow_rp, H, pos);
-    GC_HIP(hipMalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
-    if ((rc = scan_ll(pos, g->hch_rp, H + 1, s))) { hipFree(pos); return rc; }
+    GC_HIP(gc_dmalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
+    if ((rc = scan_ll(pos, g->hch_rp, H + 1, s))) { gc_dfree(pos); return rc; }
     GC_HIP(hipMemcpy(&g->nhch, g->hch_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
-    GC_HIP(hipMalloc((void**)&g->hch_own, sizeof(int) * (size_t)std::max<long long>(g->nhch, 1)));
-    GC_HIP(hipMalloc((void**)&g->hkcnt, sizeof(int) * (size_t)H));
-    GC_HIP(hipMalloc((void**)&g->hk, sizeof(unsigned) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hch_own, sizeof(int) * (size_t)std::max<long long>(g->nhch, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hkcnt, sizeof(int) * (size_t)H));
+    GC_HIP(gc_dmalloc((void**)&g->hk, sizeof(unsigned) * (size_t)H));
     hipLaunchKernelGGL(k_hch_fill, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, g->hch_rp, H, g->hch_own);
     GC_HIP(hipGetLastError());
     GC_HIP(hipStreamSynchronize(s));
-    hipFree(pos);
+    gc_dfree(pos);
     g->hub_t = T;
     g->hub_w = W;
     return GC_OK;
@@ -284,7 +304,7 @@ void gc_hubs_free(gc_graph* g) {
                     g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen,
                     g->hch_rp, g->hch_own, g->hkcnt, g->hk};
     for (void* p : ptrs)
-        if (p) hipFree(p);
+        if (p) gc_dfree(p);
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
     g->hlow2[0] = g->hlow2[1] = g->hrow = g->hlen = nullptr;
     g->hin_rp = g->hlow_rp = g->hch_rp = nullptr;

@@ -363,3 +363,13 @@ __device__ __forceinline__ bool gc_rank_lt(int du, int u, int dv, int v) {
 __device__ __forceinline__ bool gc_rank_lt_key(unsigned ku, int u, unsigned kv, int v) {
     return ku < kv || (ku == kv && u < v);
 }
+
+// seeded 32-bit priority: the top half of splitmix64(seed + (v + 1) * golden gamma)
+// (identical to prio_hash in oracle/gcolor_oracle.c)
+__device__ __forceinline__ unsigned gc_prio_hash(ull seed, long long v) {
+    ull z = seed + 0x9E3779B97F4A7C15ull * (ull)(v + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (unsigned)(z >> 32);
+}

@@ -2446,60 +2446,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_cc_seeds(GDev g, const int* list, 
 // ------------------------------------------------------------------------------------
 // validate_graph_coloring counts (coloring.py:149-162)
 // ------------------------------------------------------------------------------------
-// Rows longer than GC_HEAVY_T are left to k_validate_heavy (listed in `heavy`): one wave
-// walking a 10^5-entry hub row would hold the whole launch.
-__global__ void __launch_bounds__(GC_BLOCK) k_validate(GDev g, const int* __restrict__ colors, int* heavy) {
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_c[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
-    const int lane = gc_lane();
-    const int w = threadIdx.x / GC_WAVE;
-    ull unc = 0, conf = 0;
-    const long long nchunks = ((long long)g.n + GC_WAVE - 1) / GC_WAVE;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long v = chunk * GC_WAVE + lane;
-        const bool valid = v < g.n;
-        const int dv = valid ? g.deg[v] : 0;
-        gc_wave_append(dv > GC_HEAVY_T, (int)v, heavy, &g.ctl->list_cnt);
-        const int d = dv > GC_HEAVY_T ? 0 : dv;
-        const int cv = valid ? colors[v] : 0;
-        if (valid && cv == -1) unc++;
-        s_start[w][lane] = valid ? g.rp[v] : 0;
-        s_c[w][lane] = cv;
-        const int incl = gc_wave_incl_scan(d);
-        const int excl = incl - d;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        gc_chunk_edges(
-            g.col, s_start[w], excl, total, [&](int u) { return colors[u]; },
-            [&](int o, int, int cu) {
-                if (cu == s_c[w][o]) conf++;
-            });
-        gc_wave_sync();
-    }
-    __syncthreads();
-    gc_block_add(&g.ctl->uncolored, unc, scratch);
-    gc_block_add(&g.ctl->conflicts, conf, scratch);
-}
-
-__global__ void __launch_bounds__(GC_BLOCK) k_validate_heavy(GDev g, const int* __restrict__ colors,
-                                                             const int* heavy) {
-    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
-    const long long nh = (long long)g.ctl->list_cnt;
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    ull conf = 0;
-    for (long long j = 0; j < nh; ++j) {
-        const int v = heavy[j];
-        const int cv = colors[v];
-        const long long e1 = g.rp[v + 1];
-        for (long long e = g.rp[v] + (long long)blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += stride)
-            conf += colors[g.col[e]] == cv;
-    }
-    __syncthreads();
-    gc_block_add(&g.ctl->conflicts, conf, scratch);
-}
-
 // Final colours from the byte mirror (colours >= 254 were stored directly).
 __global__ void __launch_bounds__(GC_BLOCK) k_finalize(GDev g) {
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < g.n;
@@ -2512,117 +2458,25 @@ __global__ void __launch_bounds__(GC_BLOCK) k_finalize(GDev g) {
 // ------------------------------------------------------------------------------------
 // graph helpers
 // ------------------------------------------------------------------------------------
-// Mark every adjacency entry whose neighbour does NOT rank below the row's vertex
-// (bit 31 of col; rank = (key, pos): key = deg for the reference's coloring.py:64, or a
-// seeded priority, gc_priority.hip) and count the lower ones; k_partition_rows then lists
-// lower-rank neighbours first (gc_graph.hip).
-__global__ void __launch_bounds__(GC_BLOCK) k_rank_flags(const long long* rp, int* col, const unsigned* key, int n,
-                                                         int* nlow) {
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_cnt[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ unsigned s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
-    const int lane = gc_lane();
-    const int w = threadIdx.x / GC_WAVE;
-    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long v = chunk * GC_WAVE + lane;
-        const bool valid = v < n;
-        const int d = valid ? (int)(rp[v + 1] - rp[v]) : 0;
-        s_start[w][lane] = valid ? rp[v] : 0;
-        s_cnt[w][lane] = 0;
-        s_v[w][lane] = (int)v;
-        s_d[w][lane] = valid ? key[v] : 0u;
-        const int incl = gc_wave_incl_scan(d);
-        const int excl = incl - d;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) {
-                const long long ei = s_start[w][o] + (e - eo);
-                const int u = col[ei];
-                const bool lower = gc_rank_lt_key(key[u], u, s_d[w][o], s_v[w][o]);
-                if (lower) atomicAdd(&s_cnt[w][o], 1);
-                else col[ei] = (int)((unsigned)u | 0x80000000u);
-            }
-        }
-        gc_wave_sync();
-        if (valid) nlow[v] = s_cnt[w][lane];
-    }
-}
-
-// Stable partition of every row on the mark left by k_rank_flags (lower-rank entries
-// first), written to `out` with the marks cleared.  Each 64-slot step ranks a lane among
-// the same-owner, same-side lanes before it with a ballot; running counts per row live
-// in LDS.  Deterministic; rows of any length (a wave walks its 64 rows' edges).
-// Row v's range is [rp[v], rp[v] + len[v]); its unmarked entries go first, the marked ones
-// from rp[v] + split[v] (len = deg, split = nlow: the rank partition; variant B also splits
-// the low parts, gc_variant_b.hip).
-__global__ void __launch_bounds__(GC_BLOCK) k_partition_rows(const long long* rp, const int* col, const int* len,
-                                                             const int* split, int n, int* out) {
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ long long s_lo[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ long long s_hi[GC_WAVES_PER_BLOCK][GC_WAVE];
-    const int lane = gc_lane();
-    const int w = threadIdx.x / GC_WAVE;
-    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long v = chunk * GC_WAVE + lane;
-        const bool valid = v < n;
-        const int d = valid ? len[v] : 0;
-        const long long st = valid ? rp[v] : 0;
-        s_start[w][lane] = st;
-        s_lo[w][lane] = st;
-        s_hi[w][lane] = st + (valid ? split[v] : 0);
-        const int incl = gc_wave_incl_scan(d);
-        const int excl = incl - d;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            const bool ok = e < total;
-            unsigned u = 0;
-            if (ok) u = (unsigned)col[s_start[w][o] + (e - eo)];
-            const bool upper = ok && (u & 0x80000000u);
-            const bool lower = ok && !upper;
-            const ull mlo = __ballot(lower), mhi = __ballot(upper);
-            // lanes of owner o in this step: [max(eo - base, 0), lane]
-            const int first = eo - base > 0 ? eo - base : 0;
-            const ull seg = gc_lanemask_lt() & ~((1ull << first) - 1ull);
-            if (ok) {
-                if (lower) out[s_lo[w][o] + __popcll(mlo & seg)] = (int)u;
-                else out[s_hi[w][o] + __popcll(mhi & seg)] = (int)(u & 0x7FFFFFFFu);
-            }
-            // the last lane of each owner's run in this step advances its counters
-            const int onext = __shfl_down(o, 1, GC_WAVE);
-            const bool last = ok && (lane == GC_WAVE - 1 || e + 1 >= total || onext != o);
-            gc_wave_sync();
-            if (last) {
-                const ull own = seg | (1ull << lane);
-                s_lo[w][o] += __popcll(mlo & own);
-                s_hi[w][o] += __popcll(mhi & own);
-            }
-            gc_wave_sync();
-        }
-    }
-}
-
-__global__ void k_degrees(const long long* rp, int n, int* deg, ull* maxdeg) {
-    ull m = 0;
+// deg, its byte key kb = min(deg, 255) (the rank partition gathers it first: gc_prep.hip),
+// the max degree; *bad counts violations of the CSR offset contract
+__global__ void k_degrees(const long long* rp, int n, long long nnz, int* deg, unsigned char* kb, ull* maxdeg, ull* bad) {
+    ull m = 0, b = 0;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
         const long long d = rp[v + 1] - rp[v];
         deg[v] = (int)d;
-        m = (ull)d > m ? (ull)d : m;
+        kb[v] = (unsigned char)(d < 255 ? (d < 0 ? 0 : d) : 255);
+        m = (d > 0 && (ull)d > m) ? (ull)d : m;
+        b += d < 0;
+        if (v == 0) b += rp[0] != 0;
+        if (v == n - 1) b += rp[n] != nnz;
     }
     m = gc_wave_max(m);
-    if (gc_lane() == 0 && m) atomicMax(maxdeg, m);
+    b = gc_wave_sum(b);
+    if (gc_lane() == 0) {
+        if (m) atomicMax(maxdeg, m);
+        if (b) atomicAdd(bad, b);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2794,18 +2648,7 @@ void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, c
                   int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best, sl, sh);
 }
-void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStream_t s) {
-    hipMemsetAsync(&g.ctl->list_cnt, 0, sizeof(ull), s);
-    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, heavy);
-    hipLaunchKernelGGL(k_validate_heavy, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, colors, (const int*)heavy);
-}
-void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_rank_flags, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, key, n, nlow);
-}
-void gcl_partition_rows(const long long* rp, const int* col, const int* len, const int* split, int n, int* out,
-                        int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_partition_rows, dim3(grid), dim3(GC_BLOCK), 0, s, rp, col, len, split, n, out);
-}
-void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, deg, maxdeg);
+void gcl_degrees(const long long* rp, int n, long long nnz, int* deg, unsigned char* kb, ull* maxdeg, ull* bad, int grid,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, nnz, deg, kb, maxdeg, bad);
 }

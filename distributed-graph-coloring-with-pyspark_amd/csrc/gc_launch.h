@@ -127,13 +127,10 @@ void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStrea
 // replicated hubs after a slice seam: the other ranks' light winners flag their hubs
 void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
-void gcl_rank_flags(const long long* rp, int* col, const unsigned* key, int n, int* nlow, int grid, hipStream_t s);
-void gcl_partition_rows(const long long* rp, const int* col, const int* len, const int* split, int n, int* out,
-                        int grid, hipStream_t s);
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);
 void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, const ull* best, int* sl, int* sh,
                   int grid, hipStream_t s);
-void gcl_validate(const GDev& g, const int* colors, int* heavy, int grid, hipStream_t s);
-void gcl_degrees(const long long* rp, int n, int* deg, ull* maxdeg, int grid, hipStream_t s);
+void gcl_degrees(const long long* rp, int n, long long nnz, int* deg, unsigned char* kb, ull* maxdeg, ull* bad, int grid,
+                 hipStream_t s);

@@ -1,0 +1,879 @@
+// gc_prep.hip -- the per-graph passes over every adjacency entry, edge-balanced:
+//   * the rank partition of every row (the (deg, pos) order of coloring.py:64: lower-rank
+//     neighbours first, so the Jones-Plassmann sweeps read only those),
+//   * validate_graph_coloring's counts (coloring.py:149-162),
+//   * the hub transpose of a symmetric graph (gc_hubs.hip: the hubs each row lists).
+// All three are HBM/L2-bound integer gather work (one coalesced read of col, one random
+// gather per entry, at most one coalesced write): no MFMA.
+//
+// Tiling.  The rows of R-MAT are power-law: a wave per 64 rows (round 2's kernels) walked
+// the 4e5-entry hub rows serially and set the time of the whole pass (rank partition
+// 133 + 99 ms, validation 65 ms on R-MAT-24).  Here the CSR is cut by merge path: tile t
+// holds the rows whose key rp[r] + r falls in [t*GC_TW, (t+1)*GC_TW) -- at most GC_TW
+// rows and, rows longer than GC_TH excepted, at most GC_TW + GC_TH entries, i.e. 16 per
+// thread of a 256-thread workgroup.  A row longer than GC_TH (at most one per tile, its
+// last) is cut into GC_SEG-entry segments handled like tiles; a pass that needs a row's
+// prefix across its segments runs in two launches (counts, then positions).  The tiling
+// depends on rp only: built once per graph.
+//
+// Within a tile the entries are staged in LDS with coalesced loads; thread t takes entries
+// [16t, 16t + 16), finds its first row by binary search over the tile's row offsets (LDS)
+// and walks on; its 16 gathers are issued together.  Per-row results come from ONE block
+// scan of packed per-thread counts: a row's prefix at its start (recorded by the thread
+// holding that start) and at its end give its counts and every entry's rank.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+#include "gc_device.h"
+#include "gc_engine.h"
+
+#define GC_TW 2048   // merge-path keys (rows + entries) per tile
+#define GC_TH 2048   // rows longer than this are split into segments
+#define GC_SEG 4096  // entries per segment
+#define GC_PER 16    // entries per thread: 256 x 16 = GC_TW + GC_TH = GC_SEG
+#define GC_PREP_GRID 4096
+
+static_assert(GC_BLOCK * GC_PER == GC_TW + GC_TH && GC_BLOCK * GC_PER == GC_SEG, "tile geometry");
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// tiling
+// ------------------------------------------------------------------------------------
+__global__ void k_tile_bounds(const long long* rp, long long n, long long ntiles, int* r0) {
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
+         t += (long long)gridDim.x * blockDim.x) {
+        if (t == ntiles) { r0[t] = (int)n; continue; }
+        const long long target = t * GC_TW;
+        long long lo = 0, hi = n;  // first r with rp[r] + r >= target (n if none)
+        while (lo < hi) {
+            const long long mid = (lo + hi) >> 1;
+            if (rp[mid] + mid < target) lo = mid + 1;
+            else hi = mid;
+        }
+        r0[t] = (int)lo;
+    }
+}
+
+__global__ void k_tile_nseg(const long long* rp, const int* r0, long long ntiles, long long* cnt) {
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
+         t += (long long)gridDim.x * blockDim.x) {
+        long long c = 0;
+        if (t < ntiles) {
+            const int a = r0[t], b = r0[t + 1];
+            if (b > a) {
+                const long long d = rp[b] - rp[b - 1];
+                if (d > GC_TH) c = (d + GC_SEG - 1) / GC_SEG;
+            }
+        }
+        cnt[t] = c;
+    }
+}
+
+__global__ void k_tile_segs(const int* r0, long long ntiles, const long long* base, int* seg_row, int* seg_j) {
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
+         t += (long long)gridDim.x * blockDim.x) {
+        const long long b0 = base[t], b1 = base[t + 1];
+        if (b1 > b0) {
+            const int v = r0[t + 1] - 1;
+            for (long long j = 0; j < b1 - b0; ++j) {
+                seg_row[b0 + j] = v;
+                seg_j[b0 + j] = (int)j;
+            }
+        }
+    }
+}
+
+struct Tiles {
+    const long long* rp;
+    const int* r0;
+    long long ntiles;
+    const long long* seg_base;  // [ntiles] = segment count
+    const int* seg_row;
+    const int* seg_j;
+    int n;
+};
+
+__device__ __forceinline__ long long nseg_of(const Tiles& T) { return T.seg_base[T.ntiles]; }
+
+// ------------------------------------------------------------------------------------
+// block helpers
+// ------------------------------------------------------------------------------------
+// exclusive scan of a packed 64-bit count over the workgroup; *total = the sum
+__device__ __forceinline__ ull block_excl_scan(ull x, ull* s_w, ull* total) {
+    const int lane = gc_lane(), w = threadIdx.x / GC_WAVE;
+    ull incl = x;
+#pragma unroll
+    for (int o = 1; o < GC_WAVE; o <<= 1) {
+        const ull y = __shfl_up(incl, o, GC_WAVE);
+        if (lane >= o) incl += y;
+    }
+    if (lane == GC_WAVE - 1) s_w[w] = incl;
+    __syncthreads();
+    ull pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) {
+        pre += i < w ? s_w[i] : 0ull;
+        tot += s_w[i];
+    }
+    *total = tot;
+    __syncthreads();
+    return pre + incl - x;
+}
+
+__device__ __forceinline__ ull block_sum(ull x, ull* s_w) {
+    ull t;
+    block_excl_scan(x, s_w, &t);
+    return t;
+}
+
+// packed class counts: 16 bits per class (a tile or segment holds <= 4096 entries)
+__device__ __forceinline__ unsigned f16(ull p, int c) { return (unsigned)((p >> (16 * c)) & 0xFFFFull); }
+__device__ __forceinline__ ull pack3(unsigned a, unsigned b, unsigned c) {
+    return (ull)a | ((ull)b << 16) | ((ull)c << 32);
+}
+// counts of this thread's entries [0, x) per class, from its 16-bit class masks
+__device__ __forceinline__ ull own_before(unsigned m0, unsigned m1, unsigned m2, int x) {
+    const unsigned lt = x >= 32 ? 0xFFFFFFFFu : ((1u << x) - 1u);
+    return pack3(__popc(m0 & lt), __popc(m1 & lt), __popc(m2 & lt));
+}
+
+// Tile rows into LDS: offsets relative to the first entry; returns R (rows) and sets *e_beg,
+// *NE (light entries: the last row excluded when it is heavy), *heavy_last.
+struct TileLds {
+    int off[GC_TW + 1];
+    unsigned key[GC_TW];     // per-row word of the pass (owner key / colour / nlow)
+    int aux[GC_TW];          // second per-row word (hub index)
+    ull base[GC_TW + 1];     // packed prefix at each row's start
+    int buf[GC_TW + GC_TH];  // staged entries, then the pass's output
+    ull w[GC_WAVES_PER_BLOCK];
+    ull misc[4];
+};
+
+__device__ __forceinline__ int tile_rows(const Tiles& T, long long t, TileLds& S, int* r0o, long long* e_beg, int* NE,
+                                         bool* heavy_last) {
+    const int r0 = T.r0[t], r1 = T.r0[t + 1];
+    const int R = r1 - r0;
+    *r0o = r0;
+    if (R == 0) return 0;
+    const long long eb = T.rp[r0];
+    for (int i = threadIdx.x; i <= R; i += blockDim.x) S.off[i] = (int)(T.rp[r0 + i] - eb);
+    __syncthreads();
+    const bool hl = S.off[R] - S.off[R - 1] > GC_TH;
+    *e_beg = eb;
+    *NE = hl ? S.off[R - 1] : S.off[R];
+    *heavy_last = hl;
+    return R;
+}
+
+// this thread's entries [j0, j0 + nv) of the staged tile, with their rows
+__device__ __forceinline__ int thread_entries(const TileLds& S, int R, int NE, int* u, int* rk) {
+    const int j0 = threadIdx.x * GC_PER;
+    int nv = NE - j0;
+    nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
+    if (nv == 0) return 0;
+    int lo = 0, hi = R - 1;  // last r with off[r] <= j0
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (S.off[mid] <= j0) lo = mid;
+        else hi = mid - 1;
+    }
+    int r = lo;
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        if (k < nv) {
+            const int j = j0 + k;
+            while (S.off[r + 1] <= j) ++r;
+            rk[k] = r;
+            u[k] = S.buf[j];
+        } else {
+            rk[k] = 0;
+            u[k] = 0;
+        }
+    }
+    return nv;
+}
+
+// Row bases: the thread holding a row's first entry records prefix + its own entries before
+// it; rows starting at or past NE get the total.  Then base[R] = total.
+__device__ __forceinline__ void record_bases(TileLds& S, int R, int NE, int nv, ull prefix, ull total, unsigned m0,
+                                             unsigned m1, unsigned m2) {
+    const int j0 = threadIdx.x * GC_PER;
+    if (nv > 0) {
+        int lo = 0, hi = R;  // first r with off[r] >= j0
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (S.off[mid] < j0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int r = lo; r < R && S.off[r] < j0 + nv; ++r) S.base[r] = prefix + own_before(m0, m1, m2, S.off[r] - j0);
+    }
+    for (int r = threadIdx.x; r <= R; r += blockDim.x)
+        if (S.off[r] >= NE) S.base[r] = total;
+}
+
+// ------------------------------------------------------------------------------------
+// rank partition
+// ------------------------------------------------------------------------------------
+struct PartArgs {
+    Tiles T;
+    const int* src;
+    int* dst;
+    const int* deg;
+    const unsigned char* kb;
+    int* nlow;
+    int* neq;
+    ull seed;
+    ull* bad;
+    ull* seg_aux;       // per segment: packed class counts
+    unsigned* seg_cls;  // per segment x thread: 2-bit classes
+};
+
+__device__ __forceinline__ unsigned owner_key(const PartArgs& a, int prio, int v) {
+    return prio ? gc_prio_hash(a.seed, v) : (unsigned)a.deg[v];
+}
+
+// classes of this thread's entries against their owners' keys: 0 lower key, 1 equal key and
+// earlier position, 2 the rest (higher rank, self-loops, out-of-range entries)
+template <int PRIO>
+__device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u, const unsigned* kv, const int* v,
+                                         unsigned* m0, unsigned* m1, unsigned* m2, ull* nbad) {
+    int cls[GC_PER];
+    if (PRIO) {
+#pragma unroll
+        for (int k = 0; k < GC_PER; ++k) {
+            cls[k] = 3;
+            if (k < nv) {
+                if ((unsigned)u[k] >= (unsigned)a.T.n) { cls[k] = 2; ++*nbad; continue; }
+                const unsigned ku = gc_prio_hash(a.seed, u[k]);
+                cls[k] = gc_rank_lt_key(ku, u[k], kv[k], v[k]) ? 0 : 2;
+            }
+        }
+    } else {
+        // the byte key first (min(deg, 255): 16.8 MB against 67 MB of deg on R-MAT-24), the
+        // full degree only when both bytes saturate
+        unsigned kb8[GC_PER];
+#pragma unroll
+        for (int k = 0; k < GC_PER; ++k) {
+            const bool ok = k < nv && (unsigned)u[k] < (unsigned)a.T.n;
+            kb8[k] = ok ? (unsigned)a.kb[u[k]] : 0u;
+        }
+        bool full[GC_PER];
+        bool any_full = false;
+#pragma unroll
+        for (int k = 0; k < GC_PER; ++k) {
+            full[k] = false;
+            cls[k] = 3;
+            if (k < nv) {
+                if ((unsigned)u[k] >= (unsigned)a.T.n) { cls[k] = 2; ++*nbad; continue; }
+                const unsigned kv8 = kv[k] < 255u ? kv[k] : 255u;
+                if (kb8[k] != kv8) cls[k] = kb8[k] < kv8 ? 0 : 2;
+                else if (kv8 < 255u) cls[k] = u[k] < v[k] ? 1 : 2;
+                else { full[k] = true; any_full = true; }
+            }
+        }
+        if (any_full) {
+            unsigned du[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) du[k] = full[k] ? (unsigned)a.deg[u[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k)
+                if (full[k]) cls[k] = du[k] < kv[k] ? 0 : (du[k] > kv[k] ? 2 : (u[k] < v[k] ? 1 : 2));
+        }
+    }
+    unsigned a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        a0 |= (cls[k] == 0 ? 1u : 0u) << k;
+        a1 |= (cls[k] == 1 ? 1u : 0u) << k;
+        a2 |= (cls[k] == 2 ? 1u : 0u) << k;
+    }
+    *m0 = a0;
+    *m1 = a1;
+    *m2 = a2;
+}
+
+template <int PRIO>
+__device__ void part_tile(const PartArgs& a, TileLds& S, long long t, ull* nbad) {
+    int r0, NE;
+    long long eb;
+    bool hl;
+    const int R = tile_rows(a.T, t, S, &r0, &eb, &NE, &hl);
+    if (R == 0) return;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) S.key[i] = owner_key(a, PRIO, r0 + i);
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = a.src[eb + i];
+    __syncthreads();
+    int u[GC_PER], rk[GC_PER];
+    const int nv = thread_entries(S, R, NE, u, rk);
+    unsigned kv[GC_PER];
+    int vv[GC_PER];
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        kv[k] = S.key[rk[k]];
+        vv[k] = r0 + rk[k];
+    }
+    unsigned m0, m1, m2;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad);
+    const ull mine = pack3(__popc(m0), __popc(m1), __popc(m2));
+    ull total;
+    const ull prefix = block_excl_scan(mine, S.w, &total);  // (its barriers: every S.buf read is done)
+    record_bases(S, R, NE, nv, prefix, total, m0, m1, m2);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        if (k >= nv) break;
+        const int r = rk[k];
+        const ull b = S.base[r], b1 = S.base[r + 1];
+        const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1);
+        const unsigned bit = 1u << k;
+        const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : 2);
+        const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
+        const unsigned rank = f16(prefix, c) + __popc(mc & (bit - 1u)) - f16(b, c);
+        const unsigned start = c == 0 ? 0u : (c == 1 ? c0 : c0 + c1);
+        S.buf[S.off[r] + (int)(start + rank)] = u[k];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) a.dst[eb + i] = S.buf[i];
+    for (int r = threadIdx.x; r < R; r += blockDim.x) {
+        if (hl && r == R - 1) continue;  // the heavy row: its segments' second pass
+        const ull b = S.base[r], b1 = S.base[r + 1];
+        const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1);
+        a.nlow[r0 + r] = (int)(c0 + c1);
+        if (a.neq) a.neq[r0 + r] = (int)c1;
+    }
+}
+
+// segment of a heavy row, first pass: classes (kept for the second pass) and counts
+template <int PRIO>
+__device__ void part_seg1(const PartArgs& a, TileLds& S, long long s, ull* nbad) {
+    const int v = a.T.seg_row[s], j = a.T.seg_j[s];
+    const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
+    const long long e0 = rs + (long long)j * GC_SEG;
+    const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+    const unsigned key = owner_key(a, PRIO, v);
+    for (int i = threadIdx.x; i < len; i += blockDim.x) S.buf[i] = a.src[e0 + i];
+    __syncthreads();
+    const int j0 = threadIdx.x * GC_PER;
+    int nv = len - j0;
+    nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
+    int u[GC_PER], vv[GC_PER];
+    unsigned kv[GC_PER];
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        u[k] = k < nv ? S.buf[j0 + k] : 0;
+        vv[k] = v;
+        kv[k] = key;
+    }
+    unsigned m0, m1, m2;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad);
+    unsigned cls = 0;
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) cls |= (((m1 >> k) & 1u) | (((m2 >> k) & 1u) << 1)) << (2 * k);
+    a.seg_cls[s * GC_BLOCK + threadIdx.x] = cls;
+    const ull tot = block_sum(pack3(__popc(m0), __popc(m1), __popc(m2)), S.w);
+    if (threadIdx.x == 0) a.seg_aux[s] = tot;
+}
+
+template <int PRIO>
+__global__ void __launch_bounds__(GC_BLOCK) k_part1(PartArgs a) {
+    __shared__ TileLds S;
+    const long long nt = a.T.ntiles, ns = nseg_of(a.T);
+    ull nbad = 0;
+    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
+        if (it < nt) part_tile<PRIO>(a, S, it, &nbad);
+        else part_seg1<PRIO>(a, S, it - nt, &nbad);
+        __syncthreads();
+    }
+    nbad = gc_wave_sum(nbad);
+    if (gc_lane() == 0 && nbad) atomicAdd(a.bad, nbad);
+}
+
+// sums over segments [f, l) of a row's packed counts, per class (one wave, lane-strided)
+__device__ __forceinline__ void seg_sums(const ull* aux, long long f, long long l, ull* c) {
+    ull a0 = 0, a1 = 0, a2 = 0;
+    for (long long i = f + gc_lane(); i < l; i += GC_WAVE) {
+        const ull p = aux[i];
+        a0 += f16(p, 0);
+        a1 += f16(p, 1);
+        a2 += f16(p, 2);
+    }
+    c[0] = gc_wave_sum(a0);
+    c[1] = gc_wave_sum(a1);
+    c[2] = gc_wave_sum(a2);
+}
+
+// second pass of the heavy rows: every segment places its entries after the row's earlier
+// segments' entries of the same class
+__global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
+    __shared__ int buf[GC_SEG];
+    __shared__ ull s_w[GC_WAVES_PER_BLOCK];
+    __shared__ ull s_pre[3], s_tot[3];
+    const long long ns = nseg_of(a.T);
+    for (long long s = blockIdx.x; s < ns; s += gridDim.x) {
+        const int v = a.T.seg_row[s], j = a.T.seg_j[s];
+        const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
+        const long long e0 = rs + (long long)j * GC_SEG;
+        const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+        const long long first = s - j, nsr = (d + GC_SEG - 1) / GC_SEG;
+        if (threadIdx.x < GC_WAVE) {
+            ull p[3], t[3];
+            seg_sums(a.seg_aux, first, s, p);
+            seg_sums(a.seg_aux, first, first + nsr, t);
+            if (threadIdx.x == 0)
+                for (int c = 0; c < 3; ++c) {
+                    s_pre[c] = p[c];
+                    s_tot[c] = t[c];
+                }
+        }
+        for (int i = threadIdx.x; i < len; i += blockDim.x) buf[i] = a.src[e0 + i];
+        __syncthreads();
+        const int j0 = threadIdx.x * GC_PER;
+        int nv = len - j0;
+        nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
+        const unsigned cls = a.seg_cls[s * GC_BLOCK + threadIdx.x];
+        int u[GC_PER];
+        unsigned m0 = 0, m1 = 0, m2 = 0;
+#pragma unroll
+        for (int k = 0; k < GC_PER; ++k) {
+            u[k] = k < nv ? buf[j0 + k] : 0;
+            if (k < nv) {
+                const unsigned c = (cls >> (2 * k)) & 3u;
+                m0 |= (c == 0 ? 1u : 0u) << k;
+                m1 |= (c == 1 ? 1u : 0u) << k;
+                m2 |= (c == 2 ? 1u : 0u) << k;
+            }
+        }
+        ull segtot;
+        const ull prefix = block_excl_scan(pack3(__popc(m0), __popc(m1), __popc(m2)), s_w, &segtot);
+        const unsigned L0 = f16(segtot, 0), L1 = f16(segtot, 1);
+        // compact the segment in LDS by class (u is in registers; block_excl_scan's barriers
+        // ordered every read of buf before these writes)
+#pragma unroll
+        for (int k = 0; k < GC_PER; ++k) {
+            if (k >= nv) break;
+            const unsigned bit = 1u << k;
+            const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : 2);
+            const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
+            const unsigned sec = c == 0 ? 0u : (c == 1 ? L0 : L0 + L1);
+            buf[sec + f16(prefix, c) + __popc(mc & (bit - 1u))] = u[k];
+        }
+        __syncthreads();
+        const long long T0 = (long long)s_tot[0], T1 = (long long)s_tot[1];
+        const long long P0 = (long long)s_pre[0], P1 = (long long)s_pre[1], P2 = (long long)s_pre[2];
+        for (int i = threadIdx.x; i < len; i += blockDim.x) {
+            long long pos;
+            if (i < (int)L0) pos = P0 + i;
+            else if (i < (int)(L0 + L1)) pos = T0 + P1 + (i - (int)L0);
+            else pos = T0 + T1 + P2 + (i - (int)(L0 + L1));
+            a.dst[rs + pos] = buf[i];
+        }
+        if (j == 0 && threadIdx.x == 0) {
+            a.nlow[v] = (int)(T0 + T1);
+            if (a.neq) a.neq[v] = (int)T1;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// validate_graph_coloring counts (coloring.py:149-162): #(colour == -1) over the vertices,
+// #{(v, u): u listed in N(v), colour[u] == colour[v]} over the entries (directed, duplicates
+// and self-loops count, exactly as coloring.py:157-158)
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors, ull* unc_out,
+                                                             ull* conf_out) {
+    __shared__ TileLds S;
+    const long long nt = T.ntiles, ns = nseg_of(T);
+    ull unc = 0, conf = 0;
+    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
+        if (it < nt) {
+            int r0, NE;
+            long long eb;
+            bool hl;
+            const int R = tile_rows(T, it, S, &r0, &eb, &NE, &hl);
+            if (R == 0) continue;
+            for (int i = threadIdx.x; i < R; i += blockDim.x) {
+                const int cv = colors[r0 + i];
+                S.key[i] = (unsigned)cv;
+                unc += cv == -1;
+            }
+            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = col[eb + i];
+            __syncthreads();
+            int u[GC_PER], rk[GC_PER];
+            const int nv = thread_entries(S, R, NE, u, rk);
+            int cu[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) cu[k] = k < nv ? colors[u[k]] : 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) conf += (k < nv && cu[k] == (int)S.key[rk[k]]) ? 1 : 0;
+        } else {
+            const long long s = it - nt;
+            const int v = T.seg_row[s], j = T.seg_j[s];
+            const long long rs = T.rp[v], d = T.rp[v + 1] - rs;
+            const long long e0 = rs + (long long)j * GC_SEG;
+            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            const int cv = colors[v];
+            int cu[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {  // coalesced: entry threadIdx + k * 256
+                const int i = threadIdx.x + k * GC_BLOCK;
+                cu[k] = i < len ? colors[col[e0 + i]] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) conf += (threadIdx.x + k * GC_BLOCK < len && cu[k] == cv) ? 1 : 0;
+        }
+        __syncthreads();
+    }
+    unc = gc_wave_sum(unc);
+    conf = gc_wave_sum(conf);
+    if (gc_lane() == 0) {
+        if (unc) atomicAdd(unc_out, unc);
+        if (conf) atomicAdd(conf_out, conf);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// hub transpose of a symmetric graph: the rows that list hub x are x's own entries, so the
+// hubs each row u lists (hin, pushed into by u's commits) are u's entries that are hubs --
+// a filter of every row, no atomics on targets.  A hub row's lower-rank hubs (hlow) are the
+// entries of its hin row that lie in its low part: a prefix of that row (klow of them).
+// ------------------------------------------------------------------------------------
+struct HubArgs {
+    Tiles T;
+    const int* col;
+    const int* nlow;
+    const int* hid;
+    const unsigned* hubmap;
+    long long* hin_cnt;  // count pass: per row
+    long long* klow;     // count pass: per hub
+    const long long* hin_rp;  // fill pass
+    int* hin_col;
+    ull* seg_aux;        // per segment: hub entries (count pass)
+};
+
+// hub entries of this thread's tile entries (mask) and those inside their row's low part
+__device__ __forceinline__ void hub_masks(const HubArgs& a, const TileLds& S, int nv, const int* u, const int* rk,
+                                          unsigned* mk, unsigned* ml) {
+    const int j0 = threadIdx.x * GC_PER;
+    unsigned words[GC_PER];
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) words[k] = k < nv ? a.hubmap[u[k] >> 5] : 0u;
+    unsigned m = 0, l = 0;
+#pragma unroll
+    for (int k = 0; k < GC_PER; ++k) {
+        const bool h = k < nv && ((words[k] >> (u[k] & 31)) & 1u);
+        m |= (h ? 1u : 0u) << k;
+        const int r = rk[k];
+        const bool low = h && (j0 + k - S.off[r]) < (int)S.key[r];  // index in row < nlow
+        l |= (low ? 1u : 0u) << k;
+    }
+    *mk = m;
+    *ml = l;
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_hin_count(HubArgs a) {
+    __shared__ TileLds S;
+    const long long nt = a.T.ntiles, ns = nseg_of(a.T);
+    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
+        if (it < nt) {
+            int r0, NE;
+            long long eb;
+            bool hl;
+            const int R = tile_rows(a.T, it, S, &r0, &eb, &NE, &hl);
+            if (R == 0) continue;
+            for (int i = threadIdx.x; i < R; i += blockDim.x) {
+                S.key[i] = (unsigned)a.nlow[r0 + i];
+                S.aux[i] = a.hid[r0 + i];
+            }
+            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = a.col[eb + i];
+            __syncthreads();
+            int u[GC_PER], rk[GC_PER];
+            const int nv = thread_entries(S, R, NE, u, rk);
+            unsigned mk = 0, ml = 0;
+            hub_masks(a, S, nv, u, rk, &mk, &ml);
+            ull total;
+            const ull prefix = block_excl_scan(pack3(__popc(mk), __popc(ml), 0), S.w, &total);
+            record_bases(S, R, NE, nv, prefix, total, mk, ml, 0u);
+            __syncthreads();
+            for (int r = threadIdx.x; r < R; r += blockDim.x) {
+                if (hl && r == R - 1) continue;
+                const ull b = S.base[r], b1 = S.base[r + 1];
+                a.hin_cnt[r0 + r] = f16(b1, 0) - f16(b, 0);
+                if (S.aux[r] >= 0) a.klow[S.aux[r]] = f16(b1, 1) - f16(b, 1);
+            }
+        } else {
+            const long long s = it - nt;
+            const int v = a.T.seg_row[s], j = a.T.seg_j[s];
+            const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
+            const long long e0 = rs + (long long)j * GC_SEG;
+            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            const int nl = a.nlow[v];
+            ull ck = 0, cl = 0;
+            unsigned w[GC_PER];
+            int uu[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                const int i = threadIdx.x + k * GC_BLOCK;
+                uu[k] = i < len ? a.col[e0 + i] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) w[k] = threadIdx.x + k * GC_BLOCK < len ? a.hubmap[uu[k] >> 5] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                const int i = threadIdx.x + k * GC_BLOCK;
+                const bool h = i < len && ((w[k] >> (uu[k] & 31)) & 1u);
+                ck += h;
+                cl += h && ((long long)j * GC_SEG + i < nl);
+            }
+            const ull tot = block_sum(pack3((unsigned)ck, (unsigned)cl, 0), S.w);
+            if (threadIdx.x == 0) {
+                a.seg_aux[s] = tot;
+                atomicAdd((ull*)&a.hin_cnt[v], (ull)f16(tot, 0));
+                const int x = a.hid[v];
+                if (x >= 0 && f16(tot, 1)) atomicAdd((ull*)&a.klow[x], (ull)f16(tot, 1));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
+    __shared__ TileLds S;
+    const long long nt = a.T.ntiles, ns = nseg_of(a.T);
+    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
+        if (it < nt) {
+            int r0, NE;
+            long long eb;
+            bool hl;
+            const int R = tile_rows(a.T, it, S, &r0, &eb, &NE, &hl);
+            if (R == 0) continue;
+            for (int i = threadIdx.x; i < R; i += blockDim.x) S.key[i] = 0x7FFFFFFFu;  // low part unused here
+            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = a.col[eb + i];
+            __syncthreads();
+            int u[GC_PER], rk[GC_PER];
+            const int nv = thread_entries(S, R, NE, u, rk);
+            unsigned mk = 0, ml = 0;
+            hub_masks(a, S, nv, u, rk, &mk, &ml);
+            ull total;
+            const ull prefix = block_excl_scan(pack3(__popc(mk), 0, 0), S.w, &total);
+            record_bases(S, R, NE, nv, prefix, total, mk, 0u, 0u);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                if (!((mk >> k) & 1u)) continue;
+                const int r = rk[k];
+                const unsigned rank = f16(prefix, 0) + __popc(mk & ((1u << k) - 1u)) - f16(S.base[r], 0);
+                a.hin_col[a.hin_rp[r0 + r] + rank] = a.hid[u[k]];
+            }
+        } else {
+            const long long s = it - nt;
+            const int v = a.T.seg_row[s], j = a.T.seg_j[s];
+            const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
+            const long long e0 = rs + (long long)j * GC_SEG;
+            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            if (threadIdx.x < GC_WAVE) {
+                ull p[3];
+                seg_sums(a.seg_aux, s - j, s, p);
+                if (threadIdx.x == 0) S.misc[0] = p[0];
+            }
+            // this thread's entries are CONTIGUOUS here ([16t, 16t+16)): ranks follow row order
+            const int j0 = threadIdx.x * GC_PER;
+            int nv = len - j0;
+            nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
+            int uu[GC_PER];
+            unsigned w[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) uu[k] = k < nv ? a.col[e0 + j0 + k] : 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) w[k] = k < nv ? a.hubmap[uu[k] >> 5] : 0u;
+            unsigned mk = 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) mk |= ((k < nv && ((w[k] >> (uu[k] & 31)) & 1u)) ? 1u : 0u) << k;
+            ull tot;
+            const ull prefix = block_excl_scan((ull)__popc(mk), S.w, &tot);
+            const long long base = a.hin_rp[v] + (long long)S.misc[0] + (long long)prefix;
+            int o = 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k)
+                if ((mk >> k) & 1u) a.hin_col[base + o++] = a.hid[uu[k]];
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_hubmap(const int* hid, long long n, unsigned* map) {
+    const long long words = (n + 31) / 32;
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (long long)gridDim.x * blockDim.x) {
+        unsigned m = 0;
+        for (int k = 0; k < 32; ++k) {
+            const long long v = w * 32 + k;
+            if (v < n && hid[v] >= 0) m |= 1u << k;
+        }
+        map[w] = m;
+    }
+}
+
+// hlow rows: the klow-entry prefix of each hub's hin row (a wave per hub)
+__global__ void k_hlow_copy(const int* hub_v, long long H, const long long* hin_rp, const int* hin_col,
+                            const long long* hlow_rp, int* hlow_col) {
+    const long long waves = (long long)gridDim.x * (blockDim.x / GC_WAVE);
+    for (long long x = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE; x < H; x += waves) {
+        const long long src = hin_rp[hub_v[x]], dst = hlow_rp[x], len = hlow_rp[x + 1] - dst;
+        for (long long i = gc_lane(); i < len; i += GC_WAVE) hlow_col[dst + i] = hin_col[src + i];
+    }
+}
+
+int scan_ll(const long long* in, long long* out, long long count, hipStream_t s) {
+    size_t bytes = 0;
+    GC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s));
+    void* tmp = nullptr;
+    GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
+    hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
+    hipStreamSynchronize(s);  // the temporary goes back to the cache idle
+    gc_dfree(tmp);
+    GC_HIP(e);
+    return GC_OK;
+}
+
+int small_grid(long long items) {
+    return (int)std::max<long long>(1, std::min<long long>((items + GC_BLOCK - 1) / GC_BLOCK, 8192));
+}
+
+Tiles tiles_of(const gc_graph* g) {
+    Tiles T;
+    T.rp = g->rp;
+    T.r0 = g->tile_r0;
+    T.ntiles = g->ntiles;
+    T.seg_base = g->seg_base;
+    T.seg_row = g->seg_row;
+    T.seg_j = g->seg_j;
+    T.n = (int)g->n;
+    return T;
+}
+
+int prep_grid(const gc_graph* g) {
+    return (int)std::max<long long>(1, std::min<long long>(g->ntiles + g->nseg_cap, GC_PREP_GRID));
+}
+
+}  // namespace
+
+int gc_build_tiling(gc_graph* g) {
+    if (g->tile_r0) return GC_OK;
+    const hipStream_t s = g->stream;
+    const long long n = g->n, nnz = g->nnz;
+    g->ntiles = (nnz + n + GC_TW - 1) / GC_TW;
+    g->nseg_cap = nnz / GC_SEG + nnz / GC_TH + 1;
+    long long* cnt = nullptr;
+    GC_HIP(gc_dmalloc((void**)&g->tile_r0, sizeof(int) * (size_t)(g->ntiles + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->seg_base, sizeof(long long) * (size_t)(g->ntiles + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->seg_row, sizeof(int) * (size_t)g->nseg_cap));
+    GC_HIP(gc_dmalloc((void**)&g->seg_j, sizeof(int) * (size_t)g->nseg_cap));
+    GC_HIP(gc_dmalloc((void**)&g->seg_aux, sizeof(ull) * (size_t)g->nseg_cap));
+    GC_HIP(gc_dmalloc((void**)&g->seg_cls, sizeof(unsigned) * (size_t)g->nseg_cap * GC_BLOCK));
+    GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(g->ntiles + 1)));
+    hipLaunchKernelGGL(k_tile_bounds, dim3(small_grid(g->ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp, n, g->ntiles,
+                       g->tile_r0);
+    hipLaunchKernelGGL(k_tile_nseg, dim3(small_grid(g->ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp,
+                       (const int*)g->tile_r0, g->ntiles, cnt);
+    int rc = scan_ll(cnt, g->seg_base, g->ntiles + 1, s);
+    if (rc == GC_OK)
+        hipLaunchKernelGGL(k_tile_segs, dim3(small_grid(g->ntiles)), dim3(GC_BLOCK), 0, s, (const int*)g->tile_r0,
+                           g->ntiles, (const long long*)g->seg_base, g->seg_row, g->seg_j);
+    hipStreamSynchronize(s);
+    gc_dfree(cnt);
+    if (rc) return rc;
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad) {
+    if (g->n == 0 || g->nnz == 0) {
+        if (g->n) {
+            GC_HIP(hipMemsetAsync(g->nlow, 0, sizeof(int) * (size_t)g->n, g->stream));
+            if (g->neq) GC_HIP(hipMemsetAsync(g->neq, 0, sizeof(int) * (size_t)g->n, g->stream));
+        }
+        return GC_OK;
+    }
+    int rc = gc_build_tiling(g);
+    if (rc) return rc;
+    PartArgs a;
+    a.T = tiles_of(g);
+    a.src = src;
+    a.dst = dst;
+    a.deg = g->deg;
+    a.kb = g->kb;
+    a.nlow = g->nlow;
+    a.neq = g->neq;
+    a.seed = (ull)seed;
+    a.bad = bad;
+    a.seg_aux = g->seg_aux;
+    a.seg_cls = g->seg_cls;
+    const int grid = prep_grid(g);
+    if (prio) hipLaunchKernelGGL(k_part1<1>, dim3(grid), dim3(GC_BLOCK), 0, g->stream, a);
+    else hipLaunchKernelGGL(k_part1<0>, dim3(grid), dim3(GC_BLOCK), 0, g->stream, a);
+    hipLaunchKernelGGL(k_part2, dim3(grid), dim3(GC_BLOCK), 0, g->stream, a);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+int gc_validate_tiles(gc_graph* g, const int* colors) {
+    if (g->n == 0) return GC_OK;
+    int rc = gc_build_tiling(g);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_validate_tiles, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
+                       (const int*)g->col, colors, &g->ctl->uncolored, &g->ctl->conflicts);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+// hubmap from hid, then the count pass: hin_cnt (n + 1, zeroed here) and klow (H + 1)
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow) {
+    const hipStream_t s = g->stream;
+    int rc = gc_build_tiling(g);
+    if (rc) return rc;
+    const long long words = (g->n + 31) / 32;
+    if (!g->hubmap) GC_HIP(gc_dmalloc((void**)&g->hubmap, sizeof(unsigned) * (size_t)std::max<long long>(words, 1)));
+    hipLaunchKernelGGL(k_hubmap, dim3(small_grid(words)), dim3(GC_BLOCK), 0, s, (const int*)g->hid, g->n, g->hubmap);
+    GC_HIP(hipMemsetAsync(hin_cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
+    GC_HIP(hipMemsetAsync(klow, 0, sizeof(long long) * (size_t)(H + 1), s));
+    HubArgs a;
+    a.T = tiles_of(g);
+    a.col = g->col;
+    a.nlow = g->nlow;
+    a.hid = g->hid;
+    a.hubmap = g->hubmap;
+    a.hin_cnt = hin_cnt;
+    a.klow = klow;
+    a.hin_rp = nullptr;
+    a.hin_col = nullptr;
+    a.seg_aux = g->seg_aux;
+    if (g->nnz > 0) hipLaunchKernelGGL(k_hin_count, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, s, a);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}
+
+// fill pass (hin_rp / hin_col allocated), then hlow rows as klow-prefixes (hlow_rp ready)
+int gc_hub_transpose_fill(gc_graph* g, long long H) {
+    const hipStream_t s = g->stream;
+    HubArgs a;
+    a.T = tiles_of(g);
+    a.col = g->col;
+    a.nlow = g->nlow;
+    a.hid = g->hid;
+    a.hubmap = g->hubmap;
+    a.hin_cnt = nullptr;
+    a.klow = nullptr;
+    a.hin_rp = g->hin_rp;
+    a.hin_col = g->hin_col;
+    a.seg_aux = g->seg_aux;
+    if (g->nnz > 0) hipLaunchKernelGGL(k_hin_fill, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, s, a);
+    if (H > 0)
+        hipLaunchKernelGGL(k_hlow_copy, dim3((int)std::min<long long>((H + 3) / 4, 8192)), dim3(GC_BLOCK), 0, s,
+                           (const int*)g->hub_v, H, (const long long*)g->hin_rp, (const int*)g->hin_col,
+                           (const long long*)g->hlow_rp, g->hlow_col);
+    GC_HIP(hipGetLastError());
+    return GC_OK;
+}

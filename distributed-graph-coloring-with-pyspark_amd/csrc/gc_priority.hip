@@ -33,21 +33,6 @@
 
 namespace {
 
-// seeded 32-bit priority: the top half of splitmix64(seed + (v + 1) * golden gamma)
-// (identical to prio_hash in oracle/gcolor_oracle.c)
-__device__ __forceinline__ unsigned prio_hash(ull seed, long long v) {
-    ull z = seed + 0x9E3779B97F4A7C15ull * (ull)(v + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (unsigned)(z >> 32);
-}
-
-__global__ void k_prio_key(long long n, int prio, ull seed, const int* deg, unsigned* key) {
-    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x)
-        key[v] = prio ? prio_hash(seed, v) : (unsigned)deg[v];
-}
-
 // per-round counter reset of a speculative round (one thread)
 __global__ void k_spec_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -203,28 +188,22 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
     if (g->borrowed) { gc_set_error("a shard view cannot change the row partition"); return GC_EINVAL; }
     const hipStream_t s = g->stream;
     if (g->n > 0 && g->nnz > 0) {
-        unsigned* key = nullptr;
         int* tmp = nullptr;
-        GC_HIP(hipMalloc((void**)&key, sizeof(unsigned) * (size_t)g->n));
-        if (hipMalloc((void**)&tmp, sizeof(int) * (size_t)g->nnz) != hipSuccess) {
-            hipFree(key);
-            gc_set_error("hipMalloc of the partition scratch (%lld entries) failed", g->nnz);
+        if (gc_dmalloc((void**)&tmp, sizeof(int) * (size_t)g->nnz) != hipSuccess) {
+            gc_set_error("allocation of the partition scratch (%lld entries) failed", g->nnz);
             return GC_ENOMEM;
         }
-        const int grid = gc_grid_for_waves(g->n, 8192);
-        hipLaunchKernelGGL(k_prio_key, dim3(grid), dim3(GC_BLOCK), 0, s, (long long)g->n, prio, (ull)seed, g->deg, key);
-        gcl_rank_flags(g->rp, g->col, key, (int)g->n, g->nlow, grid, s);
-        gcl_partition_rows(g->rp, g->col, g->deg, g->nlow, (int)g->n, tmp, grid, s);
-        hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
+        int rc = gc_partition(g, g->col, tmp, prio, seed, &g->ctl->conflicts);
+        if (rc == GC_OK) hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
         const hipError_t e = hipStreamSynchronize(s);
-        hipFree(tmp);
-        hipFree(key);
+        gc_dfree(tmp);
+        if (rc) return rc;
         if (e != hipSuccess || hipGetLastError() != hipSuccess) { gc_set_error("row re-partition failed"); return GC_EHIP; }
         // the in-neighbour lists of an asymmetric graph are sets: their order is unaffected
     }
     g->part_prio = prio;
     g->part_seed = seed;
-    g->bpart = false;  // the low parts were rebuilt
+    g->bpart = prio == GC_PRIORITY_REF;  // the (deg, pos) partition also splits the low parts by degree
     return GC_OK;
 }
 

@@ -90,7 +90,7 @@ static GDev shard_view(gc_shard* sh) {
 static void shard_free_hubs(gc_shard* sh) {
     void* ptrs[] = {sh->hbits, sh->hk, sh->hkill, sh->hcur, sh->hpc, sh->hrow, sh->hlen, sh->hkcnt, sh->hseen};
     for (void* p : ptrs)
-        if (p) hipFree(p);
+        if (p) gc_dfree(p);
     sh->hbits = sh->hk = sh->hkill = nullptr;
     sh->hcur = sh->hpc = sh->hrow = sh->hlen = sh->hkcnt = sh->hseen = nullptr;
     sh->repl = false;
@@ -99,7 +99,7 @@ static void shard_free_hubs(gc_shard* sh) {
 // the shard's hub arrays: the bitmaps, and with replicated hubs the hub JP state
 static int shard_alloc_hubs(gc_shard* sh) {
     const size_t H = (size_t)sh->nhub;
-    if (hipMalloc((void**)&sh->hbits, sizeof(unsigned) * H * (size_t)sh->hub_w) != hipSuccess) {
+    if (gc_dmalloc((void**)&sh->hbits, sizeof(unsigned) * H * (size_t)sh->hub_w) != hipSuccess) {
         sh->hbits = nullptr;
         gc_set_error("hipMalloc of the shard's hub bitmaps failed");
         return GC_ENOMEM;
@@ -108,7 +108,7 @@ static int shard_alloc_hubs(gc_shard* sh) {
     void** arrs[] = {(void**)&sh->hk, (void**)&sh->hkill, (void**)&sh->hcur, (void**)&sh->hpc,
                      (void**)&sh->hrow, (void**)&sh->hlen, (void**)&sh->hkcnt, (void**)&sh->hseen};
     for (void** a : arrs) {
-        if (hipMalloc(a, 4 * H) != hipSuccess) {
+        if (gc_dmalloc(a, 4 * H) != hipSuccess) {
             *a = nullptr;
             gc_set_error("hipMalloc of the shard's hub state failed");
             return GC_ENOMEM;
@@ -155,8 +155,8 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&v.ev0)) != hipSuccess || (e = hipEventCreate(&v.ev1)) != hipSuccess ||
-        (e = hipMalloc((void**)&v.ctl, sizeof(DevCtl))) != hipSuccess ||
-        (e = hipHostMalloc((void**)&v.hctl, sizeof(DevCtl), hipHostMallocDefault)) != hipSuccess) {
+        (e = gc_dmalloc((void**)&v.ctl, sizeof(DevCtl))) != hipSuccess ||
+        (e = gc_hmalloc((void**)&v.hctl, sizeof(DevCtl))) != hipSuccess) {
         gc_set_error("shard allocation failed: %s", hipGetErrorString(e));
         gc_free_all(&v);
         delete sh;

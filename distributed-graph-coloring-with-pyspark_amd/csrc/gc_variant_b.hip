@@ -98,51 +98,10 @@ struct BLists {
 };
 __device__ __forceinline__ ull* b_cnt(DevCtl* c, int kind, int slot) { return &c->bcnt[kind * 3 + slot]; }
 
-// Row layout (ensure_bpart): [lower degree | equal degree, earlier | higher rank].  The
-// admission of v can only be blocked by an earlier u with deg(u) >= deg(v): the entries
-// from nlow[v] - neq[v] on.  An evictor of u has a higher degree: the entries from
-// nlow[u] on.
-__global__ void __launch_bounds__(GC_BLOCK) k_b_eqflags(const long long* rp, int* col, const int* deg, const int* nlow,
-                                                         int n, int* neq, int* split) {
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_cnt[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
-    const int lane = gc_lane();
-    const int w = threadIdx.x / GC_WAVE;
-    const long long nchunks = ((long long)n + GC_WAVE - 1) / GC_WAVE;
-    for (long long chunk = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; chunk < nchunks;
-         chunk += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
-        const long long v = chunk * GC_WAVE + lane;
-        const bool valid = v < n;
-        const int len = valid ? nlow[v] : 0;
-        s_start[w][lane] = valid ? rp[v] : 0;
-        s_cnt[w][lane] = 0;
-        s_d[w][lane] = valid ? deg[v] : 0;
-        const int incl = gc_wave_incl_scan(len);
-        const int excl = incl - len;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        for (int base = 0; base < total; base += GC_WAVE) {
-            const int e = base + lane;
-            const int o = gc_owner(excl, e);
-            const int eo = __shfl(excl, o, GC_WAVE);
-            if (e < total) {
-                const long long ei = s_start[w][o] + (e - eo);
-                const int u = col[ei];
-                if (deg[u] == s_d[w][o]) {
-                    atomicAdd(&s_cnt[w][o], 1);
-                    col[ei] = (int)((unsigned)u | 0x80000000u);
-                }
-            }
-        }
-        gc_wave_sync();
-        if (valid) {
-            neq[v] = s_cnt[w][lane];
-            split[v] = len - s_cnt[w][lane];
-        }
-    }
-}
-
+// Row layout (the (deg, pos) rank partition, gc_prep.hip): [lower degree | equal degree,
+// earlier | higher rank].  The admission of v can only be blocked by an earlier u with
+// deg(u) >= deg(v): the entries from nlow[v] - neq[v] on.  An evictor of u has a higher
+// degree: the entries from nlow[u] on.
 // Round start: every proposer is undecided; its admission range starts at the equal-degree
 // entries; eviction times unknown (-1).
 __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B, int* ev, const int* neq) {
@@ -437,35 +396,14 @@ struct RunB {
 
 }  // namespace
 
-// Splits every row's low part (once per graph and row partition): lower-degree entries
-// first, then the equal-degree ones (all earlier in file order under the (deg, pos) rank);
-// neq[v] counts the latter.  Variant A never looks inside a low part, so it is unaffected.
+// The (deg, pos) rank partition (graph creation, gc_set_priority) already splits every low
+// part by degree and counts the equal-degree entries (neq); variant A never looks inside a
+// low part, so the layout serves both variants.
 static int ensure_bpart(gc_graph* g) {
-    if (g->bpart) return GC_OK;
-    if (g->part_prio != GC_PRIORITY_REF) { gc_set_error("variant B needs the (deg, pos) row partition"); return GC_EINVAL; }
-    const hipStream_t s = g->stream;
-    if (!g->neq) GC_HIP(hipMalloc((void**)&g->neq, sizeof(int) * (size_t)std::max<long long>(g->n, 1)));
-    if (g->n > 0) GC_HIP(hipMemsetAsync(g->neq, 0, sizeof(int) * (size_t)g->n, s));
-    if (g->n > 0 && g->nnz > 0) {
-        int *tmp = nullptr, *split = nullptr;
-        if (hipMalloc((void**)&tmp, sizeof(int) * (size_t)g->nnz) != hipSuccess ||
-            hipMalloc((void**)&split, sizeof(int) * (size_t)g->n) != hipSuccess) {
-            hipFree(tmp);
-            gc_set_error("hipMalloc of the variant B row split scratch failed");
-            return GC_ENOMEM;
-        }
-        const int grid = gc_grid_for_waves(g->n, 8192);
-        hipMemcpyAsync(tmp, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);  // keeps the high parts
-        hipLaunchKernelGGL(k_b_eqflags, dim3(grid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->deg, g->nlow, (int)g->n,
-                           g->neq, split);
-        gcl_partition_rows(g->rp, g->col, g->nlow, split, (int)g->n, tmp, grid, s);
-        hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
-        const hipError_t e = hipStreamSynchronize(s);
-        hipFree(tmp);
-        hipFree(split);
-        if (e != hipSuccess || hipGetLastError() != hipSuccess) { gc_set_error("variant B row split failed"); return GC_EHIP; }
+    if (g->part_prio != GC_PRIORITY_REF || !g->bpart || !g->neq) {
+        gc_set_error("variant B needs the (deg, pos) row partition");
+        return GC_EINVAL;
     }
-    g->bpart = true;
     return GC_OK;
 }
 

@@ -93,6 +93,18 @@ class DeviceGraph:
         return cls(h)
 
     @classmethod
+    def from_device(cls, d_row_ptr, d_col, n, nnz, symmetric=False):
+        """A graph from a CSR already resident in HBM: device pointers (ints, e.g. a torch
+        tensor's ``data_ptr()``) to int64[n+1] offsets and int32[nnz] positions.  The rows are
+        read in place and rank-partitioned into the graph's own array (gc_graph_create_device)."""
+        lib = nat.load()
+        h = ctypes.c_void_p()
+        nat.check("gc_graph_create_device", lib.gc_graph_create_device(
+            ctypes.c_void_p(d_row_ptr), ctypes.c_void_p(d_col), int(n), int(nnz),
+            nat.GC_GRAPH_SYMMETRIC if symmetric else 0, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
     def rmat(cls, scale, edge_factor=16, a=0.57, b=0.19, c=0.19, seed=1):
         lib = nat.load()
         h = ctypes.c_void_p()
@@ -139,6 +151,12 @@ class DeviceGraph:
         c = np.empty(max(self.nnz, 1), np.int32) if col else None
         nat.check("gc_graph_export", self._lib.gc_graph_export(self._h, _ptr(rp), _ptr(c)))
         return rp, (c[: self.nnz] if col else None)
+
+    def export_device(self, d_row_ptr, d_col):
+        """Device-to-device copy of the CSR (rows as the engine stores them) into caller-owned
+        device buffers (pointers as ints; either may be None)."""
+        nat.check("gc_graph_export_device", self._lib.gc_graph_export_device(
+            self._h, ctypes.c_void_p(d_row_ptr) if d_row_ptr else None, ctypes.c_void_p(d_col) if d_col else None))
 
     def lower_counts(self):
         """nlow[v]: entries at the head of exported row v that rank below v (deg, pos)."""

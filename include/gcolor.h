@@ -50,7 +50,9 @@ typedef struct gc_graph gc_graph;
    Replaces: sc.parallelize(graph.nodes)...persist(), coloring.py:201-209.           */
 int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t nnz,
                     uint32_t flags, gc_graph** out);
-/* Same, from device pointers already resident in HBM (copied device-to-device).      */
+/* Same, from device pointers already resident in HBM: rp is copied, the rows are read in
+   place and written rank-partitioned into the graph's own array (no copy of col).  The
+   caller's buffers need to stay valid only for the duration of the call.             */
 int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                            uint32_t flags, gc_graph** out);
 /* Device-side synthetic generators (no host round trip):
@@ -66,6 +68,8 @@ int gc_graph_info(const gc_graph* g, int64_t* n, int64_t* nnz, int64_t* max_degr
    Rows come back in the engine's order: each row lists its lower-rank neighbours
    (rank = (deg, pos), coloring.py:64) first -- the same multiset as the input row.   */
 int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col);
+/* The same into caller-owned DEVICE buffers (device-to-device; either may be NULL).    */
+int gc_graph_export_device(const gc_graph* g, int64_t* d_row_ptr, int32_t* d_col);
 /* nlow_out (host int32[n]): how many entries at the head of each exported row rank
    below the row's vertex.                                                            */
 int gc_graph_lower_counts(const gc_graph* g, int32_t* nlow_out);
@@ -259,6 +263,9 @@ void gc_csr_free(gc_csr* c);
 
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gc_last_error(void);
+/* Return every device / pinned block the library's allocator has parked for reuse (graph
+   handles that are created and destroyed repeatedly get their buffers from that cache).  */
+int gc_release_cache(void);
 int gc_device_count(int32_t* count);
 int gc_set_device(int32_t device);
 

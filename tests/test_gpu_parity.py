@@ -240,6 +240,87 @@ def _check_partition(dg):
     assert np.array_equal(lower, head), "rows must list exactly their lower-rank neighbours first"
 
 
+def _expected_layout(rp, col):
+    """The rank partition as gc_prep.hip states it, restated on the host: every row stably
+    split into [lower degree | equal degree, earlier position | higher rank] (coloring.py:64's
+    (deg, pos) order; the middle class is variant B's equal-degree block)."""
+    deg = np.diff(rp)
+    n = len(rp) - 1
+    src = np.repeat(np.arange(n, dtype=np.int64), deg)
+    du, dv = deg[col], deg[src]
+    cls = np.where(du < dv, 0, np.where((du == dv) & (col < src), 1, 2))
+    order = np.argsort(src * 3 + cls, kind="stable")
+    nlow = np.bincount(src, weights=(cls < 2), minlength=n).astype(np.int64)
+    neq = np.bincount(src, weights=(cls == 1), minlength=n).astype(np.int64)
+    return col[order], nlow, neq
+
+
+def _heavy_graph(seed):
+    """Rows past the tile geometry (2048 keys per tile, segments of 4096 entries): a few rows
+    of 2049..20000 entries, runs of empty rows, duplicates and self-loops, directed."""
+    rng = np.random.default_rng(seed)
+    n = 30000
+    deg = rng.integers(0, 12, n)
+    deg[rng.integers(0, n, 3000)] = 0
+    deg[[5, 6, 777, 20000, n - 1]] = [2049, 4096, 4097, 20000, 9000]
+    deg[100:2100] = 0  # a long run of isolated rows inside a tile window
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum(deg)
+    col = rng.integers(0, n, rp[-1]).astype(np.int32)
+    col[rp[5]:rp[5] + 100] = 5  # self-loops
+    return rp, col
+
+
+@pytest.mark.parametrize("kind", ["golden", "directed", "heavy", "heavy2"])
+def test_partition_is_the_stable_three_class_split(kind):
+    """Graph creation writes every row as the stable [lower deg | equal deg & earlier | rest]
+    split of the input row -- tiles, segmented rows and empty rows alike (gc_prep.hip)."""
+    DG = _dg()
+    if kind == "golden":
+        ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s0"))
+    elif kind == "directed":
+        rp, col = _random_directed(2000, 9000, 7)
+    else:
+        rp, col = _heavy_graph(1 if kind == "heavy" else 2)
+    exp, nlow, neq = _expected_layout(rp, col)
+    with DG.from_csr(rp, col) as dg:
+        rp2, col2 = dg.export()
+        assert np.array_equal(rp, rp2)
+        assert np.array_equal(col2, exp)
+        assert np.array_equal(dg.lower_counts(), nlow)
+        # the same from a device-resident CSR (rows read in place)
+        import torch
+        d_rp = torch.from_numpy(rp).cuda()
+        d_col = torch.from_numpy(col).cuda()
+        torch.cuda.synchronize()
+        with DG.from_device(d_rp.data_ptr(), d_col.data_ptr(), len(rp) - 1, len(col)) as dg2:
+            assert np.array_equal(dg2.export()[1], exp)
+            assert np.array_equal(dg2.lower_counts(), nlow)
+            out_rp = torch.empty_like(d_rp)
+            out_col = torch.empty_like(d_col)
+            dg2.export_device(out_rp.data_ptr(), out_col.data_ptr())
+            assert np.array_equal(out_col.cpu().numpy(), exp) and np.array_equal(out_rp.cpu().numpy(), rp)
+        # validation over tiles and segmented rows, host and device colours
+        rng = np.random.default_rng(3)
+        for ncol in (1, 3, 50):
+            cols = rng.integers(-1, ncol, len(rp) - 1).astype(np.int32)
+            assert dg.validate(cols) == oracle.c_validate(rp, col, cols)
+
+
+def test_create_device_rejects_bad_input():
+    from gcolor_amd import _native as nat
+    import torch
+    DG = _dg()
+    rp = np.array([0, 2, 3], np.int64)
+    col = np.array([1, 5, 0], np.int32)  # 5 is out of range
+    with pytest.raises(nat.GcolorError):
+        DG.from_device(torch.from_numpy(rp).cuda().data_ptr(), torch.from_numpy(col).cuda().data_ptr(), 2, 3)
+    rp_bad = torch.from_numpy(np.array([0, 3, 2], np.int64)).cuda()
+    col_ok = torch.from_numpy(np.array([1, 0, 1], np.int32)).cuda()
+    with pytest.raises(nat.GcolorError):
+        DG.from_device(rp_bad.data_ptr(), col_ok.data_ptr(), 2, 3)
+
+
 @pytest.mark.parametrize("kind", ["golden", "directed", "rmat", "mesh"])
 def test_rows_list_lower_rank_neighbours_first(kind):
     """Graph creation stores each row lower-rank-first (rank = (deg, pos), coloring.py:64)
