@@ -3,9 +3,12 @@
 
 Workload (default, BASELINE.json configs[2] = C3, the largest single-GPU config):
 R-MAT scale 24, edge factor 16, (A,B,C) = (0.57,0.19,0.19), seed 1, self-loops dropped,
-symmetrised, de-duplicated, generated on the device.  A step is one full colouring
-(coloring.py:73-132 semantics, variant A unless --variant B) from the resident CSR to a
-complete valid colouring; value = m / t (m = undirected edges = nnz/2), whole job.
+symmetrised, de-duplicated, generated on the device.  A step is SURVEY.md §8d's t: from a
+CSR resident in HBM (rows in generation order) to a complete, validated colouring --
+gc_graph_create_device (the rank partition of every row, coloring.py:64), gc_color (the hub
+index is built inside; coloring.py:73-132 semantics, variant A unless --variant B),
+gc_validate (coloring.py:149-162), gc_graph_destroy.  value = m / t (m = undirected edges =
+nnz/2), whole job.  `recolour_ms` is the colouring alone on a persistent handle.
 Other workloads (--workload): uniform10M (C2), rmat26 (north star), mesh512 (C4 on one
 GPU), mesh256, uniform1M, rmat28 (C5, sharded runs).
 
@@ -18,14 +21,17 @@ the K timed steps, max time over ranks; value = m / t_max.
 Extra objects on the JSON line:
   roofline      the kernel class that dominates the step BY TIME (every class, JP sweeps
                 included), event-timed on the engine's stream over a second pass of the K
-                steps right after the timed ones (events around a class's launch runs add
-                2-10% to a step: mesh 512^3 ~11 ms; `value` comes from the event-free pass,
+                steps right after the timed ones (`value` comes from the event-free pass,
                 `roofline.event_pass_ms_per_step` is the second pass's wall time).
                 achieved = SURVEY.md §8d algorithmic bytes / time when the class is credited
                 any, else (the later JP sweeps: no §8d credit) the rocprofv3 FETCH+WRITE
                 bytes of the class (profiles/pmc/<workload>.json) / time; `traffic` is the
                 PMC bytes per launch.  `classes_probe_step` lists every class (probe step) and flags
                 any whose algorithmic rate exceeds the HBM peak (bytes credited, not moved).
+  whole_job_*   §8d bytes / t / peak (raw, and capped per class at what the peak could move
+                in the class's time) and the physical fraction: rocprofv3 FETCH+WRITE bytes of
+                every kernel of a timed step (--selected-regions run) / t / peak.
+  north_star    R-MAT scale 26 on the same GPU, the same step (default run only).
   cpu_baseline  oracle/gcolor_omp.c, the multi-core C restatement (bit-exact with the
                 oracle, tests/test_oracle_omp.py), on the box's host cores, rank 0 at N=1
 """
@@ -138,27 +144,173 @@ def pmc_class_bytes(workload, variant):
     return out, os.path.relpath(p, REPO)
 
 
-def cpu_baseline(w, host_csr, dg, colors_gpu):
+def cpu_baseline(w, host_csr, colors_gpu):
     """oracle/gcolor_omp.c (bit-exact restatement of the oracle) on every host core this
-    process may use; TEPS of a full colouring of the same graph, or of a sample for the
-    largest workloads (stated in `sample`)."""
+    process may use; TEPS of a full colouring of the same graph."""
     sys.path.insert(0, REPO)
     from oracle import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    sample = "full graph"
-    if host_csr is None:
-        host_csr = dg.export()
     rp, col = host_csr
     t0 = time.perf_counter()
-    o = oracle.omp_color(rp, col, symmetric=dg.symmetric, threads=threads, want_rounds=False)
+    o = oracle.omp_color(rp, col, symmetric=True, threads=threads, want_rounds=False)
     dt = time.perf_counter() - t0
     m = len(col) / 2
     same = colors_gpu is not None and np.array_equal(o["colors"], colors_gpu)
     return {"value": m / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/gcolor_omp.c (OpenMP, {threads} threads) colouring the {sample} of {w['desc']} "
+            "sample": f"oracle/gcolor_omp.c (OpenMP, {threads} threads) colouring the full graph of {w['desc']} "
                       f"in {dt:.1f} s on {platform.processor() or platform.machine()} ({os.cpu_count()} CPUs "
                       f"visible); colours identical to the GPU's: {same}",
             "colors": int(o["max_color"]) + 1, "seconds": dt, "identical": same}
+
+
+class StepRunner:
+    """The §8d step on one GPU, from a resident CSR ("device wall time from a
+    resident CSR to a full valid colouring"): gc_graph_create_device (the rank partition of the
+    input rows, coloring.py:64), gc_color (the hub index is built inside: a fresh handle has
+    none), gc_validate (coloring.py:149-162), gc_graph_destroy."""
+
+    def __init__(self, dg0, variant, mode, torch, barrier):
+        self.V, self.mode, self.torch, self.barrier = variant, mode, torch, barrier
+        self.n, self.nnz, self.max_degree, self.sym = dg0.n, dg0.nnz, dg0.max_degree, dg0.symmetric
+        self.d_rp, self.d_col = resident_csr(dg0, torch)
+
+    def recolour_ms(self, dg0, reps=2):
+        return min(dg0.color(self.V, want_rounds=False, want_colors=False, **self.mode).device_ms
+                   for _ in range(reps))
+
+    def step(self, timing=None):
+        from gcolor_amd.engine import DeviceGraph
+        a = time.perf_counter()
+        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym)
+        b = time.perf_counter()
+        r = dg.color(self.V, kernel_timing=timing, want_rounds=False, want_colors=False, **self.mode)
+        c = time.perf_counter()
+        unc, conf = dg.validate()
+        d = time.perf_counter()
+        dg.close()
+        e = time.perf_counter()
+        assert unc == 0 and (conf == 0 or not self.sym), f"invalid colouring: {unc} uncoloured, {conf} conflicts"
+        return r, {"create": b - a, "colour": c - b, "validate": d - c, "destroy": e - d}
+
+    def steps(self, k, timing, roctx=False):
+        kern, ph = {}, {}
+        r = None
+        self.barrier()
+        if roctx:
+            roctx_resume()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            r, p = self.step(timing)
+            for key, v in r.kernels.items():
+                a = kern.setdefault(key, {"ms": 0.0, "launches": 0, "bytes": 0.0})
+                a["ms"] += v["ms"]
+                a["launches"] += v["launches"]
+                a["bytes"] += v["bytes"]
+            for key, v in p.items():
+                ph[key] = ph.get(key, 0.0) + v / k
+        self.barrier()
+        t = (time.perf_counter() - t0) / k
+        if roctx:
+            roctx_pause()
+        for a in kern.values():
+            a["ms"] /= k
+            a["launches"] //= k
+            a["bytes"] /= k
+        return t, kern, r, ph
+
+    def final_colouring(self):
+        from gcolor_amd.engine import DeviceGraph
+        with DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz,
+                                     symmetric=self.sym) as dg:
+            res = dg.color(self.V, want_colors=True, want_rounds=False, **self.mode)
+            unc, conf = dg.validate()
+            assert unc == 0 and conf == 0
+            return {"colors": res.colors, "csr": dg.export()}
+
+    def close(self):
+        self.d_rp = self.d_col = None
+        self.torch.cuda.empty_cache()
+
+
+_ROCTX = None
+
+
+def _roctx():
+    """rocprofv3 --selected-regions collects only between roctxProfilerResume/Pause: the
+    profiling runs (tools/gpu_profile.sh) count the timed steps' kernels alone."""
+    global _ROCTX
+    if _ROCTX is None:
+        _ROCTX = False
+        if os.environ.get("GC_ROCTX"):
+            import ctypes
+            rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+            for name in (os.path.join(rocm, "lib", "librocprofiler-sdk-roctx.so.1"), "librocprofiler-sdk-roctx.so.1",
+                         os.path.join(rocm, "lib", "libroctx64.so.4")):
+                try:
+                    _ROCTX = ctypes.CDLL(name)
+                    break
+                except OSError:
+                    continue
+    return _ROCTX
+
+
+def roctx_resume():
+    lib = _roctx()
+    if lib:
+        lib.roctxProfilerResume(0)
+
+
+def roctx_pause():
+    lib = _roctx()
+    if lib:
+        lib.roctxProfilerPause(0)
+
+
+def capped_alg(kern, n, nnz):
+    """§8d algorithmic bytes of a step with no class credited more than the HBM peak could
+    move in that class's (event-timed) time, plus the validate pass."""
+    tot = 0.0
+    for v in kern.values():
+        b = v["bytes"]
+        if v["ms"] > 0:
+            b = min(b, v["ms"] / 1e3 * HBM_PEAK_GBS * 1e9)
+        tot += b
+    return tot + 20.0 * n + 8.0 * nnz
+
+
+def pmc_step_frac(workload, variant, t):
+    """Physical fraction of the whole step: rocprofv3 FETCH_SIZE + WRITE_SIZE of every kernel
+    of the timed steps (profiles/pmc/<workload>.json "_step", a --selected-regions run of this
+    bench command) / t / peak."""
+    p = pmc_file(workload, variant)
+    if not os.path.exists(p):
+        return None
+    st = json.load(open(p)).get("_step")
+    if not st or not st.get("steps"):
+        return None
+    b = st["bytes"] / st["steps"]
+    return {"bytes_per_step": b, "GBps": b / t / 1e9, "frac": b / t / 1e9 / HBM_PEAK_GBS,
+            "source": os.path.relpath(p, REPO)}
+
+
+def north_star(torch, barrier, args):
+    """BASELINE.json north_star's target graph, R-MAT scale 26 on one GPU, measured the same way
+    (a few steps: it adds ~20 s to the default run)."""
+    w = WORKLOADS["rmat26"]
+    dg0, _ = build_graph(w)
+    S = StepRunner(dg0, "A", {"priority": None, "speculative": False}, torch, barrier)
+    dg0.close()
+    S.step()
+    t, kern, r, ph = S.steps(args.north_star_steps, None)
+    m = S.nnz // 2
+    balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
+    out = {"workload": w["desc"], "n": S.n, "m_undirected": m, "steps": args.north_star_steps,
+           "ms_per_step": t * 1e3, "edges_per_s": m / t, "colors_used": r.num_colors, "rounds": r.rounds,
+           "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
+           "algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
+           "pmc_frac": pmc_step_frac("rmat26", "A", t)}
+    S.close()
+    return out
 
 
 def class_table(kern, pmc):
@@ -304,6 +456,9 @@ def main():
                     help="sharded runs: JP sweep seams a fused round runs ahead of the host (gcolor_amd.shard)")
     ap.add_argument("--seam-inline-max", type=int, default=1 << 16,
                     help="sharded runs: largest inline delta part of a seam (gcolor_amd.shard)")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the R-MAT-26 measurement the default run adds (north_star object)")
+    ap.add_argument("--north-star-steps", type=int, default=3)
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
@@ -344,43 +499,31 @@ def main():
     if V == "B" and (args.priority_seed is not None or args.speculative):
         raise SystemExit("--priority-seed / --speculative are variant A modes")
     t0 = time.time()
-    dg, host_csr = build_graph(w)
+    dg0, host_csr = build_graph(w)
     gen_s = time.time() - t0
-    m = dg.nnz // 2
 
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
+    S = StepRunner(dg0, V, mode, torch, barrier)
+    info = {"n": S.n, "nnz": S.nnz, "max_degree": S.max_degree}
+    m = S.nnz // 2
+    recolour_ms = S.recolour_ms(dg0)  # the same graph kept resident (round 2's step), for reference
+    dg0.close()
     # warmup; the last warmup step brackets every launch with HIP events to find the class
     # that dominates by time, whose launches alone are then event-timed in the timed region
     # (bracketing every launch costs ~30% of the step in inter-kernel gaps)
     probe = None
     for i in range(max(args.warmup, 1)):
-        probe = dg.color(V, kernel_timing=(i == max(args.warmup, 1) - 1), want_rounds=False, want_colors=False,
-                         **mode)
+        probe, _ = S.step(timing=(i == max(args.warmup, 1) - 1))
     dom_class = max(probe.kernels.items(), key=lambda kv: kv[1]["ms"])[0]
-    barrier()
-    # Timed region: K full colourings from the resident CSR, no events.  Then the same K
-    # steps again with the dominant class's launch runs bracketed by HIP events on the
-    # engine's own stream (the roofline's launch durations).
-    def steps(timing):
-        kern = {}
-        r = None
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            r = dg.color(V, kernel_timing=timing, want_rounds=False, want_colors=False, **mode)
-            for k, v in r.kernels.items():
-                a = kern.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0.0})
-                a["ms"] += v["ms"]
-                a["launches"] += v["launches"]
-                a["bytes"] += v["bytes"]
-        barrier()
-        return (time.perf_counter() - t0) / args.steps, kern, r
-
-    t, kern, r = steps(None)
+    # Timed region: K full steps: resident CSR -> graph with its rank
+    # partition -> colouring (hub index built inside) -> validation -> handle released, no
+    # events.  Then the same K steps again with the dominant class's launch runs bracketed by
+    # HIP events on the engine's own stream (the roofline's launch durations).
+    t, kern, r, phases = S.steps(args.steps, None, roctx=True)
     rounds, sweeps, reseeds, colours = r.rounds, r.jp_sweeps, r.reseeds, r.num_colors
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
@@ -388,16 +531,8 @@ def main():
         t = float(tt.item())
     t_ev = None
     if not args.no_event_timing:
-        t_ev, kern, _ = steps(dom_class)
-    for a in kern.values():
-        a["ms"] /= args.steps
-        a["launches"] //= args.steps
-        a["bytes"] /= args.steps
+        t_ev, kern, _, _ = S.steps(args.steps, dom_class)
 
-    # validity of the colouring (outside the timed region)
-    res = dg.color(V, want_colors=True, want_rounds=False, **mode)
-    unc, conf = dg.validate()
-    assert unc == 0 and (conf == 0 or not dg.symmetric), f"invalid colouring: {unc} uncoloured, {conf} conflicts"
     pmc, pmc_src = pmc_class_bytes(args.workload, V)
     dom = kern[dom_class]
     launches = max(dom["launches"], 1)
@@ -410,18 +545,25 @@ def main():
         basis, achieved = "rocprofv3 FETCH_SIZE+WRITE_SIZE (class has no §8d credit)", traffic / (avg_ms / 1e3) / 1e9
     else:
         basis, achieved = None, None
-    balg = sum(v["bytes"] for v in kern.values()) + 20.0 * dg.n + 8.0 * dg.nnz
+    balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
     cpu = None
+    final = None
     if world == 1 and not args.no_cpu_baseline and V == "A" and args.priority_seed is None and not args.speculative:
-        cpu = cpu_baseline(w, host_csr, dg, res.colors)
+        final = S.final_colouring()  # outside the timed region
+        cpu = cpu_baseline(w, host_csr or final["csr"], final["colors"])
         assert cpu.pop("identical"), "GPU colouring differs from the CPU restatement"
         cpu.pop("colors")
         cpu.pop("seconds")
+    ns = None
+    if world == 1 and args.workload == "rmat24" and not args.no_north_star and V == "A" and not any(mode.values()):
+        S.close()
+        ns = north_star(torch, barrier, args)
+    classes = class_table(probe.kernels, pmc)
     line = {
         "metric": METRIC,
         "value": m / t,
@@ -431,20 +573,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": w["desc"], "n": dg.n, "m_undirected": m, "nnz": dg.nnz,
-                   "max_degree": dg.max_degree, "variant": "A (coloring.py)" if V == "A" else
+        "config": {"workload": w["desc"], "n": info["n"], "m_undirected": m, "nnz": info["nnz"],
+                   "max_degree": info["max_degree"], "variant": "A (coloring.py)" if V == "A" else
                    "B (coloring_optimized.py)", "parallelism": "replicas" if world > 1 else "single",
                    "rank": ("(deg, pos) (coloring.py:64)" if args.priority_seed is None
                             else f"prio_hash(seed={args.priority_seed}, v), pos"),
                    "resolution": "speculative first-fit, one-shot" if args.speculative else "Jones-Plassmann LFMIS",
+                   "step": "resident CSR (HBM, rows in generation order) -> gc_graph_create_device (rank "
+                           "partition) -> gc_color (hub index built inside) -> gc_validate -> destroy",
                    "rounds": rounds, "jp_extra_sweeps": sweeps, "reseeds": reseeds,
                    "graph_build_s": round(gen_s, 2),
                    "event_timed_class": None if args.no_event_timing else dom_class},
         "colors_used": colours,
+        "phases_ms": {k: round(v * 1e3, 3) for k, v in phases.items()},
+        "recolour_ms": round(recolour_ms, 3),
         "roofline": {"bound": "hbm", "kernel": dom_class, "kernels": CLASS_KERNELS.get(dom_class),
                      "achieved": achieved, "achieved_basis": basis, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
@@ -453,10 +599,15 @@ def main():
                      "launches_per_step": dom["launches"],
                      "share_of_step": dom["ms"] / (t_ev * 1e3) if t_ev else None,
                      "event_pass_ms_per_step": t_ev and t_ev * 1e3},
-        "classes_probe_step": class_table(probe.kernels, pmc),
+        "classes_probe_step": classes,
         # whole job, §8d algorithmic bytes / t: a work-efficiency ratio against the peak, NOT
-        # bandwidth (hub bitmaps skip row reads §8d credits)
+        # bandwidth (hub bitmaps skip row reads §8d credits); the capped figure credits no class
+        # more bytes than the peak could move in its time
         "whole_job_algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
+        "whole_job_algorithmic_frac_capped": capped_alg(probe.kernels, info["n"], info["nnz"]) / t / 1e9
+                                              / HBM_PEAK_GBS,
+        "whole_job_pmc_frac": pmc_step_frac(args.workload, V, t),
+        "north_star": ns,
         "cpu_baseline": cpu,
     }
     s = json.dumps(line)

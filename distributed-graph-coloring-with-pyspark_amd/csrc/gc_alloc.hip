@@ -90,6 +90,9 @@ hipError_t alloc(void** p, size_t bytes, bool host) {
 hipError_t gc_dmalloc(void** p, size_t bytes) { return alloc(p, bytes, false); }
 hipError_t gc_hmalloc(void** p, size_t bytes) { return alloc(p, bytes, true); }
 
+// parked bytes beyond this are freed at once (one graph's buffers fit many times over)
+static const size_t kIdleCap = (size_t)64 << 30;
+
 hipError_t gc_dfree(void* p) {
     if (!p) return hipSuccess;
     Cache& c = cache();
@@ -98,6 +101,7 @@ hipError_t gc_dfree(void* p) {
     if (it == c.live.end()) return hipFree(p);  // not ours (never expected)
     const Block b = it->second;
     c.live.erase(it);
+    if (c.idle_bytes + b.bytes > kIdleCap) return b.host ? hipHostFree(p) : hipFree(p);
     c.idle.insert({{b.host ? -1 : b.device, b.bytes}, p});
     c.idle_bytes += b.bytes;
     return hipSuccess;
@@ -108,6 +112,15 @@ extern "C" int gc_release_cache(void) {
     std::lock_guard<std::mutex> lk(c.mu);
     release_locked(c);
     return GC_OK;
+}
+
+// one-off buffers (generators): not cached; a failure releases the cache and retries once
+hipError_t gc_raw_malloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+    gc_release_cache();
+    return hipMalloc(p, bytes ? bytes : 1);
 }
 
 size_t gc_cache_idle_bytes(void) {

@@ -98,7 +98,9 @@ struct gc_graph {
     unsigned* seg_cls = nullptr;  // per segment and thread: 16 x 2-bit classes
     long long* seg_base = nullptr;  // [ntiles + 1] exclusive scan of the tiles' segment counts; [ntiles] = total
     long long nseg_cap = 0;
-    unsigned* hubmap = nullptr;   // bit per vertex: hid >= 0 (symmetric hub transpose)
+    unsigned* hubmap = nullptr;   // bit per vertex: hid >= 0
+    unsigned* hubpre = nullptr;   // hubs in the words before (id-order index of a hub = hubpre + rank in its word)
+    int* hperm = nullptr;         // id-order index -> hub index (rank order)
 };
 
 // caching allocator (gc_alloc.hip): every device / pinned-host buffer of the library
@@ -106,6 +108,7 @@ hipError_t gc_dmalloc(void** p, size_t bytes);
 hipError_t gc_hmalloc(void** p, size_t bytes);
 hipError_t gc_dfree(void* p);
 size_t gc_cache_idle_bytes(void);  // parked bytes (count as free memory)
+hipError_t gc_raw_malloc(void** p, size_t bytes);  // uncached (one-off buffers); releases the cache on failure
 
 // gc_prep.hip: tiling, rank partition, validation and hub-transpose passes
 int gc_build_tiling(gc_graph* g);

@@ -395,7 +395,7 @@ extern "C" int gc_graph_create_mesh(int64_t nx, int64_t ny, int64_t nz, gc_graph
     int* raw = nullptr;
     if ((rc = alloc_scratch(g, &raw))) return rc;
     long long* cnt = nullptr;
-    if (hipMalloc((void**)&cnt, sizeof(long long) * (size_t)(n + 1)) != hipSuccess) {
+    if (gc_raw_malloc((void**)&cnt, sizeof(long long) * (size_t)(n + 1)) != hipSuccess) {
         gc_dfree(raw); gc_free_all(g); delete g; gc_set_error("mesh alloc failed"); return GC_ENOMEM;
     }
     hipLaunchKernelGGL(k_mesh_deg, dim3(grid_for(n)), dim3(GC_BLOCK), 0, g->stream, nx, ny, nz, cnt);
@@ -429,9 +429,9 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
     long long nuniq = 0, nnz = 0;
     gc_graph* g = nullptr;
     do {
-        if (hipMalloc((void**)&k0, sizeof(ull) * (size_t)m2) != hipSuccess ||
-            hipMalloc((void**)&k1, sizeof(ull) * (size_t)m2) != hipSuccess ||
-            hipMalloc((void**)&d_count, sizeof(size_t)) != hipSuccess) {
+        if (gc_raw_malloc((void**)&k0, sizeof(ull) * (size_t)m2) != hipSuccess ||
+            gc_raw_malloc((void**)&k1, sizeof(ull) * (size_t)m2) != hipSuccess ||
+            gc_raw_malloc((void**)&d_count, sizeof(size_t)) != hipSuccess) {
             gc_set_error("R-MAT key buffers (%lld keys) do not fit", m2);
             rc = GC_ENOMEM;
             break;
@@ -443,7 +443,7 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
         size_t bytes_u = 0;
         rocprim::unique(nullptr, bytes_u, k1, k0, d_count, (size_t)m2, rocprim::equal_to<ull>(), s);
         bytes = std::max(bytes, bytes_u);
-        if (hipMalloc(&tmp, bytes ? bytes : 1) != hipSuccess) { gc_set_error("sort temp alloc failed"); rc = GC_ENOMEM; break; }
+        if (gc_raw_malloc(&tmp, bytes ? bytes : 1) != hipSuccess) { gc_set_error("sort temp alloc failed"); rc = GC_ENOMEM; break; }
         if (rocprim::radix_sort_keys(tmp, bytes, k0, k1, (size_t)m2, 0, 2 * scale, s) != hipSuccess ||
             rocprim::unique(tmp, bytes, k1, k0, d_count, (size_t)m2, rocprim::equal_to<ull>(), s) != hipSuccess) {
             gc_set_error("R-MAT sort/unique failed");
@@ -465,7 +465,7 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
         tmp = nullptr;
         hipSetDevice(dev);
         if ((rc = new_graph(out, n, nnz, GC_GRAPH_SYMMETRIC, &g))) break;
-        if (hipMalloc((void**)&raw, sizeof(int) * (size_t)std::max<long long>(nnz, 1)) != hipSuccess) {
+        if (gc_raw_malloc((void**)&raw, sizeof(int) * (size_t)std::max<long long>(nnz, 1)) != hipSuccess) {
             gc_set_error("R-MAT rows (%lld entries) do not fit", nnz);
             rc = GC_ENOMEM;
             break;

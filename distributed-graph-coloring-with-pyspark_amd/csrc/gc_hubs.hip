@@ -24,7 +24,9 @@
 // results stay bit-identical to the row-scan engine (and to the oracle).  The cost moves
 // to the low-degree side -- one walk of a vertex's hin row when it is coloured (bitmaps)
 // and one when it wins (flags) -- instead of every hub re-reading its row every round.
+#include <chrono>
 #include <numeric>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -36,16 +38,31 @@
 
 namespace {
 
-__global__ void k_hub_flag(const int* deg, long long n, int T, long long* f) {
-    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (long long)gridDim.x * blockDim.x)
-        f[v] = v < n && deg[v] > T ? 1 : 0;
+// hub bitmap (bit per vertex: deg > T) by ballot, and its per-word counts
+__global__ void k_hub_bits(const int* deg, long long n, int T, unsigned* map, unsigned* wcnt) {
+    const long long words = (n + 31) / 32;
+    for (long long v0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n;
+         v0 += (long long)gridDim.x * blockDim.x) {
+        const long long v = v0 + gc_lane();
+        const ull m = __ballot(v < n && deg[v] > T);
+        const long long w = v0 >> 5;
+        if (gc_lane() == 0) {
+            map[w] = (unsigned)m;
+            wcnt[w] = __popc((unsigned)m);
+        } else if (gc_lane() == 32 && w + 1 < words) {
+            map[w + 1] = (unsigned)(m >> 32);
+            wcnt[w + 1] = __popc((unsigned)(m >> 32));
+        }
+    }
 }
 
-__global__ void k_hub_ids(const int* deg, long long n, int T, const long long* pos, int* hid, int* hub_v) {
+// the hubs in vertex order (id-order index = hubpre[w] + rank within the word); hid = -1 elsewhere
+__global__ void k_hub_ids(long long n, const unsigned* map, const unsigned* pre, int* hid, int* hub_v) {
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
-        const bool h = deg[v] > T;
-        hid[v] = h ? (int)pos[v] : -1;
-        if (h) hub_v[pos[v]] = (int)v;
+        const unsigned m = map[v >> 5];
+        const unsigned bit = 1u << (v & 31);
+        hid[v] = -1;
+        if (m & bit) hub_v[pre[v >> 5] + __popc(m & (bit - 1u))] = (int)v;
     }
 }
 
@@ -57,11 +74,14 @@ __global__ void k_hub_keys(const int* deg, const int* hub_v, long long H, ull* k
         keys[x] = ((ull)(unsigned)deg[v] << 32) | (ull)(unsigned)v;
     }
 }
-__global__ void k_hub_reindex(const ull* keys, long long H, int* hid, int* hub_v) {
+__global__ void k_hub_reindex(const ull* keys, long long H, int* hid, int* hub_v, const unsigned* map,
+                              const unsigned* pre, int* hperm) {
     for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < H; x += (long long)gridDim.x * blockDim.x) {
         const int v = (int)(keys[x] & 0xFFFFFFFFull);
         hub_v[x] = v;
         hid[v] = (int)x;
+        const unsigned bit = 1u << (v & 31);
+        hperm[pre[v >> 5] + __popc(map[v >> 5] & (bit - 1u))] = (int)x;  // id-order index -> hub index
     }
 }
 
@@ -142,6 +162,18 @@ int scan_ll(const long long* in, long long* out, long long count, hipStream_t s)
     return GC_OK;
 }
 
+int scan_u32(const unsigned* in, unsigned* out, long long count, hipStream_t s) {
+    size_t bytes = 0;
+    GC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, (size_t)count, rocprim::plus<unsigned>(), s));
+    void* tmp = nullptr;
+    GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
+    hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0u, (size_t)count, rocprim::plus<unsigned>(), s);
+    hipStreamSynchronize(s);
+    gc_dfree(tmp);
+    GC_HIP(e);
+    return GC_OK;
+}
+
 int grid_of(long long items) {
     return (int)std::max<long long>(1, std::min<long long>((items + GC_BLOCK - 1) / GC_BLOCK, 8192));
 }
@@ -155,19 +187,40 @@ int env_int(const char* name, int dflt) {
     return atoi(e);
 }
 
+// GC_PREP_TIMING=1: host-side phase times of the hub build on stderr (each phase ends in a
+// stream synchronisation)
+struct PhaseClock {
+    bool on = getenv("GC_PREP_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what, hipStream_t s) {
+        if (!on) return;
+        hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[gc hubs] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 int build(gc_graph* g, int T, int W) {
+    PhaseClock pc;
     hipStream_t s = g->stream;
     const long long n = g->n;
-    long long *pos = nullptr, *flag = nullptr;
-    GC_HIP(gc_dmalloc((void**)&pos, sizeof(long long) * (size_t)(n + 1)));
-    GC_HIP(gc_dmalloc((void**)&flag, sizeof(long long) * (size_t)(n + 1)));
-    hipLaunchKernelGGL(k_hub_flag, dim3(grid_of(n + 1)), dim3(GC_BLOCK), 0, s, g->deg, n, T, flag);
-    int rc = scan_ll(flag, pos, n + 1, s);
-    gc_dfree(flag);
-    long long H = 0;
-    if (!rc && hipMemcpy(&H, pos + n, sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess) rc = GC_EHIP;
+    // hub bitmap + per-word prefix counts (the hub transpose resolves an entry's hub index
+    // from them: 2 + 2 MB on R-MAT-24 against the 67 MB hid array)
+    const long long words = (n + 31) / 32;
+    if (!g->hubmap) GC_HIP(gc_dmalloc((void**)&g->hubmap, sizeof(unsigned) * (size_t)std::max<long long>(words, 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hubpre, sizeof(unsigned) * (size_t)(words + 1)));
+    unsigned* wcnt = nullptr;
+    GC_HIP(gc_dmalloc((void**)&wcnt, sizeof(unsigned) * (size_t)(words + 1)));
+    GC_HIP(hipMemsetAsync(wcnt + words, 0, sizeof(unsigned), s));
+    hipLaunchKernelGGL(k_hub_bits, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, g->deg, n, T, g->hubmap, wcnt);
+    int rc = scan_u32(wcnt, g->hubpre, words + 1, s);
+    gc_dfree(wcnt);
+    unsigned Hu = 0;
+    if (!rc && hipMemcpy(&Hu, g->hubpre + words, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) rc = GC_EHIP;
+    const long long H = Hu;
+    long long* pos = nullptr;
     if (rc || H == 0) {
-        gc_dfree(pos);
         g->hub_t = T;
         g->nhub = 0;
         return rc;
@@ -178,15 +231,18 @@ int build(gc_graph* g, int T, int W) {
     freeb += gc_cache_idle_bytes();
     const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (28.0 + 4.0 * W) * (double)H;
     if (need > 0.5 * (double)freeb) {  // no room: row scans as before
-        gc_dfree(pos);
         g->hub_t = T;
         g->nhub = 0;
         return GC_OK;
     }
     g->nhub = H;
+    GC_HIP(gc_dmalloc((void**)&pos, sizeof(long long) * (size_t)(n + 1)));
     GC_HIP(gc_dmalloc((void**)&g->hid, sizeof(int) * (size_t)std::max<long long>(n, 1)));
     GC_HIP(gc_dmalloc((void**)&g->hub_v, sizeof(int) * (size_t)H));
-    hipLaunchKernelGGL(k_hub_ids, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, g->deg, n, T, pos, g->hid, g->hub_v);
+    GC_HIP(gc_dmalloc((void**)&g->hperm, sizeof(int) * (size_t)H));
+    hipLaunchKernelGGL(k_hub_ids, dim3(grid_of(n)), dim3(GC_BLOCK), 0, s, n, (const unsigned*)g->hubmap,
+                       (const unsigned*)g->hubpre, g->hid, g->hub_v);
+    pc.mark("bitmap+ids", s);
     {  // re-index the hubs in rank order
         ull *k0 = nullptr, *k1 = nullptr;
         GC_HIP(gc_dmalloc((void**)&k0, sizeof(ull) * (size_t)H));
@@ -198,13 +254,15 @@ int build(gc_graph* g, int T, int W) {
         GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
         const hipError_t e = rocprim::radix_sort_keys(tmp, bytes, k0, k1, (size_t)H, 0, 64, s);
         if (e == hipSuccess)
-            hipLaunchKernelGGL(k_hub_reindex, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const ull*)k1, H, g->hid, g->hub_v);
+            hipLaunchKernelGGL(k_hub_reindex, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const ull*)k1, H, g->hid, g->hub_v,
+                               (const unsigned*)g->hubmap, (const unsigned*)g->hubpre, g->hperm);
         hipStreamSynchronize(s);
         gc_dfree(tmp);
         gc_dfree(k0);
         gc_dfree(k1);
         GC_HIP(e);
     }
+    pc.mark("rank sort", s);
     const int hgrid = (int)std::max<long long>(1, std::min<long long>((H + 3) / 4, 8192));
     long long E = 0, EL = 0;
     const bool sym = (g->flags & GC_GRAPH_SYMMETRIC) != 0;
@@ -222,6 +280,7 @@ int build(gc_graph* g, int T, int W) {
     GC_HIP(gc_dmalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
     if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { gc_dfree(pos); gc_dfree(klow); return rc; }
     GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
+    pc.mark("hin count", s);
     hipMemGetInfo(&freeb, &totalb);
     freeb += gc_cache_idle_bytes();
     const double need2 = 24.0 * (double)E + (28.0 + 4.0 * W) * (double)H;  // hin + hlow copies <= 5 E
@@ -267,6 +326,7 @@ int build(gc_graph* g, int T, int W) {
         hipLaunchKernelGGL(k_hlow_fill, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->nlow, g->hid, g->hub_v,
                            H, g->hlow_rp, g->hlow_col);
     }
+    pc.mark("hin fill", s);
     if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
         size_t bytes = 0;
         GC_HIP(rocprim::segmented_radix_sort_keys(nullptr, bytes, g->hlow_col, g->hpend[0], (unsigned)EL, (unsigned)H,
@@ -281,6 +341,7 @@ int build(gc_graph* g, int T, int W) {
         std::swap(g->hlow_col, g->hpend[0]);  // the unsorted copy becomes working memory
     }
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
+    pc.mark("hlow sort", s);
     hipLaunchKernelGGL(k_hch_count, dim3(grid_of(H + 1)), dim3(GC_BLOCK), 0, s, g->hlow_rp, H, pos);
     GC_HIP(gc_dmalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
     if ((rc = scan_ll(pos, g->hch_rp, H + 1, s))) { gc_dfree(pos); return rc; }
@@ -294,17 +355,21 @@ int build(gc_graph* g, int T, int W) {
     gc_dfree(pos);
     g->hub_t = T;
     g->hub_w = W;
+    pc.mark("chunks", s);
+    if (pc.on) fprintf(stderr, "[gc hubs] H=%lld E=%lld EL=%lld\n", H, E, EL);
     return GC_OK;
 }
 
 }  // namespace
 
 void gc_hubs_free(gc_graph* g) {
-    void* ptrs[] = {g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
+    void* ptrs[] = {g->hubpre, g->hperm, g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
                     g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen,
                     g->hch_rp, g->hch_own, g->hkcnt, g->hk};
     for (void* p : ptrs)
         if (p) gc_dfree(p);
+    g->hubpre = nullptr;
+    g->hperm = nullptr;
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;
     g->hlow2[0] = g->hlow2[1] = g->hrow = g->hlen = nullptr;
     g->hin_rp = g->hlow_rp = g->hch_rp = nullptr;

@@ -547,6 +547,8 @@ struct HubArgs {
     const int* nlow;
     const int* hid;
     const unsigned* hubmap;
+    const unsigned* hubpre;  // hub index of u = hperm[hubpre[u >> 5] + rank of u in its word]
+    const int* hperm;
     long long* hin_cnt;  // count pass: per row
     long long* klow;     // count pass: per hub
     const long long* hin_rp;  // fill pass
@@ -666,7 +668,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
                 if (!((mk >> k) & 1u)) continue;
                 const int r = rk[k];
                 const unsigned rank = f16(prefix, 0) + __popc(mk & ((1u << k) - 1u)) - f16(S.base[r], 0);
-                a.hin_col[a.hin_rp[r0 + r] + rank] = a.hid[u[k]];
+                const unsigned bit = 1u << (u[k] & 31);
+                a.hin_col[a.hin_rp[r0 + r] + rank] = a.hperm[a.hubpre[u[k] >> 5] + __popc(a.hubmap[u[k] >> 5] & (bit - 1u))];
             }
         } else {
             const long long s = it - nt;
@@ -698,21 +701,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
             int o = 0;
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k)
-                if ((mk >> k) & 1u) a.hin_col[base + o++] = a.hid[uu[k]];
+                if ((mk >> k) & 1u) {
+                    const unsigned bit = 1u << (uu[k] & 31);
+                    a.hin_col[base + o++] = a.hperm[a.hubpre[uu[k] >> 5] + __popc(w[k] & (bit - 1u))];
+                }
         }
         __syncthreads();
-    }
-}
-
-__global__ void k_hubmap(const int* hid, long long n, unsigned* map) {
-    const long long words = (n + 31) / 32;
-    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (long long)gridDim.x * blockDim.x) {
-        unsigned m = 0;
-        for (int k = 0; k < 32; ++k) {
-            const long long v = w * 32 + k;
-            if (v < n && hid[v] >= 0) m |= 1u << k;
-        }
-        map[w] = m;
     }
 }
 
@@ -829,14 +823,11 @@ int gc_validate_tiles(gc_graph* g, const int* colors) {
     return GC_OK;
 }
 
-// hubmap from hid, then the count pass: hin_cnt (n + 1, zeroed here) and klow (H + 1)
+// the count pass (hubmap / hubpre / hperm ready): hin_cnt (n + 1, zeroed here) and klow (H + 1)
 int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow) {
     const hipStream_t s = g->stream;
     int rc = gc_build_tiling(g);
     if (rc) return rc;
-    const long long words = (g->n + 31) / 32;
-    if (!g->hubmap) GC_HIP(gc_dmalloc((void**)&g->hubmap, sizeof(unsigned) * (size_t)std::max<long long>(words, 1)));
-    hipLaunchKernelGGL(k_hubmap, dim3(small_grid(words)), dim3(GC_BLOCK), 0, s, (const int*)g->hid, g->n, g->hubmap);
     GC_HIP(hipMemsetAsync(hin_cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
     GC_HIP(hipMemsetAsync(klow, 0, sizeof(long long) * (size_t)(H + 1), s));
     HubArgs a;
@@ -845,6 +836,8 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long
     a.nlow = g->nlow;
     a.hid = g->hid;
     a.hubmap = g->hubmap;
+    a.hubpre = g->hubpre;
+    a.hperm = g->hperm;
     a.hin_cnt = hin_cnt;
     a.klow = klow;
     a.hin_rp = nullptr;
@@ -864,6 +857,8 @@ int gc_hub_transpose_fill(gc_graph* g, long long H) {
     a.nlow = g->nlow;
     a.hid = g->hid;
     a.hubmap = g->hubmap;
+    a.hubpre = g->hubpre;
+    a.hperm = g->hperm;
     a.hin_cnt = nullptr;
     a.klow = nullptr;
     a.hin_rp = g->hin_rp;

@@ -1,0 +1,64 @@
+#!/bin/bash
+# One gpurun session: a list of steps, each under its own time limit, chained so that the
+# first failure ends the session (no GPU step runs after a fault, abort or timeout).
+#   bash tools/gpu_session.sh TAG STEP [STEP ...]
+# Steps:
+#   tests             pytest -m gpu (every GPU test)
+#   tests:EXPR        pytest -m gpu -k EXPR
+#   file:PATH[:EXPR]  pytest -m gpu on one test file (optionally -k EXPR)
+#   smoke             __graft_entry__.smoke()
+#   bench:WL[:ARGS]   bench.py --workload WL [ARGS, comma-separated]
+#   step:WL           tools/step_timing.py WL (phase times of the step)
+#   profile:WL[:ARGS] tools/gpu_profile.sh TAG WL [ARGS] (trace + PMC passes, summaries)
+# Output: gpurun_out/TAG/ (merged back by gpurun).
+set -uo pipefail
+TAG=$1
+shift
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$ROOT/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$ROOT"
+i=0
+for st in "$@"; do
+  i=$((i + 1))
+  kind=${st%%:*}
+  rest=${st#*:}
+  [ "$rest" = "$st" ] && rest=""
+  log="$O/$(printf %02d $i)_${kind}.log"
+  echo "== step $i: $st" | tee -a "$O/session.log"
+  case $kind in
+    tests)
+      if [ -n "$rest" ]; then
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$rest" > "$log" 2>&1
+      else
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
+      fi ;;
+    file)
+      f=${rest%%:*}; k=${rest#*:}; [ "$k" = "$rest" ] && k=""
+      if [ -n "$k" ]; then
+        timeout -k 10 1000 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread -k "$k" > "$log" 2>&1
+      else
+        timeout -k 10 1000 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
+      fi ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
+    bench)
+      wl=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      timeout -k 10 600 python -u bench.py --workload "$wl" ${a//,/ } --json-out "$O/bench_${wl}.json" > "$log" 2>&1 ;;
+    step)
+      timeout -k 10 400 python -u tools/step_timing.py "$rest" 4 > "$log" 2>&1 ;;
+    profile)
+      wl=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      bash tools/gpu_profile.sh "$TAG" "$wl" ${a//,/ } > "$log" 2>&1 ;;
+    *)
+      echo "unknown step $st" > "$log"; false ;;
+  esac
+  rc=$?
+  tail -3 "$log" | cut -c1-400 | tee -a "$O/session.log"
+  if [ $rc -ne 0 ]; then
+    echo "== step $i ($st) failed: rc=$rc" | tee -a "$O/session.log"
+    tail -40 "$log"
+    exit $rc
+  fi
+done
+echo "== session $TAG done" | tee -a "$O/session.log"

@@ -30,14 +30,21 @@ def per_kernel(path, counter):
     return {k: (c, v) for k, (c, v) in agg.items()}
 
 
-def main(d):
+def totals(d, tag):
+    f = per_kernel(os.path.join(d, f"pmc_fetch{tag}", "run_counter_collection.csv"), "FETCH_SIZE")
+    w = per_kernel(os.path.join(d, f"pmc_write{tag}", "run_counter_collection.csv"), "WRITE_SIZE")
+    return sum(v for _, v in f.values()) * 1024, sum(v for _, v in w.values()) * 1024
+
+
+def main(d, steps=None):
     stats = {}
     p = os.path.join(d, "trace", "run_kernel_stats.csv")
     for r in csv.DictReader(open(p)):
         stats[r["Name"]] = {"launches": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
                             "total_ms": float(r["TotalDurationNs"]) / 1e6, "pct": float(r["Percentage"])}
-    fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    tag = "3" if os.path.isdir(os.path.join(d, "pmc_fetch3")) else ""
+    fetch = per_kernel(os.path.join(d, f"pmc_fetch{tag}", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, f"pmc_write{tag}", "run_counter_collection.csv"), "WRITE_SIZE")
     out = {}
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"]):
         e = dict(s)
@@ -51,9 +58,16 @@ def main(d):
         if "fetch_bytes_per_launch" in e and "write_bytes_per_launch" in e:
             e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
         out[k] = e
+    if tag == "3" and os.path.isdir(os.path.join(d, "pmc_fetch1")):
+        f3, w3 = totals(d, "3")
+        f1, w1 = totals(d, "1")
+        fb, wb = (f3 - f1) / 2, (w3 - w1) / 2
+        out["_step"] = {"steps": 1, "bytes": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
+                        "note": "FETCH_SIZE + WRITE_SIZE of every kernel, (run at 3 timed steps - run at 1) / 2: "
+                                "one step, as counted (KiB x 1024)"}
     json.dump(out, sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
