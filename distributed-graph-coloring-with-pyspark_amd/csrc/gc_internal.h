@@ -163,6 +163,7 @@ struct DevCtl {
     int proposed;           // the current round's proposals were made by the last (fused) commit
     int pad3;
     long long acc_last;     // shards: winners of the last finished round (k_shard_reset keeps them for the seam header)
+    long long acc_round;    // shards: round + 1 whose reset took acc_last (a repeated propose seam keeps it)
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };

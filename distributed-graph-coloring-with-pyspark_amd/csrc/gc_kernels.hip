@@ -2262,7 +2262,10 @@ __global__ void k_shard_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
     if (c->halt == GC_H_SWEEPS) return;  // the last finish halted: everything stays for gc_shard_resume_hubs
-    c->acc_last = (long long)c->accepted;
+    if (c->acc_round != round + 1) {  // a repeated seam (after a hub halt) keeps the first reset's count:
+        c->acc_last = (long long)c->accepted;  // `accepted` was zeroed by it
+        c->acc_round = round + 1;
+    }
     c->halt = GC_RUN;
     c->round = round;
     c->heavy_cnt = 0;

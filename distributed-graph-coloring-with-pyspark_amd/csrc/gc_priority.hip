@@ -186,6 +186,11 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
     if (prio != 0 && prio != 1) { gc_set_error("unknown priority %d", prio); return GC_EINVAL; }
     if (g->part_prio == prio && (prio == 0 || g->part_seed == seed)) return GC_OK;
     if (g->borrowed) { gc_set_error("a shard view cannot change the row partition"); return GC_EINVAL; }
+    if (g->shard_refs > 0) {  // shards read col / nlow and the hub lists built under the (deg, pos) rank
+        gc_set_error("%d shard(s) borrow this graph's (deg, pos) partition: destroy them before changing the priority",
+                     g->shard_refs);
+        return GC_EINVAL;
+    }
     const hipStream_t s = g->stream;
     if (g->n > 0 && g->nnz > 0) {
         int* tmp = nullptr;

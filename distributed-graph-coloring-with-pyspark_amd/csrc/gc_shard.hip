@@ -33,6 +33,7 @@ struct gc_shard {
     // bitmaps are this rank's replica, kept current by pushes from every winner, the rank's
     // own (k_commit) and the others' (k_shard_list_commit / k_shard_scan_commit).
     gc_graph* parent = nullptr;
+    gc_graph* owner = nullptr;  // the graph whose rows this shard borrows (its shard_refs counts us)
     unsigned* hbits = nullptr;
     int hub_w = 0;
     long long nhub = 0;
@@ -193,12 +194,15 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
         gc_set_error("%s", keep.c_str());
         return rc;
     }
+    sh->owner = g;
+    g->shard_refs++;
     *out = sh;
     return GC_OK;
 }
 
 extern "C" void gc_shard_destroy(gc_shard* sh) {
     if (!sh) return;
+    if (sh->owner) sh->owner->shard_refs--;
     gc_free_all(&sh->v);
     shard_free_hubs(sh);
     delete sh;
@@ -209,6 +213,11 @@ extern "C" void gc_shard_destroy(gc_shard* sh) {
 extern "C" int gc_shard_begin(gc_shard* sh, int64_t num_colors, int32_t track_rounds, int64_t* U_out, int64_t* F_out) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
+    if (sh->owner && (sh->owner->part_prio != GC_PRIORITY_REF ||
+                      (sh->parent && (sh->parent->nhub != sh->nhub || sh->parent->hub_prio != GC_PRIORITY_REF)))) {
+        gc_set_error("gc_shard_begin: the parent graph's row partition or hub lists changed under the shard");
+        return GC_EINVAL;
+    }
     GC_HIP(hipSetDevice(g->device));
     DevCtl& h = *g->hctl;
     memset(&h, 0, sizeof(DevCtl));
@@ -271,6 +280,14 @@ extern "C" int gc_shard_set_stream(gc_shard* sh, void* stream) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;
     GC_HIP(hipSetDevice(g->device));
+    if (stream) {  // a stream of another GPU would run the shard's kernels on the wrong device
+        hipDevice_t sd = -1;
+        GC_HIP(hipStreamGetDevice(reinterpret_cast<hipStream_t>(stream), &sd));
+        if ((int)sd != g->device) {
+            gc_set_error("gc_shard_set_stream: the stream belongs to device %d, the graph to device %d", (int)sd, g->device);
+            return GC_EINVAL;
+        }
+    }
     GC_HIP(hipStreamSynchronize(g->stream));
     if (g->own_stream && g->stream) GC_HIP(hipStreamDestroy(g->stream));
     g->stream = reinterpret_cast<hipStream_t>(stream);

@@ -363,12 +363,6 @@ H_SWEEPS = 5  # halt code of a checked finish whose hub JP had not converged (GC
 H_SEAM = 7    # halt code of a fused propose seam that could not be applied (GC_H_SEAM)
 
 
-def _hdr_words(vals):
-    """Header values as int64 words that read as padding to the delta appliers (vertex
-    field -1): (0xFFFFFFFF << 32) | value, value as unsigned 32 bits."""
-    return torch.tensor([((0xFFFFFFFF << 32) | (int(x) & 0xFFFFFFFF)) - (1 << 64) for x in vals], dtype=torch.int64)
-
-
 def _hdr_values(words):
     """int64 array [P, HDR] of header words -> their signed 32-bit values."""
     x = np.asarray(words, dtype=np.int64) & 0xFFFFFFFF

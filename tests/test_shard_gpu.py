@@ -106,6 +106,25 @@ def test_uniform_and_mesh_sharded():
         same_as_single(dg, 2, deferred=False)
 
 
+def test_seeded_colour_between_sharded_runs():
+    """A seeded colouring re-partitions the rows in place (gc_set_priority): refused while a
+    shard borrows the (deg, pos) partition, allowed once it is gone, and a shard created
+    after it runs the reference rank again, bit-identical to one GPU."""
+    from gcolor_amd import _native as nat
+    from gcolor_amd import shard as sh
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(11, 16, seed=3) as dg:
+        same_as_single(dg, 2)
+        live = sh.HipShard(dg, 0, dg.n)
+        with pytest.raises(nat.GcolorError, match="shard"):
+            dg.color("A", priority=7)
+        live.close()
+        seeded = dg.color("A", priority=7)
+        o = oracle.c_color_prio(*dg.export(), priority=1, seed=7)
+        assert np.array_equal(seeded.colors, o["colors"])
+        same_as_single(dg, 3)
+
+
 @pytest.mark.parametrize("seed", range(2))
 def test_replicated_hubs_sharded(seed, monkeypatch):
     """A low hub threshold makes most proposers replicated hubs: every rank proposes,
