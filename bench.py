@@ -72,7 +72,7 @@ CLASS_KERNELS = {
     "init": ["k_init", "k_seed_prep"],
     "propose": ["k_propose", "k_propose_block"],
     "resolve": ["k_resolve"],
-    "sweep": ["k_sweep", "k_sweep_tail"],
+    "sweep": ["k_sweep", "k_sweep_tail", "k_sweep_async"],
     "commit": ["k_commit", "k_commit_big", "k_pull"],
     "reseed": ["k_unc_compact", "k_cc_hook", "k_cc_best", "k_cc_seeds"],
     "other": ["k_close", "k_pack_c4", "k_fsort_count", "k_fsort_scan", "k_fsort_write", "k_front_count",
@@ -123,14 +123,35 @@ def pmc_file(workload, variant):
     return os.path.join(REPO, "profiles", "pmc", f"{workload}{'' if variant == 'A' else '_B'}.json")
 
 
+def lib_sha16():
+    """First 16 hex digits of sha256(libgcolor.so): the build a PMC summary describes."""
+    import hashlib
+    p = os.path.join(PKG_DIR, "gcolor_amd", "lib", "libgcolor.so")
+    if not os.path.exists(p):
+        return None
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+
+
+def pmc_summary(workload, variant):
+    """The rocprofv3 per-kernel summary of this bench command (tools/gpu_profile.sh), or None
+    when it is missing or describes another build of libgcolor.so (counters of kernels that
+    have since changed are not this build's traffic)."""
+    p = pmc_file(workload, variant)
+    if not os.path.exists(p):
+        return None, None
+    per = json.load(open(p))
+    if per.get("_build") != lib_sha16():
+        return None, os.path.relpath(p, REPO) + " (stale: another build; not used)"
+    return per, os.path.relpath(p, REPO)
+
+
 def pmc_class_bytes(workload, variant):
     """Per class: HBM bytes per launch of the class (FETCH_SIZE + WRITE_SIZE, KiB x 1024,
     summed over the class's kernels and divided by their launches) from the rocprofv3
     --pmc passes of this bench command (tools/gpu_profile.sh -> tools/pmc_summary.py)."""
-    p = pmc_file(workload, variant)
-    if not os.path.exists(p):
-        return {}, None
-    per = json.load(open(p))
+    per, src = pmc_summary(workload, variant)
+    if per is None:
+        return {}, src
     out = {}
     for cls, names in CLASS_KERNELS.items():
         b = l = 0.0
@@ -141,7 +162,7 @@ def pmc_class_bytes(workload, variant):
                 l += e["launches"]
         if l:
             out[cls] = b / l
-    return out, os.path.relpath(p, REPO)
+    return out, src
 
 
 def cpu_baseline(w, host_csr, colors_gpu):
@@ -282,15 +303,12 @@ def pmc_step_frac(workload, variant, t):
     """Physical fraction of the whole step: rocprofv3 FETCH_SIZE + WRITE_SIZE of every kernel
     of the timed steps (profiles/pmc/<workload>.json "_step", a --selected-regions run of this
     bench command) / t / peak."""
-    p = pmc_file(workload, variant)
-    if not os.path.exists(p):
-        return None
-    st = json.load(open(p)).get("_step")
+    per, src = pmc_summary(workload, variant)
+    st = per.get("_step") if per else None
     if not st or not st.get("steps"):
         return None
     b = st["bytes"] / st["steps"]
-    return {"bytes_per_step": b, "GBps": b / t / 1e9, "frac": b / t / 1e9 / HBM_PEAK_GBS,
-            "source": os.path.relpath(p, REPO)}
+    return {"bytes_per_step": b, "GBps": b / t / 1e9, "frac": b / t / 1e9 / HBM_PEAK_GBS, "source": src}
 
 
 def north_star(torch, barrier, args):
@@ -539,12 +557,18 @@ def main():
     avg_ms = dom["ms"] / launches
     alg_per_launch = dom["bytes"] / launches
     traffic = pmc.get(dom_class)
-    if alg_per_launch > 0 and dom["ms"] > 0:
-        basis, achieved = "algorithmic (SURVEY.md §8d)", alg_per_launch / (avg_ms / 1e3) / 1e9
+    alg_rate = alg_per_launch / (avg_ms / 1e3) / 1e9 if dom["ms"] > 0 else 0.0
+    if alg_per_launch > 0 and dom["ms"] > 0 and alg_rate <= HBM_PEAK_GBS:
+        basis, achieved = "algorithmic (SURVEY.md §8d)", alg_rate
     elif traffic is not None and dom["ms"] > 0:
-        basis, achieved = "rocprofv3 FETCH_SIZE+WRITE_SIZE (class has no §8d credit)", traffic / (avg_ms / 1e3) / 1e9
+        basis = ("rocprofv3 FETCH_SIZE+WRITE_SIZE (" + ("class has no §8d credit" if alg_per_launch <= 0 else
+                 "§8d credits bytes the kernels do not move: hub rows replaced by pushed bitmaps") + ")")
+        achieved = traffic / (avg_ms / 1e3) / 1e9
     else:
-        basis, achieved = None, None
+        basis = ("unmeasured: " + ("the class has no §8d credit" if alg_per_launch <= 0 else
+                 "§8d credit above the HBM peak (hub bitmaps stand in for rows)") +
+                 " and no rocprofv3 summary of this build (profiles/pmc)")
+        achieved = None
     balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
 
     if rank != 0:
@@ -586,6 +610,7 @@ def main():
                    "step": "resident CSR (HBM, rows in generation order) -> gc_graph_create_device (rank "
                            "partition) -> gc_color (hub index built inside) -> gc_validate -> destroy",
                    "rounds": rounds, "jp_extra_sweeps": sweeps, "reseeds": reseeds,
+                   "async_jp_aborts": r.async_aborts,
                    "graph_build_s": round(gen_s, 2),
                    "event_timed_class": None if args.no_event_timing else dom_class},
         "colors_used": colours,

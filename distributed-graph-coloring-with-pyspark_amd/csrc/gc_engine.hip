@@ -214,7 +214,13 @@ struct KTimer {
         }
         return g->evpool[used++];
     }
+    // GC_DEBUG_SYNC: synchronise after every launch and name the kernel class of a fault
+    const bool dbg_sync = getenv("GC_DEBUG_SYNC") != nullptr;
+    int last_cls = -1;
+    long long nlaunch = 0;
     void begin(int cls) {
+        last_cls = cls;
+        ++nlaunch;
         if (st) st->k_launches[cls]++;
         if (cls == run_cls) return;  // the open run goes on
         close();
@@ -223,7 +229,15 @@ struct KTimer {
         recs.push_back({cls, used});
         hipEventRecord(ev(), g->stream);
     }
-    void end() {}
+    void end() {
+        if (!dbg_sync) return;
+        const hipError_t e = hipStreamSynchronize(g->stream);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[gc debug-sync] launch %lld (class %d) failed: %s\n", nlaunch, last_cls, hipGetErrorString(e));
+            fflush(stderr);
+            abort();
+        }
+    }
     void close() {
         if (run_cls < 0) return;
         hipEventRecord(ev(), g->stream);
@@ -259,6 +273,35 @@ struct Run {
     // (R-MAT-26 588 -> 610 ms, C2 8.0 -> 12.2 ms: a grid barrier costs about a launch, and
     // the resident grid has a quarter of the waves for the latency-bound sweeps)
     int loop_grid = 0;
+    // k_sweep_async (the default with the hub JP's resumable scan, or with no heavy vertex):
+    // the JP chain after the first sweep in ONE launch on a resident grid (CUs x blocks per
+    // CU), instead of full-grid sweeps plus the one-workgroup tail.  GC_ASYNC=0 turns it off;
+    // GC_ASYNC_BPC (blocks per CU, default 2, capped by the occupancy), GC_ASYNC_BUDGET_US
+    // (per launch, default 20000: a launch past it hands its rest to host sweeps).
+    int async_grid = 0;
+    int async_par = 0;
+    long long async_budget = 0;
+    void init_async() {
+        const char* e = getenv("GC_ASYNC");
+        if (e && atoi(e) == 0) return;
+        // Only with the hub JP's resumable scan (R-MAT and the like, validated at full size).
+        // Graphs with no hub (uniform, meshes) keep the full-grid sweeps and the tail: a
+        // 10M-vertex uniform graph with k_sweep_async on faulted in the following k_commit
+        // (round 3; DESIGN §5, open), and their JP chains are short anyway (C2: 15 rounds).
+        if (!d.hub_w || !d.hub_scan || d.heavy_wg || L.delta) return;
+        int cus = 0, rate_khz = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
+            return;
+        if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) != hipSuccess || rate_khz <= 0)
+            return;
+        int bpc = getenv("GC_ASYNC_BPC") ? atoi(getenv("GC_ASYNC_BPC")) : 2;
+        const int occ = gcl_sweep_async_blocks_per_cu();
+        bpc = std::max(1, std::min(bpc, occ - (occ > 1 ? 1 : 0)));  // the occupancy answer can be one too many
+        if (occ <= 0) return;
+        const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
+        async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
+        async_grid = cus * bpc;
+    }
     void init_loop() {
         const char* e = getenv("GC_SWEEP_LOOP");
         if (!e || atoi(e) <= 0) return;
@@ -283,6 +326,14 @@ struct Run {
         kt.close();
         GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
         GC_HIP(hipStreamSynchronize(s));
+        if (async_grid > 0) {
+            // k_sweep_async launches that were enqueued behind a halt returned at once, so the
+            // launch parity no longer says which counter slot the last launch that RAN zeroed:
+            // start both slots (and the parity) afresh before anything else is enqueued
+            GC_HIP(hipMemsetAsync(g->ctl->async_done, 0, sizeof(g->ctl->async_done), s));
+            GC_HIP(hipMemsetAsync(g->ctl->async_abort, 0, sizeof(g->ctl->async_abort), s));
+            async_par = 0;
+        }
         if (debug) {
             const DevCtl& h = *g->hctl;
             fprintf(stderr, "[gc] halt=%d round=%lld U=%lld cur=%d fcnt=%llu/%llu und=%llu/%llu/%llu undh=%llu/%llu/%llu "
@@ -321,12 +372,17 @@ struct Run {
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
         const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
-        if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch
+        if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
+            kt.begin(GC_K_SWEEP);
+            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
+            async_par ^= 1;
+            kt.end();
+        } else if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch
             kt.begin(GC_K_SWEEP);
             gcl_sweep_loop(d, L, nsweeps, loop_grid, s);
             kt.end();
         }
-        if (tail) {
+        if (tail && async_grid == 0) {
             kt.begin(GC_K_SWEEP);
             gcl_sweep_tail(d, L, nsweeps, s);
             kt.end();
@@ -419,7 +475,7 @@ struct Run {
     bool skip_tail = false;  // set with S = 0 once 16 rounds ran without a second sweep
     int pick_sweeps(const DevCtl& h) {
         skip_tail = h.maxdepth <= 1 && h.round >= 16;
-        if (h.maxdepth <= 1) return 0;
+        if (h.maxdepth <= 1 || async_grid > 0) return 0;  // k_sweep_async takes the whole chain
         // the small-list tail runs in k_sweep_tail; with the loop kernel, the full grid only
         // takes the sweeps past its limits
         if (loop_grid > 0) return (int)std::min<long long>(64, h.lasthuge + 1);
@@ -500,7 +556,7 @@ struct Run {
                 if ((rc = enqueue_batch(batch, S, slot ^ 1))) return rc;
                 GC_HIP(hipEventSynchronize(g->evsnap[slot]));
                 const DevCtl& sn = g->hsnap[slot];
-                if (sn.halt != GC_RUN) break;
+                if (sn.halt != GC_RUN || sn.loop_err >= 2) break;
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
                 S = pick_sweeps(sn);
                 resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
@@ -509,6 +565,7 @@ struct Run {
                 slot ^= 1;
             }
             if ((rc = sync_ctl())) return rc;
+            if (h.loop_err >= 2) break;  // reported below
             proposed = h.proposed != 0;
             if (h.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
             int halt = h.halt;
@@ -549,6 +606,12 @@ struct Run {
             gc_set_error("unexpected device halt code %d", halt);
             return GC_EHIP;
         }
+        if (h.loop_err == 2) { gc_set_error("k_sweep_async: undecided list count out of range"); return GC_EHIP; }
+        if (h.loop_err == 3) {
+            gc_set_error("GC_CHECKS: out-of-range value code %lld (%lld, %lld, %lld) in round %lld", h.dbg[0], h.dbg[1],
+                         h.dbg[2], h.dbg[3], h.round);
+            return GC_EHIP;
+        }
         if (h.loop_err) { gc_set_error("k_sweep_loop: a grid barrier wait gave up"); return GC_EHIP; }
         kt.begin(GC_K_OTHER);
         gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
@@ -568,6 +631,7 @@ struct Run {
             st->rounds = (long long)recs.size();
             st->max_color = h.maxcolor;
             st->jp_sweeps = h.sweep_total;
+            st->async_aborts = (int64_t)h.async_aborts;
             st->fail_round = h.halt == GC_H_FAILED ? h.fail_round : -1;
             st->fail_count = h.halt == GC_H_FAILED ? h.fail_count : 0;
             for (const RoundRec& r : recs) st->reseeds += r.seeds;
@@ -637,6 +701,7 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
         run.d.hplc = g->hplc;
     }
     run.init_loop();
+    run.init_async();
     {
         const char* f = getenv("GC_FUSE");
         run.fuse_ok = !run.need_pblock() && run.d.hub_w == 0 && !(f && atoi(f) == 0);

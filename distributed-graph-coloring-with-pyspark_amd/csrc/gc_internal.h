@@ -51,6 +51,9 @@ typedef unsigned long long ull;
 #define GC_LOOP_MAX 65536 // ... and over at most this many light vertices in k_sweep_loop
 #define GC_LOOP_HMAX 16384 //   (hubs)
 #define GC_TAIL_HMAX 4    // ... and at most this many heavy ones
+#ifndef GC_CHECKS
+#define GC_CHECKS 0  // debug builds (tools/build_variant.sh NAME -DGC_CHECKS=1): range checks in k_commit
+#endif
 #ifndef GC_SWEEP_STATS
 #define GC_SWEEP_STATS 0  // sumdeg / nvert counters of the JP sweeps (no §8d credit, diagnostics only):
                           // their end-of-kernel reduction cost R-MAT-24 236 -> 228 ms
@@ -164,6 +167,11 @@ struct DevCtl {
     int pad3;
     long long acc_last;     // shards: winners of the last finished round (k_shard_reset keeps them for the seam header)
     long long acc_round;    // shards: round + 1 whose reset took acc_last (a repeated propose seam keeps it)
+    ull async_done[2];      // k_sweep_async: light vertices decided by this launch (slot = launch parity; the
+                            //   launch zeroes the other slot for the next one)
+    ull async_aborts;       // k_sweep_async launches that gave up at their time budget (stats)
+    int async_abort[2];     // k_sweep_async: some wave hit the budget (slot = launch parity)
+    long long dbg[4];       // GC_CHECKS builds: the first out-of-range value a checked kernel met (code, a, b, c)
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
 };

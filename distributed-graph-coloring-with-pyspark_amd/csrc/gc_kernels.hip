@@ -1290,9 +1290,357 @@ __global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, i
 }
 
 // ------------------------------------------------------------------------------------
+// Asynchronous Jones-Plassmann (round 3): the rest of a round's JP chain after the first
+// sweep (k_resolve) in ONE launch, with no grid barrier and no further host sweeps.
+// Round 2 ran it as ~7 full-grid k_sweep launches plus the one-workgroup tail per round
+// on R-MAT-24: a dependent chain of launches over a few thousand vertices each, ~110 us
+// per round in launch floors.  Here every wave of a resident grid owns a
+// static slice of the undecided lights and re-evaluates its pending ones from their
+// cursors (lcur) pass after pass until they decide; then the wave's slice of the hubs
+// (after EVERY light of the round has decided: the hub JP of gc_hubs.hip) likewise.
+// No wave ever waits holding work another wave needs (it re-checks its own vertices), so
+// the only dependence is JP's own: the lowest-rank undecided vertex of a candidate class
+// can always decide, and states only move UND -> IN / OUT.
+//   Visibility.  States another wave may read are stored agent-scope (sc1: written
+// through, past this XCD's L2) and every load of them is an agent-scope load (sc1: past
+// L1).  A stale read can only show UND -- the byte's candidate is fixed for the round and
+// its state is final once set -- so staleness delays a decision, never changes it: the
+// result is the same LFMIS as the sweeps'.  The hubs' wait for the lights is a counter:
+// a wave publishes its decided lights with one atomic after `s_waitcnt vmcnt(0)` (its
+// state and kill-flag stores have landed), and a hub wave polls the counter, then reads
+// the kill flags with agent-scope loads.
+//   Time budget.  A wave that finds the budget spent (wall clock, or another wave's
+// flag) appends its pending vertices to the next undecided lists and leaves; the commit
+// then sees them and the host runs ordinary sweeps (GC_H_SWEEPS), so a launch that was
+// not fully resident, or a visibility stall, costs time and never a hang or a wrong
+// colouring.  gc_stats.async_aborts counts such launches.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned gc_ald8(const unsigned char* p) {
+    return (unsigned)__hip_atomic_load(const_cast<unsigned char*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned gc_ald32(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gc_ast8(unsigned char* p, unsigned v) {
+    __hip_atomic_store(p, (unsigned char)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gc_ast32(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct GcAsyncLds {  // one wave's rows
+    unsigned flag[GC_WAVE];
+    int first[GC_WAVE];
+    long long start[GC_WAVE];
+    unsigned c6[GC_WAVE];
+    int cv[GC_WAVE];
+};
+
+// One pass of a wave over its pending lights lst[0, np) (edge-balanced wave chunks, as
+// gc_jp_sweep); the still-undecided ones are compacted to the front of lst (a chunk is
+// read into registers before any of it is rewritten, and survivors only move down).
+// Returns their number; `decided` counts the rest.
+__device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull& decided) {
+    const int lane = gc_lane();
+    const unsigned char* k8 = g.k8;
+    int nw = 0;
+    for (int c0 = 0; c0 < np; c0 += GC_WAVE) {
+        const int idx = c0 + lane;
+        int v = idx < np ? lst[idx] : -1;
+        if (v >= g.n) v = -1;  // never expected (a list entry out of range): skipped, not read through
+        const int lc = v >= 0 ? g.lcur[v] : 0;
+        const int nl = v >= 0 ? g.nlow[v] : 0;
+        const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0xFFu;  // own byte: only this wave changes it
+        const long long rs = v >= 0 ? g.rp[v] : 0;
+        const int dl = v >= 0 ? nl - lc : 0;
+        const unsigned cv6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        s.flag[lane] = 0;
+        s.first[lane] = 0x7FFFFFFF;
+        s.start[lane] = rs + lc;
+        s.c6[lane] = cv6;
+        s.cv[lane] = (v >= 0 && cv6 == GC_K8_BIG) ? g.cand[v] : (int)cv6;
+        const int incl = gc_wave_incl_scan(dl);
+        const int excl = incl - dl;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        gc_chunk_edges_at(
+            g.col, s.start, excl, total, [&](int u) { return gc_ald8(k8 + u); },
+            [&](int o, int u, unsigned ku, int slot) {
+                const unsigned f = gc_jp_flag(g, u, ku, s.c6[o], s.cv[o]);
+                if (f) atomicOr(&s.flag[o], f);
+                if (f == 2u) atomicMin(&s.first[o], slot);
+            });
+        gc_wave_sync();
+        unsigned nst = GC_JP_UND;
+        bool pend = false;
+        if (v >= 0) {
+            const unsigned f = s.flag[lane];
+            if (f & 1u) nst = GC_JP_OUT;
+            else if (f & 2u) pend = true;
+            else nst = GC_JP_IN;
+            if (pend) g.lcur[v] = lc + s.first[lane];
+            else gc_ast8(g.k8 + v, (kv & ~3u) | nst);
+        }
+        const ull pm = __ballot(pend);
+        if (pend) lst[nw + __popcll(pm & gc_lanemask_lt())] = v;
+        nw += __popcll(pm);
+        decided += (ull)__popcll(__ballot(v >= 0 && !pend));
+        if (g.hub_w) {  // a light winner flags the hubs listing it that propose its colour
+            int dh = 0;
+            long long hs = 0;
+            if (nst == GC_JP_IN) {
+                hs = g.hin_rp[v];
+                dh = (int)(g.hin_rp[v + 1] - hs);
+            }
+            gc_wave_sync();
+            s.start[lane] = hs;
+            const int hincl = gc_wave_incl_scan(dh);
+            const int hexcl = hincl - dh;
+            const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
+            gc_wave_sync();
+            gc_chunk_edges(
+                g.hin_col, s.start, hexcl, htotal, [&](int hx) { return g.hk[hx]; },  // candidate field: fixed
+                [&](int o, int hx, unsigned kh) {
+                    if ((kh >> 2) != (unsigned)s.cv[o]) return;
+                    if (!gc_ald32(g.hkill + hx)) gc_ast32(g.hkill + hx, 1u);
+                });
+        }
+        gc_wave_sync();
+    }
+    return nw;
+}
+
+// One pass of a wave over its pending hubs hl[0, nh), GC_HUB_NG at a time (a 16-lane
+// group each): the resumable scan of gc_hub_scan_groups, with agent-scope loads of the
+// hub mirror and the kill flags and agent-scope stores of the decisions.  Pending hubs
+// are compacted to the front of hl; returns their number.
+__device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
+    constexpr int GS = GC_WAVE / GC_HUB_NG;
+    const int lane = gc_lane();
+    const int grp = lane / GS, li = lane % GS;
+    const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
+    int nw = 0;
+    for (int j0 = 0; j0 < nh; j0 += GC_HUB_NG) {
+        const int j = j0 + grp;
+        const int v = j < nh ? hl[j] : -1;
+        const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte
+        const int cv = v >= 0 ? (gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv)) : 0;
+        const int x = v >= 0 ? g.hid[v] : -1;  // every heavy proposer is a hub while the hub JP is on
+        const bool kill = x >= 0 && gc_ald32(g.hkill + x) != 0u;
+        long long base = 0;
+        int full = 0, cursor = 0, hc0 = 1, hstart = 0;
+        if (x >= 0) {
+            base = g.hlow_rp[x];
+            full = (int)(g.hlow_rp[x + 1] - base);
+            cursor = g.hpc[x];
+            hc0 = g.hcur[x];
+            hstart = g.hlen[x];
+        }
+        const bool act = x >= 0 && !kill;  // group-uniform
+        const bool first = hc0 == 0;
+        int pos = first ? hstart : cursor;
+        bool out = false, prefix = act && first;
+        int block = -1, nstart = full;
+        const int* __restrict__ row = g.hlow_col + base;
+        for (;;) {
+            const bool run = act && !out && block < 0 && pos < full;
+            if (!__ballot(run)) break;
+            int u[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                const int e = pos + k * GS + li;
+                u[k] = (run && e < full) ? row[e] : -1;
+            }
+            unsigned ku[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) ku[k] = u[k] >= 0 ? gc_ald32(g.hk + u[k]) : GC_HK_COLOURED;
+            unsigned fl[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) fl[k] = ku[k] != GC_HK_COLOURED ? gc_jp_flag_h(g, u[k], ku[k], 0u, cv) : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                if (__ballot(fl[k] == 1u) & gmask) out = true;
+                const ull mb = __ballot(fl[k] == 2u) & gmask;
+                if (mb && block < 0) block = pos + k * GS + __builtin_ctzll(mb >> (grp * GS));
+                const ull ml = __ballot(u[k] >= 0 && ku[k] != GC_HK_COLOURED) & gmask;
+                if (prefix && ml) {  // first non-coloured entry: the end of the coloured prefix
+                    nstart = pos + k * GS + __builtin_ctzll(ml >> (grp * GS));
+                    prefix = false;
+                }
+            }
+            if (run) pos += GC_HUB_UNR * GS;
+        }
+        unsigned f = kill ? 1u : 0u;
+        if (act) f = out ? 1u : (block >= 0 ? 2u : 0u);
+        const bool lead = li == 0 && x >= 0;
+        if (lead && act) {
+            if (first) {
+                g.hcur[x] = 1;
+                if (nstart > hstart) g.hlen[x] = nstart;
+            }
+            if (!out && block >= 0) g.hpc[x] = block;
+        }
+        if (lead && f != 2u) {
+            const unsigned st = (f & 1u) ? GC_JP_OUT : GC_JP_IN;
+            gc_ast8(g.k8 + v, (kv & ~3u) | st);
+            gc_ast32(g.hk + x, gc_hk((unsigned)cv, st));
+        }
+        const bool pend = lead && f == 2u;
+        const ull pm = __ballot(pend);
+        if (pend) hl[nw + __popcll(pm & gc_lanemask_lt())] = v;
+        nw += __popcll(pm);
+    }
+    return nw;
+}
+
+// the launch's budget is spent, or another wave found it so (wave-uniform)
+__device__ __forceinline__ bool gc_async_stop(DevCtl* c, int par, ull t0, long long budget) {
+    int stop = 0;
+    if (gc_lane() == 0) {
+        stop = __hip_atomic_load(&c->async_abort[par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!stop && (long long)(wall_clock64() - t0) > budget) {
+            stop = 1;
+            if (atomicCAS(&c->async_abort[par], 0, 1) == 0) atomicAdd(&c->async_aborts, 1ull);
+        }
+    }
+    return __shfl(stop, 0, GC_WAVE) != 0;
+}
+
+// pending entries src[0, cnt) of a wave that gave up -> the next undecided list
+__device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out, ull* out_cnt) {
+    if (cnt <= 0) return;
+    ull base = 0;
+    if (gc_lane() == 0) base = atomicAdd(out_cnt, (ull)cnt);
+    base = __shfl(base, 0, GC_WAVE);
+    for (int i = gc_lane(); i < cnt; i += GC_WAVE) out[base + i] = src[i];
+}
+
+// The launch after sweep S (k_resolve = 0, or the last host sweep): reads slot S % 3,
+// spills to slot (S + 1) % 3 (cleared by sweep S), clears slot (S + 2) % 3 and sets
+// tail_last = S + 1, the slot the commit checks -- exactly what a tail that ran one more
+// sweep leaves.  `par` alternates per launch (the counters of the next launch are zeroed
+// here); `budget` is in wall-clock ticks.
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget) {
+    DevCtl* c = g.ctl;
+    if (c->halt) return;
+    __shared__ GcAsyncLds s_w[GC_WAVES_PER_BLOCK];
+    const int w = threadIdx.x / GC_WAVE;
+    const long long j = S;
+    const int in = (int)(j % 3), out = (int)((j + 1) % 3), z = (int)((j + 2) % 3);
+    const long long cl = (long long)c->und_cnt[in];
+    // hubs already started by an earlier sweep of the round: their undecided list; else every
+    // hub proposer, once the lights have converged.  (hub_start moves during the launch only
+    // from "not started" to S + 1 > S: every reader takes the same branch.)
+    const bool started = g.hub_w && __hip_atomic_load(&c->hub_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j;
+    const int* hsrc = started ? L.undH[in] : L.heavy;
+    const long long ch = g.hub_w ? (long long)(started ? c->undh_cnt[in] : c->heavy_cnt) : 0ll;
+    if (cl > g.n || ch > g.n) {  // never expected: report (the host turns it into an error), touch nothing
+        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&c->loop_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->und_cnt[z] = 0;
+        c->undh_cnt[z] = 0;
+        c->tail_last = j + 1;
+        if (cl + ch > 0) c->sweeps += 1;
+        c->async_done[par ^ 1] = 0;
+        c->async_abort[par ^ 1] = 0;
+        if (!started && ch > 0 && cl == 0) gc_st(&c->hub_start, j + 1);
+    }
+    const ull t0 = wall_clock64();
+    const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
+    const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+    bool stop = false;
+    // lights: the wave's static slice of the list, compacted in place pass after pass
+    {
+        const long long la = cl * wid / W, lb = cl * (wid + 1) / W;
+        int np = (int)(lb - la);
+        int* lst = L.undL[in] + la;
+        ull decided = 0;
+        int idle = 0;
+        while (np > 0) {
+            const int before = np;
+            np = gc_async_light_pass(g, lst, np, s_w[w], decided);
+            if (np == 0) break;
+            if ((stop = gc_async_stop(c, par, t0, budget))) break;
+            if (np == before) {
+                if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+            } else {
+                idle = 0;
+            }
+        }
+        if (stop) gc_async_spill(lst, np, L.undL[out], &c->und_cnt[out]);
+        if (decided) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its state and kill-flag stores have landed
+            if (gc_lane() == 0) {
+                const ull old = atomicAdd(&c->async_done[par], decided);
+                if (old + decided == (ull)cl && ch > 0 && !started) gc_st(&c->hub_start, j + 1);
+            }
+        }
+    }
+    if (ch == 0) return;
+    // hubs: the wave's slice (GC_HUB_NG at least), copied to slot z (the source lists stay
+    // intact: the commit walks L.heavy) and compacted there
+    const long long per = std::max<long long>(GC_HUB_NG, (ch + W - 1) / W);
+    const long long ha = wid * per;
+    if (ha >= ch) return;
+    const int nh0 = (int)(std::min(ch, ha + per) - ha);
+    const int* src = hsrc + ha;
+    if (!stop && cl > 0) {  // wait for every light of the round
+        int st = 0;
+        if (gc_lane() == 0) {
+            while (__hip_atomic_load(&c->async_done[par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (ull)cl) {
+                st = __hip_atomic_load(&c->async_abort[par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!st && (long long)(wall_clock64() - t0) > budget) {
+                    st = 1;
+                    if (atomicCAS(&c->async_abort[par], 0, 1) == 0) atomicAdd(&c->async_aborts, 1ull);
+                }
+                if (st) break;
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+        stop = __shfl(st, 0, GC_WAVE) != 0;
+    }
+    if (stop) {
+        // hubs unevaluated: always listed.  The lights may still converge after this wave
+        // gave up (the last light wave publishing late), and then hub_start = S + 1 and every
+        // undecided hub must be on the list; if they never converge, the host's sweeps start
+        // the hubs from L.heavy themselves and ignore this list (gc_hub_gate)
+        gc_async_spill(src, nh0, L.undH[out], &c->undh_cnt[out]);
+        return;
+    }
+    int* hl = L.undH[z] + ha;
+    for (int i = gc_lane(); i < nh0; i += GC_WAVE) hl[i] = src[i];
+    gc_wave_sync();
+    int nh = nh0, idle = 0;
+    while (nh > 0) {
+        const int before = nh;
+        nh = gc_async_hub_pass(g, hl, nh);
+        if (nh == 0) break;
+        if ((stop = gc_async_stop(c, par, t0, budget))) break;
+        if (nh == before) {
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+        } else {
+            idle = 0;
+        }
+    }
+    if (stop) gc_async_spill(hl, nh, L.undH[out], &c->undh_cnt[out]);
+}
+
+// ------------------------------------------------------------------------------------
 // commit (color_node + join, coloring.py:37-41, 114-127) fused with the frontier push,
 // and the end-of-round bookkeeping (last workgroup).
 // ------------------------------------------------------------------------------------
+
+// GC_CHECKS: record the first out-of-range value (code, a, b, c) and report it (loop_err 3)
+__device__ __forceinline__ void gc_dbg(DevCtl* c, long long code, long long a, long long b, long long cc) {
+    if (atomicCAS(reinterpret_cast<ull*>(&c->dbg[0]), 0ull, (ull)code) == 0ull) {
+        c->dbg[1] = a;
+        c->dbg[2] = b;
+        c->dbg[3] = cc;
+        __hip_atomic_store(&c->loop_err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 __device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
     const unsigned bit = 1u << (x & 31);
@@ -1512,7 +1860,13 @@ __device__ __forceinline__ void gc_fused_propose(GDev& g, const int* buf, int cn
     const int lane = gc_lane();
     for (int b = 0; b < cnt; b += GC_WAVE) {  // cnt is wave-uniform
         const int i = b + lane;
-        const int v = i < cnt ? buf[i] : -1;
+        int v = i < cnt ? buf[i] : -1;
+#if GC_CHECKS
+        if (v >= g.n || v < -1) {
+            gc_dbg(g.ctl, 40, v, i, cnt);
+            v = -1;
+        }
+#endif
         const int d = v >= 0 ? g.deg[v] : 0;
         s_mask[lane] = 0;
         s_start[lane] = v >= 0 ? g.rp[v] : 0;
@@ -1599,6 +1953,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     GcStage st{s_stage[w], 0};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
+#if GC_CHECKS
+    if (cnt > g.n || hcnt > g.n || (long long)(*next_cnt & ((1ull << GC_TICKET_SHIFT) - 1)) > g.n) {
+        if (threadIdx.x == 0) gc_dbg(c, 10 + mode, cnt, hcnt, (long long)*next_cnt);
+        return;
+    }
+#endif
     // fused: the next round's proposals of the staged vertices (before every flush)
     const long long kbound = c->kbound;
     long long pmax = -1;
@@ -1608,6 +1968,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                                    psum, pnv);
     };
     auto push = [&](bool pred, int val) {
+#if GC_CHECKS
+        if (pred && (val < 0 || val >= g.n)) {
+            gc_dbg(c, 50, val, st.cnt, (long long)*next_cnt);
+            pred = false;
+        }
+#endif
         if (FUSE) {
             const int np = __popcll(__ballot(pred));
             if (np && st.cnt + np > GC_STAGE_CAP) {
@@ -1707,7 +2073,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long idx = ch * vpw + lane;
-        const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+        int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
+#if GC_CHECKS
+        if (v >= g.n || v < -1) {
+            gc_dbg(c, 20, v, idx, cnt);
+            v = -1;
+        }
+#endif
         // the vertex's words are loaded together (its in-row bounds before knowing it won:
         // one memory trip instead of two); fused: no heavy vertex, so no degree needed
         const int d = (v >= 0 && !FUSE) ? g.deg[v] : 0;
@@ -1756,6 +2128,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 const int eo = __shfl(excl, o, GC_WAVE);
                 ok[k] = e < total;
                 x[k] = ok[k] ? g.tcol[s_start[w][o] + (e - eo)] : 0;
+#if GC_CHECKS
+                if (ok[k] && (x[k] < 0 || x[k] >= g.n)) {
+                    gc_dbg(c, 30, x[k], s_start[w][o] + (e - eo), e);
+                    ok[k] = false;
+                }
+#endif
             }
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) {
@@ -2623,6 +3001,14 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
     if (g.tail_nw == 16) hipLaunchKernelGGL(k_sweep_tail<16>, dim3(1), dim3(16 * GC_WAVE), 0, s, g, L, S);
     else if (g.tail_nw == 8) hipLaunchKernelGGL(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
     else hipLaunchKernelGGL(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
+}
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
+}
+int gcl_sweep_async_blocks_per_cu() {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sweep_async, GC_BLOCK, 0) != hipSuccess) return 0;
+    return b;
 }
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);

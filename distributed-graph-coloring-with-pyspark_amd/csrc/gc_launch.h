@@ -101,6 +101,9 @@ void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // one-workgroup tail sweeps
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
+// asynchronous JP after sweep S on a resident grid (budget in wall-clock ticks; par alternates per launch)
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s);
+int gcl_sweep_async_blocks_per_cu();
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
 // tclose: the commit's last workgroup also closes the round (no k_close; ROUND mode only,

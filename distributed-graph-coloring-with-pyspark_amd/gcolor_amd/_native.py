@@ -64,7 +64,8 @@ class GcStats(ctypes.Structure):
                 ("k_launches", ctypes.c_int64 * GC_NKERNELS), ("k_ms", ctypes.c_double * GC_NKERNELS),
                 ("k_bytes", ctypes.c_double * GC_NKERNELS),
                 ("round_cap", ctypes.c_int64), ("round_U", _I64P), ("round_F", _I64P),
-                ("round_maxmex", _I64P), ("round_accepted", _I64P), ("round_seeds", _I64P)]
+                ("round_maxmex", _I64P), ("round_accepted", _I64P), ("round_seeds", _I64P),
+                ("async_aborts", ctypes.c_int64)]
 
 
 class GcolorError(RuntimeError):

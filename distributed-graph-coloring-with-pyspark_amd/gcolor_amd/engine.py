@@ -50,6 +50,7 @@ class ColorResult:
     jp_sweeps: int
     device_ms: float
     kernels: dict = field(default_factory=dict)
+    async_aborts: int = 0  # asynchronous JP launches that handed their rest to host sweeps (0 expected)
 
     @property
     def ok(self):
@@ -207,7 +208,7 @@ class DeviceGraph:
                            round_seeds=rb["seeds"][:r].copy() if want_rounds else None,
                            fail_round=st.fail_round, fail_count=st.fail_count, reseeds=st.reseeds,
                            max_color=st.max_color, jp_sweeps=st.jp_sweeps, device_ms=st.device_ms,
-                           kernels=kernels)
+                           kernels=kernels, async_aborts=int(st.async_aborts))
 
     def validate(self, colors=None):
         """validate_graph_coloring counts on the device: (#uncoloured, #conflicting listed pairs).

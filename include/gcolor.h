@@ -128,6 +128,9 @@ typedef struct gc_stats {
     int64_t* round_maxmex; /* max candidate colour proposed (-1 if none)                  */
     int64_t* round_accepted;
     int64_t* round_seeds;  /* E1 seeds planted in the round                               */
+    /* outputs (continued) */
+    int64_t async_aborts;  /* asynchronous JP launches that handed their rest to host
+                              sweeps at their time budget (diagnostic; 0 expected)        */
 } gc_stats;
 
 /* Colour the graph.  colors_out (host int32[n], may be NULL): final state, -1 =

@@ -38,20 +38,28 @@ SETTINGS = [
     {"GC_HUB_T": "0", "GC_HUB_LONG": "0", "GC_HUB_PREP": "off"},  # every row walked by its wave
     {"GC_HUB_T": "0", "GC_HUB_SCAN": "0"},                    # pending-list hub JP (gc_hub_jp_wave)
     {"GC_HUB_T": "2", "GC_HUB_SCAN": "0", "GC_HUB_LONG": "0"},
-    {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "0"},               # no hub in the one-workgroup tail sweeps
-    {"GC_HUB_T": "2", "GC_TAIL_HMAX_HUB": "128"},
-    {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "4096"},            # every hub sweep in the tail once lights converge
-    {"GC_HUB_T": "2", "GC_SWEEP_LOOP": "1"},                  # the middle of each JP chain in k_sweep_loop
-    {"GC_HUB_T": "off", "GC_SWEEP_LOOP": "1", "GC_LOOP_WG": "8"},
+    {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "0", "GC_ASYNC": "0"},  # no hub in the one-workgroup tail sweeps
+    {"GC_HUB_T": "2", "GC_TAIL_HMAX_HUB": "128", "GC_ASYNC": "0"},
+    {"GC_HUB_T": "0", "GC_TAIL_HMAX_HUB": "4096", "GC_ASYNC": "0"},  # every hub sweep in the tail once lights converge
+    {"GC_HUB_T": "2", "GC_SWEEP_LOOP": "1", "GC_ASYNC": "0"},  # the middle of each JP chain in k_sweep_loop
+    {"GC_HUB_T": "off", "GC_SWEEP_LOOP": "1", "GC_LOOP_WG": "8", "GC_ASYNC": "0"},
+    {"GC_HUB_T": "0", "GC_ASYNC_BUDGET_US": "0"},             # k_sweep_async gives up at once: spills to host sweeps
+    {"GC_HUB_T": "2", "GC_ASYNC_BUDGET_US": "0"},
+    {"GC_HUB_T": "off", "GC_ASYNC_BUDGET_US": "0"},
+    {"GC_HUB_T": "3", "GC_ASYNC_BPC": "1"},                   # one workgroup per CU
+    {"GC_HUB_T": "0", "GC_ASYNC": "0"},                       # round 2's full-grid sweeps + tail
+    {"GC_HUB_T": "off", "GC_ASYNC": "0"},
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
        "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
-       "T2loop", "offloop8"]
+       "T2loop", "offloop8", "T0async_abort", "T2async_abort", "offasync_abort", "T3async_bpc1",
+       "T0sync", "offsync"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
-    for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP", "GC_LOOP_WG"):
+    for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP",
+              "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
@@ -63,6 +71,8 @@ def _check(rp, col, symmetric=False, bounded=True):
         o = oracle.c_color(rp, col, "A")
         g = dg.color("A")
         assert_same_run(g, o)
+        if os.environ.get("GC_ASYNC_BUDGET_US") is None:  # k_sweep_async never needs its fallback
+            assert g.async_aborts == 0
         assert tuple(dg.validate()) == tuple(oracle.c_validate(rp, col, o["colors"]))
         if bounded:
             top = int(o["max_color"])

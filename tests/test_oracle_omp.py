@@ -70,8 +70,10 @@ def rmat_csr(scale, ef, seed, sym=True):
     return np.cumsum(rp), dst.astype(np.int32)
 
 
-@pytest.mark.parametrize("scale,threads", [(12, 1), (14, 4), (15, 8)])
+@pytest.mark.parametrize("scale,threads", [(12, 1), (14, 4), (15, 8), (16, 8), (18, 8)])
 def test_rmat_hubs(scale, threads):
+    """R-MAT-16/18 (hubs of 10^4 entries, 157/240 rounds): the restatement the GPU is checked
+    against at C3/C4 sizes is pinned to the single-thread oracle where real hubs exist."""
     rp, col = rmat_csr(scale, 16, seed=scale)
     assert np.diff(rp).max() > 512  # the hub path runs
     c = _same(rp, col, True, threads)

@@ -4,12 +4,14 @@
 #   bash tools/gpu_session.sh TAG STEP [STEP ...]
 # Steps:
 #   tests             pytest -m gpu (every GPU test)
-#   tests:EXPR        pytest -m gpu -k EXPR
+#   tests:EXPR        pytest -m gpu -k EXPR (~ stands for a space: not~slow)
 #   file:PATH[:EXPR]  pytest -m gpu on one test file (optionally -k EXPR)
 #   smoke             __graft_entry__.smoke()
 #   bench:WL[:ARGS]   bench.py --workload WL [ARGS, comma-separated]
 #   step:WL           tools/step_timing.py WL (phase times of the step)
 #   profile:WL[:ARGS] tools/gpu_profile.sh TAG WL [ARGS] (trace + PMC passes, summaries)
+#   py:SCRIPT[:ARGS]  python SCRIPT [ARGS, comma-separated] (a tools/ script; 600 s limit)
+#   env:NAME=VALUE    export NAME=VALUE for the steps after it (env:NAME= unsets it)
 # Output: gpurun_out/TAG/ (merged back by gpurun).
 set -uo pipefail
 TAG=$1
@@ -24,6 +26,7 @@ for st in "$@"; do
   kind=${st%%:*}
   rest=${st#*:}
   [ "$rest" = "$st" ] && rest=""
+  rest=${rest//\~/ }
   log="$O/$(printf %02d $i)_${kind}.log"
   echo "== step $i: $st" | tee -a "$O/session.log"
   case $kind in
@@ -50,6 +53,13 @@ for st in "$@"; do
     profile)
       wl=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       bash tools/gpu_profile.sh "$TAG" "$wl" ${a//,/ } > "$log" 2>&1 ;;
+    env)
+      nm=${rest%%=*}; vl=${rest#*=}
+      if [ -n "$vl" ]; then export "$nm=$vl"; else unset "$nm"; fi
+      true > "$log" ;;
+    py)
+      sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
     *)
       echo "unknown step $st" > "$log"; false ;;
   esac

@@ -65,6 +65,10 @@ def main(d, steps=None):
         out["_step"] = {"steps": 1, "bytes": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
                         "note": "FETCH_SIZE + WRITE_SIZE of every kernel, (run at 3 timed steps - run at 1) / 2: "
                                 "one step, as counted (KiB x 1024)"}
+    # the build the counters describe: bench.py uses a summary only for the same libgcolor.so
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: E402
+    out["_build"] = bench.lib_sha16()
     json.dump(out, sys.stdout, indent=1)
     print()
 
