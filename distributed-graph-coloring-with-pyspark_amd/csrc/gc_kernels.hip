@@ -1548,6 +1548,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         if (!started && ch > 0 && cl == 0) gc_st(&c->hub_start, j + 1);
     }
     const ull t0 = wall_clock64();
+    // the budget grows with the launch's lists (20 ns of wall clock per light, 80 per hub): a
+    // give-up is for stalls, not for big rounds (R-MAT-28's lists reach ~10^7)
+    budget += 2 * (cl + 4 * ch);
     const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
     const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
     bool stop = false;
