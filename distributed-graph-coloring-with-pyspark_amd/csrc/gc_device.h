@@ -128,6 +128,28 @@ __device__ __forceinline__ void gc_hub_push_wave(const GDev& g, bool win, int v,
     gc_wave_sync();
 }
 
+// agent-scope (sc1) loads and stores of state another workgroup of the same launch reads or
+// writes (the asynchronous JP, k_sweep_async; variant B's asynchronous fold): stores write
+// through past this XCD's L2, loads bypass L1
+__device__ __forceinline__ unsigned gc_ald8(const unsigned char* p) {
+    return (unsigned)__hip_atomic_load(const_cast<unsigned char*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned gc_ald32(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int gc_aldi(const int* p) {
+    return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gc_ast8(unsigned char* p, unsigned v) {
+    __hip_atomic_store(p, (unsigned char)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gc_ast32(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gc_asti(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // heavy entries the one-workgroup tail sweeps may take
 __device__ __forceinline__ long long gc_tail_hmax(const GDev& g) { return g.tail_hmax; }
 

@@ -284,11 +284,12 @@ struct Run {
     void init_async() {
         const char* e = getenv("GC_ASYNC");
         if (e && atoi(e) == 0) return;
+        const bool force = e && atoi(e) == 2;  // GC_ASYNC=2: also without hubs (staged tests, tests/test_gpu_staged.py)
         // Only with the hub JP's resumable scan (R-MAT and the like, validated at full size).
         // Graphs with no hub (uniform, meshes) keep the full-grid sweeps and the tail: a
         // 10M-vertex uniform graph with k_sweep_async on faulted in the following k_commit
         // (round 3; DESIGN §5, open), and their JP chains are short anyway (C2: 15 rounds).
-        if (!d.hub_w || !d.hub_scan || d.heavy_wg || L.delta) return;
+        if ((!d.hub_w && !force) || (d.hub_w && !d.hub_scan) || d.heavy_wg || L.delta) return;
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
             return;

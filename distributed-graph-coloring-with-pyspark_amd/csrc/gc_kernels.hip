@@ -1315,18 +1315,6 @@ __global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, i
 // not fully resident, or a visibility stall, costs time and never a hang or a wrong
 // colouring.  gc_stats.async_aborts counts such launches.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned gc_ald8(const unsigned char* p) {
-    return (unsigned)__hip_atomic_load(const_cast<unsigned char*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned gc_ald32(const unsigned* p) {
-    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gc_ast8(unsigned char* p, unsigned v) {
-    __hip_atomic_store(p, (unsigned char)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gc_ast32(unsigned* p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 struct GcAsyncLds {  // one wave's rows
     unsigned flag[GC_WAVE];

@@ -23,6 +23,8 @@ for p in (REPO, PKG_DIR):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through gpurun)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "gpu_staged: GPU test of an opt-in path not yet validated on the GPU "
+                                       "(run with -m gpu_staged; promoted to gpu once green)")
 
 
 def golden_names():

@@ -1,0 +1,90 @@
+"""Staged GPU tests (marker gpu_staged, NOT selected by -m gpu): opt-in paths written in a
+round whose GPU access had closed, to be run with `pytest -m gpu_staged` on the next box and
+promoted to `gpu` once green.
+
+* Variant B's asynchronous fold (GC_B_ASYNC=1, csrc/gc_variant_b.hip k_b_async): every
+  variant-B parity case of tests/test_gpu_variant_b.py, with the normal budget and with a zero
+  budget (every launch hands its items back to the host's passes).
+Run: GC_RUN_STAGED=1 python -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v
+* The asynchronous JP without hubs (GC_ASYNC=2): the uniform / mesh / directed cases that
+  faulted at 10M vertices in round 3, small first, then C2.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import test_gpu_variant_b as vb  # noqa: E402
+from conftest import golden_names, load_golden  # noqa: E402
+
+# selected only by `-m gpu_staged` with GC_RUN_STAGED=1 (the CPU suite's -m "not gpu" skips them)
+pytestmark = [pytest.mark.gpu_staged,
+              pytest.mark.skipif(not os.environ.get("GC_RUN_STAGED"), reason="staged: GC_RUN_STAGED=1 -m gpu_staged")]
+
+B_ENVS = [{"GC_B_ASYNC": "1"}, {"GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"}]
+B_IDS = ["basync", "basync_abort"]
+
+
+@pytest.fixture(params=B_ENVS, ids=B_IDS)
+def benv(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+@pytest.mark.parametrize("name", vb.GOLD_B[::2])
+def test_b_async_golden(benv, name):
+    vb.test_golden_graphs_variant_b(name)
+
+
+def test_b_async_pins(benv):
+    vb.test_shipped_colors_json_is_the_failed_k2_snapshot()
+    vb.test_survey_pins_seed0_10000_variant_b()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_b_async_directed(benv, seed):
+    vb.test_directed_multigraphs_with_selfloops_variant_b(seed)
+
+
+@pytest.mark.parametrize("n,d,seed", [(200_000, 16, 1), (50_000, 40, 3)])
+def test_b_async_uniform(benv, n, d, seed):
+    vb.test_uniform_graphs_variant_b(n, d, seed)
+
+
+@pytest.mark.parametrize("scale", [8, 12])
+def test_b_async_rmat(benv, scale):
+    vb.test_rmat_graphs_variant_b(scale)
+
+
+def test_b_async_heavy(benv):
+    vb.test_heavy_vertices_and_wide_mex_variant_b()
+
+
+def test_b_async_rmat24_matches_passes(monkeypatch):
+    """C3 under variant B: the asynchronous fold equals the host passes, round for round."""
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(24, 16, seed=1) as dg:
+        ref = dg.color("B")
+        monkeypatch.setenv("GC_B_ASYNC", "1")
+        g = dg.color("B")
+        assert g.async_aborts == 0
+        assert np.array_equal(g.colors, ref.colors)
+        assert list(g.round_U) == list(ref.round_U) and list(g.round_accepted) == list(ref.round_accepted)
+
+
+@pytest.mark.parametrize("n", [100_000, 1_000_000, 10_000_000])
+def test_async_jp_without_hubs_uniform(monkeypatch, n):
+    """GC_ASYNC=2 forces k_sweep_async on graphs with no hub (round 3: C2 at 10M faulted in
+    the k_commit after it); against the synchronous sweeps."""
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    rp, col = uniform_csr(n, 16, 42)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        monkeypatch.setenv("GC_ASYNC", "0")
+        ref = dg.color("A")
+        monkeypatch.setenv("GC_ASYNC", "2")
+        g = dg.color("A")
+        assert np.array_equal(g.colors, ref.colors)
+        assert list(g.round_U) == list(ref.round_U)
