@@ -281,6 +281,9 @@ struct Run {
     int async_grid = 0;
     int async_par = 0;
     long long async_budget = 0;
+    // GC_ASYNC_RESOLVE=1 (opt-in, staged): k_sweep_async also makes the round's first sweep
+    // (no k_resolve launch; one kernel boundary less per round)
+    bool async_first = false;
     void init_async() {
         const char* e = getenv("GC_ASYNC");
         if (e && atoi(e) == 0) return;
@@ -302,6 +305,7 @@ struct Run {
         const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
         async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
         async_grid = cus * bpc;
+        async_first = getenv("GC_ASYNC_RESOLVE") && atoi(getenv("GC_ASYNC_RESOLVE")) > 0;
     }
     void init_loop() {
         const char* e = getenv("GC_SWEEP_LOOP");
@@ -367,15 +371,15 @@ struct Run {
 
     // big = the host also enqueues the big-round frontier build (k_pull, k_front_*): the
     // device then decides per round (gc_big_on) whether the commit pushes or marks.
-    void launch_commit(int mode, int nsweeps, bool fuse = false) {
+    void launch_commit(int mode, int nsweeps, bool fuse = false, bool first = false) {
         const int big = mode == GC_CM_ROUND && resort_hint && !fuse;
         // no sweeps enqueued and >= 16 rounds so far all decided by their first sweep (meshes):
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
-        const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
+        const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail || first);
         if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
-            kt.begin(GC_K_SWEEP);
-            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
+            kt.begin(first ? GC_K_RESOLVE : GC_K_SWEEP);
+            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s, first ? 1 : 0);
             async_par ^= 1;
             kt.end();
         } else if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch
@@ -426,6 +430,10 @@ struct Run {
     void enqueue_round(int S) {
         const bool fuse = fuse_now();
         if (!proposed) enqueue_propose();
+        if (async_first) {  // k_sweep_async makes the first sweep too
+            launch_commit(GC_CM_ROUND, 0, fuse, true);
+            return;
+        }
         kt.begin(GC_K_RESOLVE);
         gcl_resolve(d, L, s);
         kt.end();
@@ -549,7 +557,7 @@ struct Run {
         // Pipelined: batch k+1 is enqueued before the host waits on batch k's snapshot, so
         // the device never idles on the host.  Any halt drains the stream and is handled on
         // the synchronous path below, then the pipeline restarts.
-        int batch = 1, S = 1;
+        int batch = 1, S = async_first ? 0 : 1;
         for (;;) {
             int slot = 0;
             if ((rc = enqueue_batch(batch, S, slot))) return rc;

@@ -1508,21 +1508,47 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 // tail_last = S + 1, the slot the commit checks -- exactly what a tail that ran one more
 // sweep leaves.  `par` alternates per launch (the counters of the next launch are zeroed
 // here); `budget` is in wall-clock ticks.
-__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget) {
+// first = 1 (GC_ASYNC_RESOLVE, opt-in): the launch also makes the round's first sweep in place
+// of k_resolve -- its lights are the frontier's (F[cur] minus the heavy proposers, first
+// evaluated from the start of their low rows), copied to slot 0 as the waves' lists, the
+// bounded-attempt check and the first sweep's §8d credit are k_resolve's -- and S is 0.
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget,
+                                                          int first) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
+    if (first && c->kbound >= 0 && c->failcnt > 0) {  // coloring.py:104-108 (as k_resolve)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const long long r = c->round;
+            RoundRec* rec = L.rec + (r - c->rbase);
+            rec->U = c->U;
+            rec->F = (long long)c->fcnt[c->cur];
+            rec->maxmex = c->maxmex;
+            rec->accepted = 0;
+            rec->seeds = 0;
+            rec->sweeps = 0;
+            c->fail_round = r;
+            c->fail_count = (long long)c->failcnt;
+            c->round = r + 1;
+            c->halt = GC_H_FAILED;
+        }
+        return;
+    }
     __shared__ GcAsyncLds s_w[GC_WAVES_PER_BLOCK];
     const int w = threadIdx.x / GC_WAVE;
-    const long long j = S;
+    const long long j = first ? 0 : S;
     const int in = (int)(j % 3), out = (int)((j + 1) % 3), z = (int)((j + 2) % 3);
-    const long long cl = (long long)c->und_cnt[in];
+    const int cur = c->cur;
+    // first: the slices run over the frontier (cf entries); cl = its lights (every heavy
+    // proposer of F is on L.heavy once: k_propose)
+    const long long cf = first ? (long long)c->fcnt[cur] : 0ll;
+    const long long cl = first ? cf - (long long)c->heavy_cnt : (long long)c->und_cnt[in];
     // hubs already started by an earlier sweep of the round: their undecided list; else every
     // hub proposer, once the lights have converged.  (hub_start moves during the launch only
     // from "not started" to S + 1 > S: every reader takes the same branch.)
     const bool started = g.hub_w && __hip_atomic_load(&c->hub_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j;
     const int* hsrc = started ? L.undH[in] : L.heavy;
     const long long ch = g.hub_w ? (long long)(started ? c->undh_cnt[in] : c->heavy_cnt) : 0ll;
-    if (cl > g.n || ch > g.n) {  // never expected: report (the host turns it into an error), touch nothing
+    if (cl > g.n || ch > g.n || cl < 0 || cf > g.n) {  // never expected: report (the host turns it into an error), touch nothing
         if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&c->loop_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
@@ -1530,7 +1556,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         c->und_cnt[z] = 0;
         c->undh_cnt[z] = 0;
         c->tail_last = j + 1;
-        if (cl + ch > 0) c->sweeps += 1;
+        if (first) c->sweeps = 1 + (cl + ch > 0 ? 1 : 0);
+        else if (cl + ch > 0) c->sweeps += 1;
         c->async_done[par ^ 1] = 0;
         c->async_abort[par ^ 1] = 0;
         if (!started && ch > 0 && cl == 0) gc_st(&c->hub_start, j + 1);
@@ -1544,9 +1571,38 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     bool stop = false;
     // lights: the wave's static slice of the list, compacted in place pass after pass
     {
-        const long long la = cl * wid / W, lb = cl * (wid + 1) / W;
+        const long long span = first ? cf : cl;
+        const long long la = span * wid / W, lb = span * (wid + 1) / W;
         int np = (int)(lb - la);
         int* lst = L.undL[in] + la;
+        if (first) {  // the slice's lights, compacted into slot 0, each from the start of its low row
+            const int* fl = L.F[cur] + la;
+            const int lane = gc_lane();
+            int nl = 0;
+            ull lsum = 0, lnv = 0;
+            for (int i0 = 0; i0 < np; i0 += GC_WAVE) {
+                const int v = i0 + lane < np ? fl[i0 + lane] : -1;
+                const int d = v >= 0 ? g.deg[v] : 0;
+                const bool light = v >= 0 && d <= g.heavy_t;
+                const ull m = __ballot(light);
+                if (light) {
+                    lst[nl + __popcll(m & gc_lanemask_lt())] = v;
+                    g.lcur[v] = 0;
+                    lsum += (ull)d;  // the first sweep's §8d credit (k_resolve's)
+                    lnv++;
+                }
+                nl += __popcll(m);
+            }
+            np = nl;
+            lsum = gc_wave_sum(lsum);  // per wave into the stats slots (gc_stat_add's GC_STAT_WAVE form)
+            lnv = gc_wave_sum(lnv);
+            if (lane == 0) {
+                ull* slot = g.bstat + (wid % GC_STAT_SLOTS) * 16;
+                if (lsum) atomicAdd(slot + GC_K_RESOLVE, lsum);
+                if (lnv) atomicAdd(slot + 8 + GC_K_RESOLVE, lnv);
+            }
+            gc_wave_sync();
+        }
         ull decided = 0;
         int idle = 0;
         while (np > 0) {
@@ -2993,8 +3049,9 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
     else if (g.tail_nw == 8) hipLaunchKernelGGL(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
     else hipLaunchKernelGGL(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
 }
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
+                     int first) {
+    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget, first);
 }
 int gcl_sweep_async_blocks_per_cu() {
     int b = 0;

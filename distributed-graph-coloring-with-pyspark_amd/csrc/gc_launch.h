@@ -102,7 +102,9 @@ void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // one-workgroup tail sweeps
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 // asynchronous JP after sweep S on a resident grid (budget in wall-clock ticks; par alternates per launch)
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s);
+// first = 1: the launch also makes the round's first sweep (no k_resolve before it; S = 0)
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
+                     int first = 0);
 int gcl_sweep_async_blocks_per_cu();
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round

@@ -88,3 +88,49 @@ def test_async_jp_without_hubs_uniform(monkeypatch, n):
         g = dg.color("A")
         assert np.array_equal(g.colors, ref.colors)
         assert list(g.round_U) == list(ref.round_U)
+
+
+# --- the asynchronous first sweep (GC_ASYNC_RESOLVE=1: no k_resolve launch) ---------------
+import test_gpu_hubs as hubs  # noqa: E402
+
+R_ENVS = [{"GC_ASYNC_RESOLVE": "1"}, {"GC_ASYNC_RESOLVE": "1", "GC_ASYNC_BUDGET_US": "0"},
+          {"GC_ASYNC_RESOLVE": "1", "GC_HUB_T": "2"}, {"GC_ASYNC_RESOLVE": "1", "GC_HUB_T": "0", "GC_ASYNC_BUDGET_US": "0"}]
+R_IDS = ["ares", "ares_abort", "ares_T2", "ares_T0_abort"]
+
+
+@pytest.fixture(params=R_ENVS, ids=R_IDS)
+def renv(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_async_resolve_generator_graphs(renv):
+    hubs.test_reference_generator_graphs(renv)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_async_resolve_directed(renv, seed):
+    hubs.test_directed_multigraphs(renv, seed)
+
+
+@pytest.mark.parametrize("scale", [9, 12])
+def test_async_resolve_rmat(renv, scale):
+    hubs.test_rmat(renv, scale)
+
+
+def test_async_resolve_clique_star(renv):
+    hubs.test_clique_and_star(renv)
+
+
+def test_async_resolve_rmat24_matches(monkeypatch):
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(24, 16, seed=1) as dg:
+        ref = dg.color("A")
+        monkeypatch.setenv("GC_ASYNC_RESOLVE", "1")
+        g = dg.color("A")
+        assert g.async_aborts == 0
+        assert np.array_equal(g.colors, ref.colors)
+        for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
+            assert list(getattr(g, k)) == list(getattr(ref, k)), k
+        assert g.kernels["resolve"]["bytes"] == ref.kernels["resolve"]["bytes"]  # the first sweep's §8d credit
