@@ -177,11 +177,34 @@ def cpu_baseline(w, host_csr, colors_gpu):
     dt = time.perf_counter() - t0
     m = len(col) / 2
     same = colors_gpu is not None and np.array_equal(o["colors"], colors_gpu)
-    return {"value": m / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+    try:
+        py = python_restatement()
+    except Exception as e:  # context only: never lose the line over it
+        py = {"error": repr(e)[:200]}
+    return {"value": m / dt, "unit": "edges/s", "cores": threads, "kind": "port", "python_restatement": py,
             "sample": f"oracle/gcolor_omp.c (OpenMP, {threads} threads) colouring the full graph of {w['desc']} "
                       f"in {dt:.1f} s on {platform.processor() or platform.machine()} ({os.cpu_count()} CPUs "
                       f"visible); colours identical to the GPU's: {same}",
             "colors": int(o["max_color"]) + 1, "seconds": dt, "identical": same}
+
+
+def python_restatement(scale=14):
+    """Context for the CPU baseline: the oracle's pure-Python restatement (oracle.py py_color:
+    the reference's per-vertex lambdas as Python loops, one thread, without Spark's overhead)
+    on a bounded sample -- the same R-MAT generator at scale 14 -- checked against the C oracle."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(scale, 16, seed=1) as dg:
+        rp, col = dg.export()
+    adj = [col[rp[i]:rp[i + 1]].tolist() for i in range(len(rp) - 1)]
+    t0 = time.perf_counter()
+    o = oracle.py_color(adj, "A")
+    dt = time.perf_counter() - t0
+    same = np.array_equal(np.asarray(o["colors"], dtype=np.int32), oracle.c_color(rp, col, "A")["colors"])
+    return {"value": len(col) / 2 / dt, "unit": "edges/s", "cores": 1, "seconds": round(dt, 3),
+            "sample": f"R-MAT scale {scale} (edge factor 16, seed 1; {len(col) // 2} edges), oracle.py py_color, "
+                      f"colours identical to the C oracle: {same}"}
 
 
 class StepRunner:
