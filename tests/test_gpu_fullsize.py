@@ -9,9 +9,8 @@
 * C4 on one GPU (mesh 512^3): valid, 2 colours (the wavefront 2-colours the bipartite
   mesh), 1531 rounds (3 * (512 - 2) + 1, the last one empty), bit-exact
   against the multi-core restatement.
-* north star (R-MAT scale 26): valid, rounds / colours pinned, bit-exact against the
-  multi-core restatement (every per-round record).
-* C4 as two shards (ThreadTransport on one GPU) against the engine, round for round.
+* north star (R-MAT scale 26): valid, rounds / colours pinned (bit-exact against the
+  multi-core restatement, and C4 as two shards, in tests/test_xl_gpu.py).
 * C5's graph on one GPU (R-MAT scale 28, past 2^32 adjacency entries): valid, pinned; and
   R-MAT-27 (the 8-GPU weak-scaling graph) as one shard against the engine.
 """
@@ -94,36 +93,12 @@ def test_c4_mesh512():
     _same_records(g, o)
 
 
-def test_north_star_rmat26_against_multicore_restatement():
-    """The north-star graph: valid, rounds / colours pinned, and bit-exact against
-    oracle/gcolor_omp.c -- colours and every per-round record (the restatement is pinned to
-    the single-thread oracle on R-MAT graphs with hubs, tests/test_oracle_omp.py)."""
+def test_north_star_rmat26_valid():
     from gcolor_amd.engine import DeviceGraph
     with DeviceGraph.rmat(26, 16, seed=1) as dg:
-        g = dg.color("A")
+        g = dg.color("A", want_rounds=False, want_colors=False)
         assert dg.validate() == (0, 0)
         assert (g.rounds, g.max_color + 1) == (1355, 1350)
-        assert g.async_aborts == 0
-        rp, col = dg.export()
-    o = oracle.omp_color(rp, col, symmetric=True, threads=_threads())
-    del rp, col
-    _same_records(g, o)
-    assert np.array_equal(g.colored_round, o["colored_round"])
-
-
-def test_c4_mesh512_two_shards_match_engine():
-    """C4 as two shards (ThreadTransport, one GPU): byte for byte the engine's colouring and
-    round records (LFMIS under the global rank is partition-invariant)."""
-    from gcolor_amd import shard as sh
-    from gcolor_amd.engine import DeviceGraph
-    with DeviceGraph.mesh(512, 512, 512) as dg:
-        one = dg.color("A")
-        res = sh.color_threads(dg, 2, track_rounds=True)
-        for r in res:
-            assert np.array_equal(r.colors, one.colors)
-            assert np.array_equal(r.colored_round, one.colored_round)
-            for k in KEYS:
-                assert list(getattr(r, k)) == list(getattr(one, k)), k
 
 
 def test_c5_rmat28_on_one_gpu_valid():
