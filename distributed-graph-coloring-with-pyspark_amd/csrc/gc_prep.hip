@@ -30,13 +30,19 @@
 #include "gc_device.h"
 #include "gc_engine.h"
 
-#define GC_TW 2048   // merge-path keys (rows + entries) per tile
-#define GC_TH 2048   // rows longer than this are split into segments
-#define GC_SEG 4096  // entries per segment
-#define GC_PER 16    // entries per thread: 256 x 16 = GC_TW + GC_TH = GC_SEG
+// GC_TILE_PER (build knob, default 16): entries per thread.  The tile's LDS (~57 KB at 16)
+// allows two workgroups per CU; 8 halves it (A/B: tools/build_variant.sh tile8 -DGC_TILE_PER=8)
+#ifndef GC_TILE_PER
+#define GC_TILE_PER 16
+#endif
+#define GC_PER GC_TILE_PER               // entries per thread: 256 x GC_PER = GC_TW + GC_TH = GC_SEG
+#define GC_TW (GC_BLOCK / 2 * GC_PER)    // merge-path keys (rows + entries) per tile (2048 at 16)
+#define GC_TH (GC_BLOCK / 2 * GC_PER)    // rows longer than this are split into segments
+#define GC_SEG (GC_BLOCK * GC_PER)       // entries per segment (4096 at 16)
 #define GC_PREP_GRID 4096
 
 static_assert(GC_BLOCK * GC_PER == GC_TW + GC_TH && GC_BLOCK * GC_PER == GC_SEG, "tile geometry");
+static_assert(GC_PER <= 16, "2-bit classes of a thread's entries are packed in one 32-bit word");
 
 namespace {
 
