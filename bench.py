@@ -382,6 +382,28 @@ def class_table(kern, pmc):
     return out
 
 
+def scaled_workload(w, world, scaling):
+    """The workload of an N-GPU run: --scaling weak grows it with N (uniform n x N, R-MAT scale
+    + log2 N, mesh z x N), strong keeps it.  Returns (workload, description)."""
+    w = dict(w)
+    weak = scaling == "weak" and world > 1
+    if w["kind"] == "uniform":
+        if weak:
+            w["n"] *= world
+        desc = f"uniform (graph.py:30-43 process) n={w['n'] / 1e6:g}M, max-degree {w['d']}, seed {w['seed']}"
+    elif w["kind"] == "rmat":
+        if weak:
+            w["scale"] += int(round(math.log2(world)))
+        desc = f"R-MAT scale {w['scale']}, edge factor {w['ef']}, (0.57,0.19,0.19), seed {w['seed']}"
+    else:
+        x, y, z = w["dims"]
+        if weak:
+            w["dims"] = (x, y, z * world)
+        desc = f"3-D 7-point mesh {x}x{y}x{w['dims'][2]}"
+    w["desc"] = desc + (f" (= base x {world} GPUs)" if weak else "")
+    return w
+
+
 def sharded_graph(w, world, scaling):
     from gcolor_amd.engine import DeviceGraph, uniform_csr
     w = dict(w)
@@ -490,8 +512,10 @@ def main():
                     help="N > 1: weak grows the graph with N, strong keeps the workload's graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--replicas", action="store_true",
-                    help="N>1: colour N independent copies (one per GPU) instead of one sharded graph")
+    ap.add_argument("--multi", default="replicated", choices=["replicated", "sharded"],
+                    help="N>1: replicated (default) -- every rank runs the one-GPU engine on the whole graph, no "
+                         "exchange, the job's time is the slowest rank's; sharded -- one graph cut into vertex-range "
+                         "shards with round seams over RCCL (gcolor_amd.shard; slower than one GPU, DESIGN.md §7)")
     ap.add_argument("--priority-seed", type=int, default=None,
                     help="north_star mode N1: JP rounds ranked by prio_hash(seed, v) instead of (deg, pos)")
     ap.add_argument("--speculative", action="store_true",
@@ -532,14 +556,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-        if args.sharded or not args.replicas:
+        if args.sharded or args.multi == "sharded":
             return run_sharded(args, world, rank, local_rank, dist, torch)
     else:
         torch.cuda.set_device(0)
 
     from gcolor_amd import _native
     _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
-    w = WORKLOADS[args.workload]
+    w = scaled_workload(WORKLOADS[args.workload], world, args.scaling)
     V = args.variant
     # north_star N1 modes (variant A only): seeded priorities / speculative first-fit
     mode = {"priority": args.priority_seed, "speculative": args.speculative}
@@ -636,7 +660,10 @@ def main():
         "data": "synthetic",
         "config": {"workload": w["desc"], "n": info["n"], "m_undirected": m, "nnz": info["nnz"],
                    "max_degree": info["max_degree"], "variant": "A (coloring.py)" if V == "A" else
-                   "B (coloring_optimized.py)", "parallelism": "replicas" if world > 1 else "single",
+                   "B (coloring_optimized.py)",
+                   "parallelism": (f"replicated: each of the {world} ranks runs the one-GPU engine on the whole graph, "
+                                   "no exchange (the rounds are a latency chain: DESIGN.md §7); time = slowest rank")
+                                  if world > 1 else "single",
                    "rank": ("(deg, pos) (coloring.py:64)" if args.priority_seed is None
                             else f"prio_hash(seed={args.priority_seed}, v), pos"),
                    "resolution": "speculative first-fit, one-shot" if args.speculative else "Jones-Plassmann LFMIS",

@@ -1,0 +1,43 @@
+"""bench.py's host logic (no GPU): the N-GPU workload scaling, the PMC summaries' build
+identity (a summary of another libgcolor.so is never used), the roofline's capped credit."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_scaled_workload_weak_and_strong():
+    w = bench.WORKLOADS["rmat24"]
+    assert bench.scaled_workload(w, 1, "weak")["scale"] == 24
+    assert bench.scaled_workload(w, 8, "weak")["scale"] == 27
+    assert bench.scaled_workload(w, 8, "strong")["scale"] == 24
+    assert "x 8 GPUs" in bench.scaled_workload(w, 8, "weak")["desc"]
+    assert bench.scaled_workload(bench.WORKLOADS["uniform10M"], 4, "weak")["n"] == 40_000_000
+    assert bench.scaled_workload(bench.WORKLOADS["mesh512"], 2, "weak")["dims"] == (512, 512, 1024)
+    assert w["scale"] == 24  # the table is not modified
+
+
+def test_pmc_summary_of_another_build_is_stale(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    os.makedirs(tmp_path / "profiles" / "pmc")
+    p = tmp_path / "profiles" / "pmc" / "rmat24.json"
+    per = {"k_commit": {"launches": 10, "hbm_bytes_per_launch": 100.0},
+           "_step": {"steps": 1, "bytes": 8e12}}
+    monkeypatch.setattr(bench, "lib_sha16", lambda: "abc")
+    p.write_text(json.dumps(dict(per, _build="other")))
+    assert bench.pmc_class_bytes("rmat24", "A")[0] == {}
+    assert "stale" in bench.pmc_class_bytes("rmat24", "A")[1]
+    assert bench.pmc_step_frac("rmat24", "A", 1.0) is None
+    p.write_text(json.dumps(dict(per, _build="abc")))
+    cls, src = bench.pmc_class_bytes("rmat24", "A")
+    assert cls["commit"] == 100.0 and "stale" not in src
+    assert abs(bench.pmc_step_frac("rmat24", "A", 1.0)["frac"] - 1.0) < 1e-12
+
+
+def test_capped_credit():
+    kern = {"propose": {"bytes": 1e12, "ms": 10.0, "launches": 1}, "commit": {"bytes": 1e9, "ms": 10.0, "launches": 1}}
+    cap = bench.capped_alg(kern, n=0, nnz=0)
+    assert cap == 10e-3 * bench.HBM_PEAK_GBS * 1e9 + 1e9
