@@ -448,20 +448,28 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
         torch.cuda.synchronize()
         dist.barrier()
 
+    hybrid = args.multi == "hybrid"
+    switch_below = args.switch_below if args.switch_below > 0 else max(4096, dg.n // 64)
+    resume = sh.engine_resume(dg) if hybrid else None
+
+    def step(want_colors):
+        kw = dict(want_colors=want_colors, ahead=args.seam_ahead, inline_max=args.seam_inline_max)
+        if hybrid:  # sharded rounds while the frontier is large, then every rank's own engine
+            return sh.hybrid_color(ops, comm, resume, switch_below, **kw)
+        return sh.shard_color(ops, comm, **kw)
+
     for _ in range(max(args.warmup, 1)):
-        res = sh.shard_color(ops, comm, want_colors=False, ahead=args.seam_ahead,
-                             inline_max=args.seam_inline_max)
+        res = step(False)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):  # colours stay in HBM, as in the 1-GPU step
-        res = sh.shard_color(ops, comm, want_colors=False, ahead=args.seam_ahead,
-                             inline_max=args.seam_inline_max)
+        res = step(False)
     barrier()
     t = (time.perf_counter() - t0) / args.steps
     tt = torch.tensor([t], dtype=torch.float64, device="cuda")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t = float(tt.item())
-    res.colors, _ = ops.colors(False)  # outside the timed region
+    res = step(True)  # once more with the colours to host, outside the timed region
     if rank == 0:
         unc, conf = dg.validate(res.colors)
         assert unc == 0 and conf == 0, f"invalid colouring: {unc} uncoloured, {conf} conflicts"
@@ -477,7 +485,10 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
             "config": {"workload": desc, "n": dg.n, "m_undirected": m, "nnz": dg.nnz, "max_degree": dg.max_degree,
                        "variant": "A (coloring.py)",
                        "parallelism": f"{world} vertex-range shards (balanced by deg+1), round seams over "
-                                      f"{'RCCL' if comm.backend == 'nccl' else comm.backend}",
+                                      f"{'RCCL' if comm.backend == 'nccl' else comm.backend}"
+                                      + (f"; hybrid: from the first round with a frontier below {switch_below} "
+                                         f"every rank finishes on its own one-GPU engine" if hybrid else ""),
+                       "multi": "hybrid" if hybrid else "sharded", "switch_round": res.switch_round,
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
                        "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2),
@@ -512,10 +523,15 @@ def main():
                     help="N > 1: weak grows the graph with N, strong keeps the workload's graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--multi", default="replicated", choices=["replicated", "sharded"],
+    ap.add_argument("--multi", default="replicated", choices=["replicated", "sharded", "hybrid"],
                     help="N>1: replicated (default) -- every rank runs the one-GPU engine on the whole graph, no "
                          "exchange, the job's time is the slowest rank's; sharded -- one graph cut into vertex-range "
-                         "shards with round seams over RCCL (gcolor_amd.shard; slower than one GPU, DESIGN.md §7)")
+                         "shards with round seams over RCCL (gcolor_amd.shard; slower than one GPU, DESIGN.md §7); "
+                         "hybrid -- sharded rounds while the frontier is large, then every rank resumes the one-GPU "
+                         "engine from the replicated state (gcolor_amd.shard.hybrid_color)")
+    ap.add_argument("--switch-below", type=int, default=0,
+                    help="hybrid: frontier size below which the ranks switch to the one-GPU engine "
+                         "(0: max(4096, n / 64))")
     ap.add_argument("--priority-seed", type=int, default=None,
                     help="north_star mode N1: JP rounds ranked by prio_hash(seed, v) instead of (deg, pos)")
     ap.add_argument("--speculative", action="store_true",
@@ -556,7 +572,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-        if args.sharded or args.multi == "sharded":
+        if args.sharded or args.multi in ("sharded", "hybrid"):
             return run_sharded(args, world, rank, local_rank, dist, torch)
     else:
         torch.cuda.set_device(0)

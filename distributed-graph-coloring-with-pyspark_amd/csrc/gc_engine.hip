@@ -254,6 +254,14 @@ struct KTimer {
     }
 };
 
+struct ResumeArgs {
+    const int* colors;  // device int32[n], -1 uncoloured
+    const int* cround;  // device int32[n] or null
+    const int* front;   // device int32[nf]: the uncoloured vertices with a coloured listed neighbour
+    long long nf;
+    long long round0;   // rounds already run
+};
+
 struct Run {
     gc_graph* g;
     const gc_options* opt;
@@ -528,7 +536,9 @@ struct Run {
         return GC_OK;
     }
 
-    int go(int32_t* colors_out, int32_t* cround_out) {
+    // rs != null (gc_color_resume): the state at the start of round rs->round0 comes from the
+    // caller's colours and frontier instead of init + seed
+    int go(int32_t* colors_out, int32_t* cround_out, const ResumeArgs* rs = nullptr) {
         int rc;
         DevCtl& h = *g->hctl;
         memset(&h, 0, sizeof(DevCtl));
@@ -542,9 +552,22 @@ struct Run {
         h.fail_round = -1;
         h.want_cround = cround_out != nullptr;
         h.pull_off = getenv("GC_NO_PULL") ? 1 : 0;
+        if (rs) {
+            h.round = rs->round0;
+            h.rbase = rs->round0;
+            h.cur = 0;
+            h.fcnt[0] = (ull)rs->nf;
+            drained = rs->round0;
+        }
         GC_HIP(hipMemcpyAsync(g->ctl, &h, sizeof(DevCtl), hipMemcpyHostToDevice, s));
         GC_HIP(hipMemsetAsync(g->bstat, 0, sizeof(ull) * GC_STAT_SLOTS * 16, s));
         GC_HIP(hipEventRecord(g->ev0, s));
+        if (rs) {  // the caller's state (the E1 list and its count serve as the hub pushes' scratch)
+            kt.begin(GC_K_INIT);
+            gcl_resume(d, L, rs->colors, rs->cround, rs->front, rs->nf, g->ulist, &g->ctl->list_cnt, s);
+            kt.end();
+            GC_HIP(hipMemsetAsync(&g->ctl->list_cnt, 0, sizeof(ull), s));
+        } else {
         // init + seed (coloring.py:74-76)
         kt.begin(GC_K_INIT);
         gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), s);
@@ -553,6 +576,7 @@ struct Run {
         gcl_seed_prep(d, g->seeds[0], g->seeds[1], s);
         kt.end();
         launch_commit(GC_CM_INIT, 0);
+        }
         const long long max_rounds = 4ll * g->n + 16;
         // Pipelined: batch k+1 is enqueued before the host waits on batch k's snapshot, so
         // the device never idles on the host.  Any halt drains the stream and is handled on
@@ -664,8 +688,8 @@ struct Run {
 
 }  // namespace
 
-extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
-                        gc_stats* stats) {
+static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out, gc_stats* stats,
+                      const ResumeArgs* rs) {
     if (!g || !opt) { gc_set_error("gc_color: null argument"); return GC_EINVAL; }
     if (opt->variant != GC_VARIANT_A && opt->variant != GC_VARIANT_B) {
         gc_set_error("gc_color: unknown variant %d", opt->variant);
@@ -688,6 +712,10 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     }
     if (opt->variant == GC_VARIANT_B && (opt->priority != GC_PRIORITY_REF || opt->speculative)) {
         gc_set_error("gc_color: seeded priorities and the speculative mode are variant A only");
+        return GC_EINVAL;
+    }
+    if (rs && (opt->variant != GC_VARIANT_A || opt->priority != GC_PRIORITY_REF || opt->speculative)) {
+        gc_set_error("gc_color_resume: variant A with the reference rank only");
         return GC_EINVAL;
     }
     // the rows are partitioned for the rank of this colouring (re-partitioned when it changes)
@@ -717,7 +745,23 @@ extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out,
     }
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
-    return run.go(colors_out, cround_out);  // stats->rounds may exceed round_cap: the caller re-asks
+    return run.go(colors_out, cround_out, rs);  // stats->rounds may exceed round_cap: the caller re-asks
+}
+
+extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
+                        gc_stats* stats) {
+    return color_impl(g, opt, colors_out, cround_out, stats, nullptr);
+}
+
+extern "C" int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t* colors_dev, const int32_t* cround_dev,
+                               const int32_t* front_dev, int64_t nfront, int64_t round0, int32_t* colors_out,
+                               int32_t* cround_out, gc_stats* stats) {
+    if (!g || !colors_dev || (nfront > 0 && !front_dev) || nfront < 0 || nfront > g->n || round0 < 0) {
+        gc_set_error("gc_color_resume: bad argument");
+        return GC_EINVAL;
+    }
+    const ResumeArgs rs{colors_dev, cround_dev, front_dev, (long long)nfront, (long long)round0};
+    return color_impl(g, opt, colors_out, cround_out, stats, &rs);
 }
 
 extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts) {

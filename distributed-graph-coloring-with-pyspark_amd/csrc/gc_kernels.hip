@@ -2884,6 +2884,98 @@ __global__ void __launch_bounds__(GC_BLOCK) k_finalize(GDev g) {
 }
 
 // ------------------------------------------------------------------------------------
+// Resume (gc_color_resume): the engine's state at the start of round `round0` from a
+// colouring in progress -- the multi-GPU hybrid hands the replicated colours and the
+// all-gathered frontier of its sharded rounds to the one-GPU engine for the rest.  The
+// state is exactly what the engine keeps at a round start: colours (c8 / color / cround),
+// k8 cleared, the claim bitmap = coloured or in the frontier, the frontier list, the hub
+// mirror and forbidden-colour bitmaps (every coloured vertex pushes its colour into the hubs
+// that list it, as its commit did), U and the max colour.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(GC_BLOCK) k_resume_init(GDev g, const int* colors, const int* cround_in) {
+    __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+    const int lane = gc_lane();
+    ull unc = 0;
+    long long mx = -1;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v - lane < g.n; v += stride) {
+        const bool valid = v < g.n;
+        const int c = valid ? colors[v] : 0;
+        const bool coloured = valid && c >= 0;
+        if (valid) {
+            g.color[v] = coloured ? c : -1;
+            g.cround[v] = cround_in ? cround_in[v] : (coloured ? 0 : -1);
+            g.c8[v] = gc_c8_of(coloured ? (long long)c : -1ll);
+            g.k8[v] = gc_k8(GC_K8_NONE, GC_JP_UND);
+            if (g.hub_w && g.hid[v] >= 0) g.hk[g.hid[v]] = coloured ? GC_HK_COLOURED : gc_hk(GC_HK_NOCAND, GC_JP_UND);
+            g.mark[v] = 0;
+            if (coloured) mx = c > mx ? c : mx;
+            else unc++;
+        }
+        const ull m = __ballot(coloured || !valid);  // claim bitmap: coloured (frontier bits: k_resume_front)
+        if (lane == 0) {
+            const long long w = (v - lane) >> 5;
+            g.inF[w] = (unsigned)m;
+            if ((v - lane) + 32 < g.n) g.inF[w + 1] = (unsigned)(m >> 32);
+        }
+    }
+    gc_block_max(&g.ctl->maxcolor, mx, (long long*)scratch);
+    gc_block_add(&g.ctl->uncolored, unc, scratch);
+}
+
+// the frontier list F[0] and its claim bits (after k_resume_init's bitmap words)
+__global__ void __launch_bounds__(GC_BLOCK) k_resume_front(GDev g, GLists L, const int* front, long long nf) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (long long)gridDim.x * blockDim.x) {
+        const int v = front[i];
+        L.F[0][i] = v;
+        atomicOr(&g.inF[v >> 5], 1u << (v & 31));
+    }
+}
+
+// every coloured vertex's colour into the bitmaps of the hubs that list it (lists longer
+// than GC_PUSH_FLAT go to `big` for gcl_hub_push_big, as in the commits)
+__global__ void __launch_bounds__(GC_BLOCK) k_resume_hbits(GDev g, const int* colors, int* big, ull* big_cnt) {
+    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long steps = (g.n + GC_WAVE - 1) / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long v = sidx * GC_WAVE + lane;
+        const int c = v < g.n ? colors[v] : -1;
+        gc_hub_push_wave(g, c >= 0, (int)v, c, s_start[w], s_cc[w], big, big_cnt);
+    }
+}
+
+// U and the start-of-round checks (one thread): U == 0 ends the colouring, an empty frontier
+// with uncoloured vertices left asks for E1 (or stalls with E1 off), as after any round
+__global__ void k_resume_close(GDev g, GLists L) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    DevCtl* c = g.ctl;
+    const long long U = (long long)c->uncolored;
+    gc_st(&c->U, U);
+    gc_precheck(L, c, U, (long long)c->fcnt[c->cur]);
+}
+
+// a shard's own frontier (F[cur] minus the replicated hubs it lists but does not own)
+__global__ void __launch_bounds__(GC_BLOCK) k_shard_own_front(GDev g, GLists L, long long lo, long long hi, int* out,
+                                                              ull* out_cnt) {
+    DevCtl* c = g.ctl;
+    const int cur = c->cur;
+    const long long cnt = (long long)c->fcnt[cur];  // (includes the replicated hubs of other ranks)
+    const int* list = L.F[cur];
+    const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
+    const int w = threadIdx.x / GC_WAVE;
+    for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
+         sidx += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
+        const long long i = sidx * GC_WAVE + gc_lane();
+        const int v = i < cnt ? list[i] : -1;
+        gc_wave_append(v >= lo && v < hi && g.c8[v] == GC_C8_NONE, v, out, out_cnt);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // graph helpers
 // ------------------------------------------------------------------------------------
 // deg, its byte key kb = min(deg, 255) (the rank partition gathers it first: gc_prep.hip),
@@ -3037,6 +3129,23 @@ void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t
 }
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big, int fused, DevCtl* snap) {
     hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big, fused, snap);
+}
+void gcl_resume(const GDev& g, const GLists& L, const int* colors, const int* cround, const int* front, long long nf,
+                int* big, ull* big_cnt, hipStream_t s) {
+    const int grid = (int)std::max<long long>(1, std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 8192));
+    hipLaunchKernelGGL(k_resume_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, cround);
+    if (nf > 0)
+        hipLaunchKernelGGL(k_resume_front, dim3((int)std::max<long long>(1, std::min<long long>((nf + GC_BLOCK - 1) / GC_BLOCK, 8192))),
+                           dim3(GC_BLOCK), 0, s, g, L, front, nf);
+    if (g.hbits_w) {
+        hipLaunchKernelGGL(k_resume_hbits, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, big, big_cnt);
+        gcl_hub_push_big(g, big, big_cnt, s);
+    }
+    hipLaunchKernelGGL(k_resume_close, dim3(1), dim3(64), 0, s, g, L);
+}
+void gcl_shard_own_front(const GDev& g, const GLists& L, long long lo, long long hi, int* out, ull* out_cnt,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_own_front, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, out, out_cnt);
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);

@@ -132,6 +132,12 @@ void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStrea
 // replicated hubs after a slice seam: the other ranks' light winners flag their hubs
 void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
+// gc_color_resume: the round-start state from colours + frontier (big: scratch list + its count)
+void gcl_resume(const GDev& g, const GLists& L, const int* colors, const int* cround, const int* front, long long nf,
+                int* big, ull* big_cnt, hipStream_t s);
+// a shard's own frontier (its F[cur] without the other ranks' replicated hubs) -> out
+void gcl_shard_own_front(const GDev& g, const GLists& L, long long lo, long long hi, int* out, ull* out_cnt,
+                         hipStream_t s);
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s);
 void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s);
 void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s);

@@ -597,6 +597,28 @@ extern "C" int gc_shard_reseed(gc_shard* sh, int64_t round, int64_t* nseeds, int
 }
 
 // final colours (every rank holds all of them) and optionally the round of colouring
+// The replicated colours (and rounds) into caller DEVICE buffers, and the rank's own frontier
+// (its F[cur] without the other ranks' replicated hubs) into front_dev (capacity hi - lo):
+// what gc_color_resume needs to finish the colouring on the one-GPU engine.
+extern "C" int gc_shard_export(gc_shard* sh, int32_t* colors_dev, int32_t* cround_dev, int32_t* front_dev,
+                               int64_t* nfront) {
+    if (!sh || !colors_dev || !front_dev || !nfront) { gc_set_error("gc_shard_export: null argument"); return GC_EINVAL; }
+    gc_graph* g = &sh->v;
+    GC_HIP(hipSetDevice(g->device));
+    const GDev d = shard_view(sh);
+    const GLists L = shard_lists(sh, nullptr);
+    gcl_finalize(d, gc_grid_for_waves(g->n, 8192), g->stream);
+    GC_HIP(hipMemcpyAsync(colors_dev, g->color, sizeof(int) * g->n, hipMemcpyDeviceToDevice, g->stream));
+    if (cround_dev) GC_HIP(hipMemcpyAsync(cround_dev, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToDevice, g->stream));
+    GC_HIP(hipMemsetAsync(&g->ctl->list_cnt, 0, sizeof(ull), g->stream));
+    gcl_shard_own_front(d, L, sh->lo, sh->hi, front_dev, &g->ctl->list_cnt, g->stream);
+    int rc = shard_sync(sh);
+    if (rc) return rc;
+    *nfront = (int64_t)g->hctl->list_cnt;
+    GC_HIP(hipMemsetAsync(&g->ctl->list_cnt, 0, sizeof(ull), g->stream));
+    return GC_OK;
+}
+
 extern "C" int gc_shard_colors(gc_shard* sh, int32_t* colors_out, int32_t* cround_out) {
     if (!sh) { gc_set_error("null shard"); return GC_EINVAL; }
     gc_graph* g = &sh->v;

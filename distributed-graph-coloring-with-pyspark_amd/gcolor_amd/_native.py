@@ -27,14 +27,14 @@ KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "va
 
 # Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
 EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
-           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_validate",
+           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate",
            "gc_gen_uniform", "gc_last_error", "gc_release_cache", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
            "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors", "gc_shard_set_stream",
            "gc_shard_propose_async", "gc_shard_sweep_async", "gc_shard_pack",
            "gc_shard_get_slice", "gc_shard_put_slices", "gc_shard_hub_count", "gc_shard_start_hubs",
            "gc_shard_start_hubs_async", "gc_shard_resume_hubs", "gc_shard_finish_async",
-           "gc_shard_apply_checked", "gc_shard_clear_halt",
+           "gc_shard_apply_checked", "gc_shard_clear_halt", "gc_shard_export",
            "gc_json_read_graph", "gc_json_write_coloring", "gc_json_write_graph", "gc_csr_write", "gc_csr_read",
            "gc_csr_free"]
 
@@ -103,6 +103,8 @@ def load():
         "gc_graph_export_device": ([P, P, P], ctypes.c_int),
         "gc_graph_lower_counts": ([P, P], ctypes.c_int),
         "gc_color": ([P, ctypes.POINTER(GcOptions), P, P, ctypes.POINTER(GcStats)], ctypes.c_int),
+        "gc_color_resume": ([P, ctypes.POINTER(GcOptions), P, P, P, I64, I64, P, P, ctypes.POINTER(GcStats)],
+                            ctypes.c_int),
         "gc_validate": ([P, P, _I64P, _I64P], ctypes.c_int),
         "gc_gen_uniform": ([I64, I32, U64, P, P, I64, _I64P], ctypes.c_int),
         "gc_last_error": ([], ctypes.c_char_p),
@@ -124,6 +126,7 @@ def load():
         "gc_shard_pack": ([P, I32, I32, P, P, I64], ctypes.c_int),
         "gc_shard_reseed": ([P, I64, _I64P, _I64P], ctypes.c_int),
         "gc_shard_colors": ([P, P, P], ctypes.c_int),
+        "gc_shard_export": ([P, P, P, P, _I64P], ctypes.c_int),
         "gc_shard_hub_count": ([P, _I64P], ctypes.c_int),
         "gc_shard_start_hubs": ([P, I32, I32, _I64P], ctypes.c_int),
         "gc_shard_start_hubs_async": ([P, I32, I32, I32], ctypes.c_int),

@@ -182,7 +182,22 @@ class DeviceGraph:
                             speculative=1 if speculative else 0, reserved=0)
         return self._color(opt, want_rounds, want_colors, ROUND_CAP)
 
-    def _color(self, opt, want_rounds, want_colors, cap):
+    def resume(self, colors_dev, front_dev, nfront, round0, cround_dev=None, num_colors=None, e1=True,
+               want_rounds=True, want_colors=True, kernel_timing=False):
+        """The colouring continued from round ``round0`` of a run in progress (gc_color_resume):
+        ``colors_dev`` / ``cround_dev`` / ``front_dev`` are DEVICE pointers (ints) of int32 arrays
+        -- the colours so far (-1 uncoloured), the round each was coloured in (or None), and the
+        ``nfront`` uncoloured vertices with a coloured listed neighbour.  Variant A, reference
+        rank.  The records are those of rounds round0, round0 + 1, ..."""
+        opt = nat.GcOptions(variant=nat.GC_VARIANT_A, e1=1 if e1 else 0,
+                            num_colors=-1 if num_colors is None else int(num_colors),
+                            kernel_timing=_timing_mask(kernel_timing), priority=nat.GC_PRIORITY_REF, seed=0,
+                            speculative=0, reserved=0)
+        args = (ctypes.c_void_p(colors_dev), ctypes.c_void_p(cround_dev) if cround_dev else None,
+                ctypes.c_void_p(front_dev) if front_dev else None, int(nfront), int(round0))
+        return self._color(opt, want_rounds, want_colors, ROUND_CAP, resume=args)
+
+    def _color(self, opt, want_rounds, want_colors, cap, resume=None):
         st = nat.GcStats()
         cap = cap if want_rounds else 0
         rb = {k: np.zeros(max(cap, 1), np.int64) for k in ("U", "F", "maxmex", "accepted", "seeds")}
@@ -192,11 +207,15 @@ class DeviceGraph:
                 setattr(st, "round_" + k, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
         colors = np.empty(self.n, np.int32) if want_colors else None
         cround = np.empty(self.n, np.int32) if want_colors else None
-        status = self._lib.gc_color(self._h, ctypes.byref(opt), _ptr(colors), _ptr(cround), ctypes.byref(st))
-        nat.check("gc_color", status, ok=(nat.GC_OK, nat.GC_FAILED, nat.GC_STALLED))
+        if resume is None:
+            status = self._lib.gc_color(self._h, ctypes.byref(opt), _ptr(colors), _ptr(cround), ctypes.byref(st))
+        else:
+            status = self._lib.gc_color_resume(self._h, ctypes.byref(opt), *resume, _ptr(colors), _ptr(cround),
+                                               ctypes.byref(st))
+        nat.check("gc_color_resume" if resume else "gc_color", status, ok=(nat.GC_OK, nat.GC_FAILED, nat.GC_STALLED))
         r = st.rounds
         if want_rounds and r > cap:  # more rounds than the buffers hold (long paths): once more, sized
-            return self._color(opt, want_rounds, want_colors, int(r))
+            return self._color(opt, want_rounds, want_colors, int(r), resume=resume)
         kernels = {}
         for i, name in enumerate(nat.KERNEL_CLASSES):
             kernels[name] = {"launches": int(st.k_launches[i]), "ms": float(st.k_ms[i]), "bytes": float(st.k_bytes[i])}

@@ -314,6 +314,17 @@ class HipShard:
         nat.check("gc_shard_reseed", self._lib.gc_shard_reseed(self._h, r, ct.byref(self._a), ct.byref(self._b)))
         return self._a.value, self._b.value
 
+    def export_state(self, track_rounds):
+        """The replicated state at a round top, in HBM (gc_shard_export): int32 tensors of the
+        colours (-1 uncoloured), the rounds they were coloured in (None unless tracked) and the
+        rank's OWN frontier (uncoloured vertices of [lo, hi) with a coloured listed neighbour)."""
+        colors = torch.empty(max(self.n, 1), dtype=torch.int32, device=self.device)
+        cround = torch.empty(max(self.n, 1), dtype=torch.int32, device=self.device) if track_rounds else None
+        front = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+        nat.check("gc_shard_export", self._lib.gc_shard_export(self._h, _p(colors), _p(cround), _p(front),
+                                                               self._ct.byref(self._a)))
+        return colors[:self.n], None if cround is None else cround[:self.n], front[:self._a.value]
+
     def colors(self, track_rounds, fetch=True):
         """Final colours (and rounds) to host; fetch=False only settles them in HBM."""
         colors = np.empty(self.n, np.int32) if fetch else None
@@ -347,6 +358,7 @@ class ShardResult:
     fused_misses: int = 0  # fused propose seams that could not be applied (the unfused path followed)
     ahead_misses: int = 0  # sweep seams run ahead that overflowed (the host moved their deltas)
     ahead_seams: int = 0  # sweep seams run ahead of the host
+    switch_round: int = None  # hybrid_color: the round the one-GPU engine took over (None: never)
 
     @property
     def rounds(self):
@@ -371,7 +383,7 @@ def _hdr_values(words):
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
                 want_colors=True, inline=4096, deferred=True, hub_budget=3, fuse=True, ahead=4,
-                inline_max=1 << 16):
+                inline_max=1 << 16, switch_below=None, round0=0):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
@@ -409,7 +421,13 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     The inline part follows the frontiers: a round's is the last round's largest per-rank
     frontier rounded up to a power of two, between ``inline`` and ``inline_max`` (every rank
     derives it from the same headers), so a round whose frontier did not outgrow the last
-    one's moves its deltas in one all-gather per seam and runs fused."""
+    one's moves its deltas in one all-gather per seam and runs fused.
+
+    ``switch_below``: stop at the top of the first round whose frontier (all ranks) is
+    non-empty and smaller than that -- after the last round's finish has resolved and before
+    any of this round's exchanges is applied by the host -- and return with ``switch_round``
+    set (``hybrid_color`` hands the state to the one-GPU engine there).  ``round0`` numbers
+    the rounds of a run started from a colouring in progress."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -443,7 +461,8 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
             words = recv.view(P, -1)[:, :HDR]
         else:  # slice seam: header bytes in front of each rank's slice
             res.dense_exchanges += 1
-            words = recv.view(P, -1)[:, :hdr_bytes].contiguous().view(torch.int64)
+            # (reshape copies unless P == 1, where the row stride need not be a multiple of 8)
+            words = recv.view(P, -1)[:, :hdr_bytes].reshape(-1).view(torch.int64).view(P, HDR)
         return _hdr_values(words.cpu().numpy()), recv
 
     def finish_deltas(kind, hdr, recv, r, dense_ok):
@@ -472,7 +491,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     fuse_on = fuse and deferred and dense is not True and C0 > 0
     last_fmax = None  # largest per-rank frontier of the last propose seam (does the next one fit inline?)
     last_seams = 1  # sweep seams the last round needed (how many a fused round runs ahead)
-    r = 0
+    r = int(round0)
     while True:
         if U == 0 and pending is None:  # coloring.py:86-90
             rec(0, 0, -1, 0, 0)
@@ -535,6 +554,10 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
                 break
         F, maxmex, fails = int(hdr[:, 0].sum()), int(hdr[:, 1].max()), int(hdr[:, 2].sum())
         last_fmax = int(hdr[:, 0].max())
+        if switch_below is not None and 0 < F < int(switch_below):
+            # the round's proposals and any sweeps run ahead touched no colour and no frontier
+            res.switch_round = r
+            break
         if F == 0:  # no proposer anywhere: the reference spins (coloring.py:93-95) -> E1
             if not e1:
                 rec(U, 0, -1, 0, 0)
@@ -605,7 +628,57 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     return res
 
 
-def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False, **kw):
+def engine_resume(dg, lock=None):
+    """``resume`` for ``hybrid_color``: the one-GPU engine (DeviceGraph.resume, gc_color_resume)
+    continues from the replicated state; ``lock`` serialises ranks that share ``dg`` (threads)."""
+    def run(colors, cround, front, round0, num_colors, e1, track_rounds, want_colors):
+        if colors.is_cuda:  # the state (and the all-gathered frontier) settled on torch's stream
+            torch.cuda.current_stream(colors.device).synchronize()
+        args = (colors.data_ptr(), front.data_ptr() if front.numel() else None, int(front.numel()), int(round0))
+        kw = dict(cround_dev=cround.data_ptr() if (track_rounds and cround is not None) else None,
+                  num_colors=num_colors, e1=e1, want_rounds=True, want_colors=want_colors)
+        if lock is None:
+            return dg.resume(*args, **kw)
+        with lock:
+            return dg.resume(*args, **kw)
+    return run
+
+
+def hybrid_color(ops, comm, resume, switch_below, num_colors=None, e1=True, track_rounds=False, want_colors=True,
+                 **kw):
+    """graph_coloring (coloring.py:73) over the ranks while the frontier is large, then on
+    every rank's own GPU alone: ``shard_color`` runs the sharded rounds until a round's
+    frontier (all ranks) drops below ``switch_below``; there every rank exports the
+    replicated colours and its own part of the frontier, the parts are all-gathered (the
+    ranges are disjoint: their union is the frontier) and ``resume`` -- the one-GPU engine
+    (``engine_resume``) -- runs the remaining rounds from that state on each rank alike.  The
+    long tail of small rounds then costs no exchange at all, while the big rounds are split
+    over the ranks.  Every rank returns the same ShardResult: the sharded rounds' records
+    followed by the engine's, the colours bit-identical to one GPU (LFMIS under the global
+    rank does not depend on where a round runs)."""
+    res = shard_color(ops, comm, num_colors, e1, track_rounds, want_colors=False, switch_below=switch_below, **kw)
+    if res.switch_round is None:  # finished (or failed / stalled) before the frontier got small
+        res.colors, res.colored_round = ops.colors(track_rounds, want_colors)
+        return res
+    colors, cround, front = ops.export_state(track_rounds)
+    counts = [int(x) for x in comm.gather_stats([front.numel()], colors.device)[:, 0]]
+    m = max(max(counts), 1)
+    send = torch.full((m,), -1, dtype=torch.int32, device=front.device)
+    send[:front.numel()].copy_(front)
+    allf = comm.allgather(send).view(comm.size, m)
+    front = torch.cat([allf[p, :counts[p]] for p in range(comm.size)])
+    tail = resume(colors, cround, front, res.switch_round, num_colors, e1, track_rounds, want_colors)
+    for key in ("U", "F", "maxmex", "accepted", "seeds"):
+        getattr(res, "round_" + key).extend(int(x) for x in getattr(tail, "round_" + key))
+    res.status, res.fail_round, res.fail_count = int(tail.status), int(tail.fail_round), int(tail.fail_count)
+    res.reseeds += int(tail.reseeds)
+    res.jp_sweeps += int(tail.jp_sweeps)
+    res.colors = tail.colors
+    res.colored_round = tail.colored_round if track_rounds else None
+    return res
+
+
+def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False, switch_below=None, **kw):
     """``parts`` shards of one colouring on the current GPU, driven by threads: the test
     and rehearsal path of the multi-GPU engine on one device."""
     rp, _ = dg.export()
@@ -616,9 +689,16 @@ def color_threads(dg, parts, num_colors=None, e1=True, track_rounds=False, **kw)
     out = [None] * parts
     err = []
 
+    lock = threading.Lock()
+
     def run(i):
         try:
-            out[i] = shard_color(shards[i], ThreadTransport(hub, i), num_colors, e1, track_rounds, **kw)
+            comm = ThreadTransport(hub, i)
+            if switch_below is None:
+                out[i] = shard_color(shards[i], comm, num_colors, e1, track_rounds, **kw)
+            else:
+                out[i] = hybrid_color(shards[i], comm, engine_resume(dg, lock), switch_below, num_colors, e1,
+                                      track_rounds, **kw)
         except BaseException as e:  # noqa: BLE001 - surface the first failure
             err.append(e)
             hub.barrier.abort()

@@ -140,6 +140,17 @@ typedef struct gc_stats {
 int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* colored_round_out,
              gc_stats* stats);
 
+/* The same colouring continued from round `round0` of a run in progress (variant A, reference
+   rank): colors_dev (DEVICE int32[n], -1 = uncoloured) are the colours so far, front_dev
+   (DEVICE int32[nfront]) the uncoloured vertices with a coloured listed neighbour (each
+   once, any order), cround_dev (DEVICE int32[n] or NULL) the round each was coloured in.
+   Replaces coloring.py:73-132 from that round on; stats hold the rounds from round0 (their
+   records, the failing round as an absolute index).  The multi-GPU hybrid hands the
+   replicated state of its sharded rounds to the one-GPU engine with it.                */
+int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t* colors_dev, const int32_t* cround_dev,
+                    const int32_t* front_dev, int64_t nfront, int64_t round0, int32_t* colors_out,
+                    int32_t* colored_round_out, gc_stats* stats);
+
 /* validate_graph_coloring counts: #uncoloured and the directed count of listed pairs
    (v, u in N(v)) with colour[u] == colour[v] (self-loops and duplicates count, as in
    coloring.py:157-158).  colors == NULL validates the device result of the last
@@ -226,6 +237,11 @@ int gc_shard_set_stream(gc_shard* s, void* stream);
 /* E1 re-seed on the replicated state (same seeds on every rank)                        */
 int gc_shard_reseed(gc_shard* s, int64_t round, int64_t* nseeds, int64_t* F_out);
 int gc_shard_colors(gc_shard* s, int32_t* colors_out, int32_t* colored_round_out);
+/* The replicated colours / rounds into DEVICE buffers and the rank's own frontier of the
+   current round (DEVICE int32, capacity hi - lo; *nfront = its length): the state
+   gc_color_resume continues from.                                                      */
+int gc_shard_export(gc_shard* s, int32_t* colors_dev, int32_t* colored_round_dev, int32_t* front_dev,
+                    int64_t* nfront);
 
 /* ---- host-side generator ------------------------------------------------------------ */
 /* The graph.py:30-43 process (per node: target = U{0..D}; draw random partners, keep

@@ -191,6 +191,12 @@ class NumpyShard:
             return None, None
         return self.c.astype(np.int32), (self.cround.astype(np.int32) if track else None)
 
+    def export_state(self, track):
+        """HipShard.export_state: the replicated colours (and rounds) and the OWN frontier."""
+        return (torch.from_numpy(self.c.astype(np.int32)),
+                torch.from_numpy(self.cround.astype(np.int32)) if track else None,
+                torch.tensor(self._frontier(), dtype=torch.int32))
+
 
 class DeferredNumpyShard(NumpyShard):
     """The stand-in with HipShard's enqueue-only round end and fused propose seam
@@ -250,3 +256,39 @@ class InflatedShard(DeferredNumpyShard):
             return super().sweep(i, count, emit)
         finally:
             self._x3 = False
+
+
+class ResumedNumpyShard(DeferredNumpyShard):
+    """One rank over every vertex, started from a colouring in progress: the stand-in for the
+    one-GPU engine's gc_color_resume in gcolor_amd.shard.hybrid_color."""
+
+    def __init__(self, rp, col, colors, cround):
+        super().__init__(rp, col, 0, len(rp) - 1)
+        self._c0 = np.asarray(colors, np.int64).copy()
+        self._r0 = None if cround is None else np.asarray(cround, np.int64).copy()
+
+    def begin(self, k, track):
+        self.acc_last, self.halted = 0, False
+        self.k, self.track = k, track
+        self.c = self._c0.copy()
+        self.cround = self._r0.copy() if self._r0 is not None else np.where(self.c >= 0, 0, -1)
+        self.cand = np.full(self.n, -1, np.int64)
+        self.state = np.zeros(self.n, np.int64)
+        return int((self.c == -1).sum()), len(self._frontier())
+
+
+def numpy_resume(rp, col, calls=None):
+    """``resume`` for hybrid_color on CPU: checks that the all-gathered frontier is exactly the
+    frontier of the exported colours, then runs the remaining rounds on one stand-in rank."""
+    from gcolor_amd import shard as shm
+
+    def run(colors, cround, front, round0, num_colors, e1, track_rounds, want_colors):
+        ops = ResumedNumpyShard(rp, col, colors.numpy(), None if cround is None else cround.numpy())
+        ops.c = ops._c0
+        got = front.tolist()
+        assert len(got) == len(set(got)) and sorted(got) == ops._frontier(), "exported frontier"
+        if calls is not None:
+            calls.append((int(round0), len(got)))
+        return shm.shard_color(ops, shm.ThreadTransport(shm.ThreadHub(1), 0), num_colors, e1, track_rounds,
+                               round0=round0)
+    return run

@@ -8,6 +8,9 @@ promoted to `gpu` once green.
 Run: GC_RUN_STAGED=1 python -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v
 * The asynchronous JP without hubs (GC_ASYNC=2): the uniform / mesh / directed cases that
   faulted at 10M vertices in round 3, small first, then C2.
+* The multi-GPU hybrid (gcolor_amd.shard.hybrid_color): gc_color_resume from the state at a
+  round start, against the uninterrupted run; sharded rounds then the one-GPU engine, against
+  one GPU.
 """
 import os
 import sys
@@ -134,3 +137,73 @@ def test_async_resolve_rmat24_matches(monkeypatch):
         for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
             assert list(getattr(g, k)) == list(getattr(ref, k)), k
         assert g.kernels["resolve"]["bytes"] == ref.kernels["resolve"]["bytes"]  # the first sweep's §8d credit
+
+
+# --- gc_color_resume and the multi-GPU hybrid -----------------------------------------------
+import test_shard_gpu as sg  # noqa: E402
+
+
+def _state_at(rp, col, colors, cround, r):
+    """the engine's state at the start of round r, from an uninterrupted run's colours and
+    rounds (coloured in round q -> cround q + 1; the seed and isolated vertices -> 0): the
+    colours so far and the frontier (uncoloured, with a coloured listed neighbour)."""
+    c = np.where(cround <= r, colors, -1).astype(np.int32)
+    cr = np.where(cround <= r, cround, -1).astype(np.int32)
+    deg = np.diff(rp)
+    src = np.repeat(np.arange(len(deg)), deg)
+    has = np.zeros(len(deg), bool)
+    np.logical_or.at(has, src, c[col] >= 0)
+    front = np.nonzero((c < 0) & has)[0].astype(np.int32)
+    return c, cr, front
+
+
+def _resume_matches(dg, rounds_at):
+    import torch
+    one = dg.color("A")
+    rp, col = dg.export()
+    for r in rounds_at:
+        r = min(r, one.rounds - 1)
+        c, cr, front = _state_at(rp, col, one.colors, one.colored_round, r)
+        ct, crt, ft = (torch.from_numpy(x).cuda() for x in (c, cr, front if len(front) else np.zeros(1, np.int32)))
+        torch.cuda.synchronize()
+        g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), r, cround_dev=crt.data_ptr())
+        assert g.status == one.status
+        assert np.array_equal(g.colors, one.colors) and np.array_equal(g.colored_round, one.colored_round)
+        for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
+            assert list(getattr(g, k)) == list(getattr(one, k))[r:], (k, r)
+
+
+def test_resume_golden_and_directed():
+    from gcolor_amd.engine import DeviceGraph
+    for name in sg.GOLD[::4]:
+        ids, adj, rp, col = sg.fixture_csr(sg.load_golden(name))
+        with DeviceGraph.from_csr(rp, col) as dg:
+            _resume_matches(dg, [0, 1, 3, 10**9])
+    for seed in range(2):
+        rp, col = sg._random_directed(3000, 9000, seed)
+        with DeviceGraph.from_csr(rp, col) as dg:
+            _resume_matches(dg, [0, 2, 7, 10**9])
+
+
+@pytest.mark.parametrize("scale", [10, 14])
+def test_resume_rmat_hubs(scale):
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(scale, 16, seed=2) as dg:
+        _resume_matches(dg, [0, 5, 40, 200])
+
+
+@pytest.mark.parametrize("switch_below", [1, 64, 2048, 10**9])
+def test_hybrid_threads(switch_below):
+    from gcolor_amd.engine import DeviceGraph
+    for name in sg.GOLD[::5]:
+        ids, adj, rp, col = sg.fixture_csr(sg.load_golden(name))
+        with DeviceGraph.from_csr(rp, col) as dg:
+            sg.same_as_single(dg, 3, switch_below=switch_below)
+    rp, col = sg._random_directed(3000, 9000, 1)
+    with DeviceGraph.from_csr(rp, col) as dg:
+        r, one = sg.same_as_single(dg, 2, switch_below=switch_below)
+        sg.same_as_single(dg, 3, k=max(one.max_color, 1), switch_below=switch_below)
+        sg.same_as_single(dg, 2, e1=False, switch_below=switch_below)
+    with DeviceGraph.rmat(13, 16, seed=4) as dg:
+        r, _ = sg.same_as_single(dg, 4, switch_below=switch_below)
+        assert (r.switch_round is None) == (switch_below == 1)

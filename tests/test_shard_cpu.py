@@ -19,7 +19,7 @@ from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
 
 sys.path.insert(0, REPO)
 from oracle import oracle  # noqa: E402
-from shard_numpy import DeferredNumpyShard, InflatedShard, NumpyShard  # noqa: E402
+from shard_numpy import DeferredNumpyShard, InflatedShard, NumpyShard, numpy_resume  # noqa: E402
 
 from gcolor_amd import shard as sh  # noqa: E402
 
@@ -33,7 +33,8 @@ def _random_directed(n, m, seed):
     return np.cumsum(rp), dst.astype(np.int32)
 
 
-def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, shard_cls=None, **kw):
+def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, shard_cls=None, switch_below=None, calls=None,
+                **kw):
     ranges = sh.balanced_ranges(rp, parts)
     hub = sh.ThreadHub(parts)
     out, err = [None] * parts, []
@@ -42,7 +43,12 @@ def run_threads(rp, col, parts, k=None, e1=True, deferred_ops=False, shard_cls=N
         try:
             cls = shard_cls or (DeferredNumpyShard if deferred_ops else NumpyShard)
             ops = cls(rp, col, *ranges[i])
-            out[i] = sh.shard_color(ops, sh.ThreadTransport(hub, i), k, e1, track_rounds=True, **kw)
+            comm = sh.ThreadTransport(hub, i)
+            if switch_below is None:
+                out[i] = sh.shard_color(ops, comm, k, e1, track_rounds=True, **kw)
+            else:
+                out[i] = sh.hybrid_color(ops, comm, numpy_resume(rp, col, calls if i == 0 else None), switch_below, k,
+                                         e1, track_rounds=True, **kw)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             hub.barrier.abort()
@@ -160,6 +166,50 @@ def test_sweep_seams_ahead_overflow(ahead):
         assert_matches_oracle(r, oracle.c_color(rp, col, "A"))
 
 
+@pytest.mark.parametrize("deferred_ops", [False, True])
+@pytest.mark.parametrize("parts", [2, 3])
+@pytest.mark.parametrize("switch_below", [1, 40, 150, 10**9])
+def test_hybrid_switch_to_one_engine(parts, switch_below, deferred_ops):
+    """hybrid_color: the sharded rounds while the frontier is large, then the rest from the
+    exported state on one engine (the stand-in for gc_color_resume): records, colours and
+    rounds equal the single-partition oracle's for every switch point -- never (1), mid-run,
+    and at round 0 (10**9) -- with the fused seams and the enqueue-only finish too."""
+    for seed in range(3):
+        rp, col = _random_directed(400, 2400, 30 + seed)
+        o = oracle.c_color(rp, col, "A")
+        calls = []
+        res = run_threads(rp, col, parts, deferred_ops=deferred_ops, switch_below=switch_below, calls=calls)
+        for r in res:
+            assert_matches_oracle(r, o)
+            assert r.switch_round == (calls[0][0] if calls else None)
+        if switch_below == 1:
+            assert not calls
+        elif switch_below == 10**9:
+            assert calls[0][0] == 0
+        if calls:  # the frontier handed over is the one the oracle's switch round proposed on
+            assert calls[0][1] == o["round_F"][calls[0][0]] and calls[0][1] < switch_below
+    ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
+    calls = []
+    res = run_threads(rp, col, parts, deferred_ops=deferred_ops, switch_below=switch_below, calls=calls)
+    assert_matches_oracle(res[-1], oracle.c_color(rp, col, "A"))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_hybrid_bounded_stalled_and_reseeded(seed):
+    """A bounded run that fails, a stall without E1 and E1 re-seeds on either side of the
+    switch: the engine's records continue the sharded ones."""
+    rp, col = _random_directed(300, 900, seed)
+    o = oracle.c_color(rp, col, "A")
+    for sw in (5, 30):
+        assert_matches_oracle(run_threads(rp, col, 2, switch_below=sw, deferred_ops=True)[0], o)
+        for k in (1, 2, int(o["max_color"])):
+            assert_matches_oracle(run_threads(rp, col, 2, k=k, switch_below=sw)[1], oracle.c_color(rp, col, "A", k=k))
+        s = oracle.c_color(rp, col, "A", e1=False)
+        r = run_threads(rp, col, 3, e1=False, switch_below=sw)[0]
+        assert r.status == s["status"] and np.array_equal(r.colors, s["colors"])
+        assert list(r.round_U) == list(s["round_U"])
+
+
 def test_more_ranks_than_vertices():
     rp = np.array([0, 1, 2], np.int64)
     col = np.array([1, 0], np.int32)
@@ -168,18 +218,22 @@ def test_more_ranks_than_vertices():
 
 
 # ---- two processes over torch.distributed (gloo), the transport the GPU ranks use -------
-def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096, deferred_ops=False):
+def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096, deferred_ops=False, switch_below=None):
     import torch.distributed as dist
     sys.path[:0] = [PKG_DIR, REPO, os.path.dirname(os.path.abspath(__file__))]
-    from shard_numpy import DeferredNumpyShard, NumpyShard
+    from shard_numpy import DeferredNumpyShard, NumpyShard, numpy_resume
     NS = DeferredNumpyShard if deferred_ops else NumpyShard
     from gcolor_amd import shard as shm
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     d = np.load(path)
     rp, col = d["rp"], d["col"]
     lo, hi = shm.balanced_ranges(rp, world)[rank]
-    res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, track_rounds=True, dense=dense,
-                          inline=inline, inline_max=inline)
+    kw = dict(track_rounds=True, dense=dense, inline=inline, inline_max=inline)
+    if switch_below is None:
+        res = shm.shard_color(NS(rp, col, lo, hi), shm.TorchTransport(), None, True, **kw)
+    else:
+        res = shm.hybrid_color(NS(rp, col, lo, hi), shm.TorchTransport(), numpy_resume(rp, col), switch_below, None,
+                               True, **kw)
     out = {"status": res.status, "colors": res.colors.tolist(), "cround": res.colored_round.tolist(),
            "U": res.round_U, "F": res.round_F, "maxmex": res.round_maxmex, "acc": res.round_accepted,
            "seeds": res.round_seeds}
@@ -188,16 +242,18 @@ def _gloo_worker(rank, world, port, path, out_dir, dense=None, inline=4096, defe
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,dense,inline,deferred_ops", [
-    ("gen_1000_8_s1", None, 4096, False), ("gen_1000_8_s1", True, 4096, False), ("asymmetric", None, 4096, False),
-    ("gen_1000_8_s1", None, 3, False), ("gen_1000_8_s1", False, 0, False),
-    ("gen_1000_8_s1", None, 4096, True), ("asymmetric", None, 3, True)])
-def test_gloo_world_size_2(case, dense, inline, deferred_ops, tmp_path):
+@pytest.mark.parametrize("case,dense,inline,deferred_ops,switch_below", [
+    ("gen_1000_8_s1", None, 4096, False, None), ("gen_1000_8_s1", True, 4096, False, None),
+    ("asymmetric", None, 4096, False, None), ("gen_1000_8_s1", None, 3, False, None),
+    ("gen_1000_8_s1", False, 0, False, None), ("gen_1000_8_s1", None, 4096, True, None),
+    ("asymmetric", None, 3, True, None), ("gen_1000_8_s1", None, 4096, True, 60), ("asymmetric", None, 3, False, 4)])
+def test_gloo_world_size_2(case, dense, inline, deferred_ops, switch_below, tmp_path):
     ids, adj, rp, col = fixture_csr(load_golden(case))
     path = str(tmp_path / "g.npz")
     np.savez(path, rp=rp, col=col)
     port = 29500 + random.randint(0, 2000)
-    torch.multiprocessing.spawn(_gloo_worker, args=(2, port, path, str(tmp_path), dense, inline, deferred_ops),
+    torch.multiprocessing.spawn(_gloo_worker,
+                                args=(2, port, path, str(tmp_path), dense, inline, deferred_ops, switch_below),
                                 nprocs=2, join=True)
     o = oracle.c_color(rp, col, "A")
     for r in range(2):
