@@ -207,3 +207,4 @@ def test_hybrid_threads(switch_below):
     with DeviceGraph.rmat(13, 16, seed=4) as dg:
         r, _ = sg.same_as_single(dg, 4, switch_below=switch_below)
         assert (r.switch_round is None) == (switch_below == 1)
+
