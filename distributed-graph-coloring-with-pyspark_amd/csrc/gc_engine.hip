@@ -640,6 +640,7 @@ struct Run {
             return GC_EHIP;
         }
         if (h.loop_err == 2) { gc_set_error("k_sweep_async: undecided list count out of range"); return GC_EHIP; }
+        if (h.loop_err == 4) { gc_set_error("gc_color_resume: a frontier entry is out of range"); return GC_EINVAL; }
         if (h.loop_err == 3) {
             gc_set_error("GC_CHECKS: out-of-range value code %lld (%lld, %lld, %lld) in round %lld", h.dbg[0], h.dbg[1],
                          h.dbg[2], h.dbg[3], h.round);

@@ -2923,10 +2923,16 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resume_init(GDev g, const int* col
     gc_block_add(&g.ctl->uncolored, unc, scratch);
 }
 
-// the frontier list F[0] and its claim bits (after k_resume_init's bitmap words)
+// the frontier list F[0] and its claim bits (after k_resume_init's bitmap words).  An entry
+// out of [0, n) is the caller's error: it is listed as vertex 0 (never read through) and
+// loop_err 4 makes k_resume_close stop the run before any round, and the host report it.
 __global__ void __launch_bounds__(GC_BLOCK) k_resume_front(GDev g, GLists L, const int* front, long long nf) {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (long long)gridDim.x * blockDim.x) {
-        const int v = front[i];
+        int v = front[i];
+        if (v < 0 || v >= g.n) {
+            __hip_atomic_store(&g.ctl->loop_err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = 0;
+        }
         L.F[0][i] = v;
         atomicOr(&g.inF[v >> 5], 1u << (v & 31));
     }
@@ -2953,6 +2959,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_resume_hbits(GDev g, const int* co
 __global__ void k_resume_close(GDev g, GLists L) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
+    if (c->loop_err == 4) {  // a frontier entry out of range (k_resume_front): no round runs
+        gc_st(&c->halt, (int)GC_H_DONE);
+        return;
+    }
     const long long U = (long long)c->uncolored;
     gc_st(&c->U, U);
     gc_precheck(L, c, U, (long long)c->fcnt[c->cur]);

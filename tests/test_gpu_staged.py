@@ -208,3 +208,19 @@ def test_hybrid_threads(switch_below):
         r, _ = sg.same_as_single(dg, 4, switch_below=switch_below)
         assert (r.switch_round is None) == (switch_below == 1)
 
+
+
+def test_resume_rejects_out_of_range_frontier():
+    """A frontier entry outside [0, n) stops gc_color_resume before any round (GC_EINVAL)."""
+    import torch
+    from gcolor_amd import _native as nat
+    from gcolor_amd.engine import DeviceGraph
+    rp, col = sg._random_directed(500, 2000, 3)
+    with DeviceGraph.from_csr(rp, col) as dg:
+        c = torch.full((dg.n,), -1, dtype=torch.int32, device="cuda")
+        c[0] = 0
+        f = torch.tensor([1, dg.n + 7], dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        with pytest.raises(nat.GcolorError, match="out of range"):
+            dg.resume(c.data_ptr(), f.data_ptr(), 2, 0)
+        assert dg.color("A").status == 0  # the handle is still usable
