@@ -403,7 +403,9 @@ __device__ __forceinline__ bool gc_async_stop_b(DevCtl* c, ull t0, long long bud
     return __shfl(stop, 0, GC_WAVE) != 0;
 }
 
-#define GC_BI_SHIFT 30
+// a work item is v | kind << GC_BI_SHIFT (kind 0 admission, 2 eviction time): non-negative
+// for n < 2^29 (-1 marks an empty lane), so the host runs k_b_async only below that
+#define GC_BI_SHIFT 29
 #define GC_BI_MASK ((1 << GC_BI_SHIFT) - 1)
 
 // b_adm_flag with agent-scope loads of the states and eviction times other waves write
@@ -431,7 +433,7 @@ struct BAsyncLds {  // one wave's rows
     int kind[GC_WAVE];
 };
 
-// one pass over the wave's light admission / eviction items l1[0, n1) (item = v | kind << 30);
+// one pass over the wave's light admission / eviction items l1[0, n1) (item = v | kind << GC_BI_SHIFT);
 // the unsettled ones are compacted to the front (an admitted vertex comes back as an
 // eviction item); returns their number
 __device__ int b_async_chunk_pass(GDev& g, int* l1, int n1, int* ev, BAsyncLds& s) {
@@ -702,7 +704,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // GC_ASYNC_BUDGET_US (20 ms) plus 20 ns per work item
     int b_async_grid = 0;
     long long b_async_budget = 0;
-    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0) {
+    // (its work items pack the vertex in GC_BI_SHIFT bits: n < 2^29)
+    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0 && g->n < (1ll << GC_BI_SHIFT)) {
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
