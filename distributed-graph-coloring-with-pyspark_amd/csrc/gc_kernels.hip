@@ -2207,12 +2207,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             const int hexcl = hincl - dh;
             const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
             gc_wave_sync();
-            for (int base = 0; base < htotal; base += GC_WAVE) {
-                const int e = base + lane;
+            gc_hub_mark_flat(g, htotal, [&](int e, int* x, int* c) {
                 const int o = gc_owner(hexcl, e);
                 const int eo = __shfl(hexcl, o, GC_WAVE);
-                if (e < htotal) gc_hub_mark(g, g.hin_col[s_start[w][o] + (e - eo)], s_cc[w][o]);
-            }
+                *x = e < htotal ? g.hin_col[s_start[w][o] + (e - eo)] : -1;
+                *c = e < htotal ? s_cc[w][o] : 0;
+            });
         }
         gc_wave_sync();
     }
