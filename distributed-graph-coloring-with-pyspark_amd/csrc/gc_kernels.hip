@@ -1701,6 +1701,11 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
 #ifndef GC_CSLOTS
 #define GC_CSLOTS 2
 #endif
+// GC_CLAIM_HOIST (build knob, staged in round 3): k_commit's claim check-loads of all
+// GC_CSLOTS slots before their atomics (see the claim loop)
+#ifndef GC_CLAIM_HOIST
+#define GC_CLAIM_HOIST 0
+#endif
 #ifndef GC_PREFETCH_ROW
 #define GC_PREFETCH_ROW 1
 #endif
@@ -2182,6 +2187,23 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 }
 #endif
             }
+#if GC_CLAIM_HOIST
+            // every slot's claim word first, then the atomics: in the loop below a slot's
+            // check-load waits for the previous slot's returning atomic (it may alias)
+            unsigned cw[GC_CSLOTS];
+#pragma unroll
+            for (int k = 0; k < GC_CSLOTS; ++k) cw[k] = (ok[k] && !mark) ? g.inF[x[k] >> 5] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_CSLOTS; ++k) {
+                claim[k] = false;
+                if (ok[k]) {
+                    const unsigned bit = 1u << (x[k] & 31);
+                    if (mark) g.mark[x[k]] = 1;
+                    else if ((FUSE && g.claim_direct) || !(cw[k] & bit))
+                        claim[k] = !(atomicOr(&g.inF[x[k] >> 5], bit) & bit);
+                }
+            }
+#else
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) {
                 claim[k] = false;
@@ -2191,6 +2213,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                     else claim[k] = gc_claim(g.inF, x[k]);
                 }
             }
+#endif
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) push(claim[k], x[k]);
         }
