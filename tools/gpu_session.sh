@@ -6,12 +6,14 @@
 #   tests             pytest -m gpu (every GPU test)
 #   tests:EXPR        pytest -m gpu -k EXPR (~ stands for a space: not~slow)
 #   file:PATH[:EXPR]  pytest -m gpu on one test file (optionally -k EXPR)
+#   staged[:EXPR]     the staged GPU tests (tests/test_gpu_staged.py, -m gpu_staged, GC_RUN_STAGED=1)
 #   smoke             __graft_entry__.smoke()
 #   bench:WL[:ARGS]   bench.py --workload WL [ARGS, comma-separated]
 #   step:WL           tools/step_timing.py WL (phase times of the step)
 #   profile:WL[:ARGS] tools/gpu_profile.sh TAG WL [ARGS] (trace + PMC passes, summaries)
 #   py:SCRIPT[:ARGS]  python SCRIPT [ARGS, comma-separated] (a tools/ script; 600 s limit)
 #   env:NAME=VALUE    export NAME=VALUE for the steps after it (env:NAME= unsets it)
+#   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
 # Output: gpurun_out/TAG/ (merged back by gpurun).
 set -uo pipefail
 TAG=$1
@@ -43,6 +45,12 @@ for st in "$@"; do
       else
         timeout -k 10 1000 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
       fi ;;
+    staged)
+      if [ -n "$rest" ]; then
+        GC_RUN_STAGED=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v --timeout 300 --timeout-method thread -k "$rest" > "$log" 2>&1
+      else
+        GC_RUN_STAGED=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
+      fi ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
     bench)
@@ -57,6 +65,10 @@ for st in "$@"; do
       nm=${rest%%=*}; vl=${rest#*=}
       if [ -n "$vl" ]; then export "$nm=$vl"; else unset "$nm"; fi
       true > "$log" ;;
+    ubench)
+      nm=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      hipcc --offload-arch=gfx950 -O3 "tools/ubench/$nm.hip" -o "$O/$nm" > "$log" 2>&1 &&
+        timeout -k 10 120 "$O/$nm" ${a//,/ } >> "$log" 2>&1 ;;
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
