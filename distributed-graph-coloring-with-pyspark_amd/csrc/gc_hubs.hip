@@ -328,13 +328,16 @@ int build(gc_graph* g, int T, int W) {
     }
     pc.mark("hin fill", s);
     if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
+        // the keys are hub indices < H: only their low bit_width(H - 1) bits are sorted
+        // (R-MAT-26: 20 of 32 bits, three 8-bit digit passes instead of four)
+        const unsigned kbits = (unsigned)std::max(1, 64 - __builtin_clzll((unsigned long long)std::max(H - 1, 1ll)));
         size_t bytes = 0;
         GC_HIP(rocprim::segmented_radix_sort_keys(nullptr, bytes, g->hlow_col, g->hpend[0], (unsigned)EL, (unsigned)H,
-                                                  g->hlow_rp, g->hlow_rp + 1, 0, 32, s));
+                                                  g->hlow_rp, g->hlow_rp + 1, 0, kbits, s));
         void* tmp = nullptr;
         GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
         const hipError_t e = rocprim::segmented_radix_sort_keys(tmp, bytes, g->hlow_col, g->hpend[0], (unsigned)EL,
-                                                                (unsigned)H, g->hlow_rp, g->hlow_rp + 1, 0, 32, s);
+                                                                (unsigned)H, g->hlow_rp, g->hlow_rp + 1, 0, kbits, s);
         hipStreamSynchronize(s);
         gc_dfree(tmp);
         GC_HIP(e);
