@@ -158,8 +158,37 @@ struct TileLds {
     ull w[GC_WAVES_PER_BLOCK];
     ull misc[4];
 };
+// GC_TILE_LDS_TRIM (build knob, default 1): each pass declares only the LDS rows it uses --
+// the rank partition and the hub fill no `aux` (48 KB: three workgroups per CU where their
+// registers allow, instead of two at 57 KB), the validation no `aux` / `base` (32 KB: four,
+// its register limit).  The tiles are latency-bound chains (~4 dependent memory trips each),
+// so more resident workgroups are more tiles in flight.  0: every pass the full TileLds.
+#ifndef GC_TILE_LDS_TRIM
+#define GC_TILE_LDS_TRIM 1
+#endif
+#if GC_TILE_LDS_TRIM
+struct TileLdsP {  // rank partition, hub fill
+    int off[GC_TW + 1];
+    unsigned key[GC_TW];
+    ull base[GC_TW + 1];
+    int buf[GC_TW + GC_TH];
+    ull w[GC_WAVES_PER_BLOCK];
+    ull misc[4];
+};
+struct TileLdsV {  // validation
+    int off[GC_TW + 1];
+    unsigned key[GC_TW];
+    int buf[GC_TW + GC_TH];
+    ull w[GC_WAVES_PER_BLOCK];
+    ull misc[4];
+};
+#else
+typedef TileLds TileLdsP;
+typedef TileLds TileLdsV;
+#endif
 
-__device__ __forceinline__ int tile_rows(const Tiles& T, long long t, TileLds& S, int* r0o, long long* e_beg, int* NE,
+template <class Lds>
+__device__ __forceinline__ int tile_rows(const Tiles& T, long long t, Lds& S, int* r0o, long long* e_beg, int* NE,
                                          bool* heavy_last) {
     const int r0 = T.r0[t], r1 = T.r0[t + 1];
     const int R = r1 - r0;
@@ -176,7 +205,8 @@ __device__ __forceinline__ int tile_rows(const Tiles& T, long long t, TileLds& S
 }
 
 // this thread's entries [j0, j0 + nv) of the staged tile, with their rows
-__device__ __forceinline__ int thread_entries(const TileLds& S, int R, int NE, int* u, int* rk) {
+template <class Lds>
+__device__ __forceinline__ int thread_entries(const Lds& S, int R, int NE, int* u, int* rk) {
     const int j0 = threadIdx.x * GC_PER;
     int nv = NE - j0;
     nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
@@ -205,7 +235,8 @@ __device__ __forceinline__ int thread_entries(const TileLds& S, int R, int NE, i
 
 // Row bases: the thread holding a row's first entry records prefix + its own entries before
 // it; rows starting at or past NE get the total.  Then base[R] = total.
-__device__ __forceinline__ void record_bases(TileLds& S, int R, int NE, int nv, ull prefix, ull total, unsigned m0,
+template <class Lds>
+__device__ __forceinline__ void record_bases(Lds& S, int R, int NE, int nv, ull prefix, ull total, unsigned m0,
                                              unsigned m1, unsigned m2) {
     const int j0 = threadIdx.x * GC_PER;
     if (nv > 0) {
@@ -303,7 +334,7 @@ __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u
 }
 
 template <int PRIO>
-__device__ void part_tile(const PartArgs& a, TileLds& S, long long t, ull* nbad) {
+__device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad) {
     int r0, NE;
     long long eb;
     bool hl;
@@ -354,7 +385,7 @@ __device__ void part_tile(const PartArgs& a, TileLds& S, long long t, ull* nbad)
 
 // segment of a heavy row, first pass: classes (kept for the second pass) and counts
 template <int PRIO>
-__device__ void part_seg1(const PartArgs& a, TileLds& S, long long s, ull* nbad) {
+__device__ void part_seg1(const PartArgs& a, TileLdsP& S, long long s, ull* nbad) {
     const int v = a.T.seg_row[s], j = a.T.seg_j[s];
     const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
     const long long e0 = rs + (long long)j * GC_SEG;
@@ -385,7 +416,7 @@ __device__ void part_seg1(const PartArgs& a, TileLds& S, long long s, ull* nbad)
 
 template <int PRIO>
 __global__ void __launch_bounds__(GC_BLOCK) k_part1(PartArgs a) {
-    __shared__ TileLds S;
+    __shared__ TileLdsP S;
     const long long nt = a.T.ntiles, ns = nseg_of(a.T);
     ull nbad = 0;
     for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
@@ -491,7 +522,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors, ull* unc_out,
                                                              ull* conf_out) {
-    __shared__ TileLds S;
+    __shared__ TileLdsV S;
     const long long nt = T.ntiles, ns = nseg_of(T);
     ull unc = 0, conf = 0;
     for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
@@ -563,7 +594,8 @@ struct HubArgs {
 };
 
 // hub entries of this thread's tile entries (mask) and those inside their row's low part
-__device__ __forceinline__ void hub_masks(const HubArgs& a, const TileLds& S, int nv, const int* u, const int* rk,
+template <class Lds>
+__device__ __forceinline__ void hub_masks(const HubArgs& a, const Lds& S, int nv, const int* u, const int* rk,
                                           unsigned* mk, unsigned* ml) {
     const int j0 = threadIdx.x * GC_PER;
     unsigned words[GC_PER];
@@ -674,7 +706,7 @@ __device__ __forceinline__ void hub_index_of(const HubArgs& a, const int* u, uns
 #endif
 
 __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
-    __shared__ TileLds S;
+    __shared__ TileLdsP S;
     const long long nt = a.T.ntiles, ns = nseg_of(a.T);
     for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
         if (it < nt) {
