@@ -210,6 +210,21 @@ def test_hybrid_bounded_stalled_and_reseeded(seed):
         assert list(r.round_U) == list(s["round_U"])
 
 
+@pytest.mark.parametrize("case", ["single", "isolated3", "edge", "selfloop"])
+def test_hybrid_tiny_graphs(case):
+    """Tiny graphs (nothing to colour, one round, a self-loop) through the hybrid, with more ranks
+    than vertices, switching never / at round 0."""
+    rp, col = {"single": ([0, 0], []), "isolated3": ([0, 0, 0, 0], []), "edge": ([0, 1, 2], [1, 0]),
+               "selfloop": ([0, 1], [0])}[case]
+    rp, col = np.array(rp, np.int64), np.array(col, np.int32)
+    o = oracle.c_color(rp, col, "A")
+    for parts in (1, 3):
+        for sw in (1, 10**9):
+            for d in (False, True):
+                for r in run_threads(rp, col, parts, switch_below=sw, deferred_ops=d):
+                    assert_matches_oracle(r, o)
+
+
 def test_more_ranks_than_vertices():
     rp = np.array([0, 1, 2], np.int64)
     col = np.array([1, 0], np.int32)
