@@ -1752,7 +1752,19 @@ struct GcClosePre {
     ull accepted, nx_failcnt, uncolored, fnext;
     long long nx_maxmex;
 };
-__device__ __attribute__((noinline)) void gc_close_round(const GLists& L, DevCtl* c, int mode, int fused,
+// GC_CLOSE_INLINE (build knob, default 1 since round 3): the close is inlined into k_commit /
+// k_close.  As a call (0, rounds 1-2) it gave both kernels a 176-byte private segment --
+// scratch set up for every wave of every launch -- for the one workgroup that closes the
+// round; inlined, no round kernel uses scratch (k_commit<0> 59 -> 69 VGPRs).
+#ifndef GC_CLOSE_INLINE
+#define GC_CLOSE_INLINE 1
+#endif
+#if GC_CLOSE_INLINE
+#define GC_CLOSE_ATTR __attribute__((always_inline)) inline
+#else
+#define GC_CLOSE_ATTR __attribute__((noinline))
+#endif
+__device__ GC_CLOSE_ATTR void gc_close_round(const GLists& L, DevCtl* c, int mode, int fused,
                                                         const GcClosePre& pre) {
     const long long acc = (long long)pre.accepted;
     long long U = c->U;
