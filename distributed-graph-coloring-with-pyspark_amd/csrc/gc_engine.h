@@ -118,7 +118,8 @@ int gc_build_tiling(gc_graph* g);
 // higher rank; nlow = c0 + c1, neq = c1 (neq may be null).  prio 0: key = deg (coloring.py:64),
 // 1: key = prio_hash(seed, v).  *bad (device) counts entries outside [0, n).
 int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad);
-int gc_validate_tiles(gc_graph* g, const int* colors);  // -> ctl->uncolored, ctl->conflicts
+// -> ctl->uncolored, ctl->conflicts; c8 (optional): the byte mirror of `colors` (the resident colouring)
+int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8 = nullptr);
 // symmetric graphs: hub transpose (hin_rp / hin_col: the hubs listed in each row) and the
 // lower-rank hubs of every hub row (hlow counts -> klow[x]); hubmap / hid / hub_v ready
 int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow);

@@ -778,7 +778,9 @@ extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolore
     }
     GC_HIP(hipMemsetAsync(&g->ctl->uncolored, 0, sizeof(ull), g->stream));
     GC_HIP(hipMemsetAsync(&g->ctl->conflicts, 0, sizeof(ull), g->stream));
-    if ((rc = gc_validate_tiles(g, src))) return rc;
+    // GC_VALIDATE_C8=1 (staged): the resident colouring's neighbours gathered from its byte mirror
+    const bool c8 = !colors && getenv("GC_VALIDATE_C8") && atoi(getenv("GC_VALIDATE_C8")) > 0;
+    if ((rc = gc_validate_tiles(g, src, c8 ? g->c8 : nullptr))) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));
     if (uncolored) *uncolored = (int64_t)g->hctl->uncolored;

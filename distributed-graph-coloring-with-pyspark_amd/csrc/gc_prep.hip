@@ -520,8 +520,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
 // #{(v, u): u listed in N(v), colour[u] == colour[v]} over the entries (directed, duplicates
 // and self-loops count, exactly as coloring.py:157-158)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors, ull* unc_out,
-                                                             ull* conf_out) {
+// C8 (GC_VALIDATE_C8=1, staged in round 3; the resident colouring only): the neighbours'
+// colours are gathered from the byte mirror c8 (n bytes instead of 4n: R-MAT-26 67 MB against
+// 268 MB of random-gather footprint), the int colour only when both bytes say ">= 254".
+// Colour equality == equal bytes and (byte < 254 or equal ints), since c8 = gc_c8_of(colour).
+__device__ __forceinline__ bool same_colour8(const int* colors, int u, unsigned cu8, int cv) {
+    const unsigned cv8 = gc_c8_of(cv);
+    return cu8 == cv8 && (cv8 != GC_C8_BIG || colors[u] == cv);
+}
+
+template <int C8>
+__global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors,
+                                                             const unsigned char* c8, ull* unc_out, ull* conf_out) {
     __shared__ TileLdsV S;
     const long long nt = T.ntiles, ns = nseg_of(T);
     ull unc = 0, conf = 0;
@@ -543,9 +553,15 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
             const int nv = thread_entries(S, R, NE, u, rk);
             int cu[GC_PER];
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) cu[k] = k < nv ? colors[u[k]] : 0;
+            for (int k = 0; k < GC_PER; ++k) cu[k] = k < nv ? (C8 ? (int)c8[u[k]] : colors[u[k]]) : 0;
+            if (C8) {
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) conf += (k < nv && cu[k] == (int)S.key[rk[k]]) ? 1 : 0;
+                for (int k = 0; k < GC_PER; ++k)
+                    conf += (k < nv && same_colour8(colors, u[k], (unsigned)cu[k], (int)S.key[rk[k]])) ? 1 : 0;
+            } else {
+#pragma unroll
+                for (int k = 0; k < GC_PER; ++k) conf += (k < nv && cu[k] == (int)S.key[rk[k]]) ? 1 : 0;
+            }
         } else {
             const long long s = it - nt;
             const int v = T.seg_row[s], j = T.seg_j[s];
@@ -553,14 +569,25 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
             const long long e0 = rs + (long long)j * GC_SEG;
             const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
             const int cv = colors[v];
-            int cu[GC_PER];
+            int uu[GC_PER], cu[GC_PER];
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {  // coalesced: entry threadIdx + k * 256
                 const int i = threadIdx.x + k * GC_BLOCK;
-                cu[k] = i < len ? colors[col[e0 + i]] : 0;
+                uu[k] = i < len ? col[e0 + i] : 0;
             }
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) conf += (threadIdx.x + k * GC_BLOCK < len && cu[k] == cv) ? 1 : 0;
+            for (int k = 0; k < GC_PER; ++k) {
+                const int i = threadIdx.x + k * GC_BLOCK;
+                cu[k] = i < len ? (C8 ? (int)c8[uu[k]] : colors[uu[k]]) : 0;
+            }
+            if (C8) {
+#pragma unroll
+                for (int k = 0; k < GC_PER; ++k)
+                    conf += (threadIdx.x + k * GC_BLOCK < len && same_colour8(colors, uu[k], (unsigned)cu[k], cv)) ? 1 : 0;
+            } else {
+#pragma unroll
+                for (int k = 0; k < GC_PER; ++k) conf += (threadIdx.x + k * GC_BLOCK < len && cu[k] == cv) ? 1 : 0;
+            }
         }
         __syncthreads();
     }
@@ -900,12 +927,16 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
     return GC_OK;
 }
 
-int gc_validate_tiles(gc_graph* g, const int* colors) {
+int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8) {
     if (g->n == 0) return GC_OK;
     int rc = gc_build_tiling(g);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_validate_tiles, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
-                       (const int*)g->col, colors, &g->ctl->uncolored, &g->ctl->conflicts);
+    if (c8)
+        hipLaunchKernelGGL(k_validate_tiles<1>, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
+                           (const int*)g->col, colors, c8, &g->ctl->uncolored, &g->ctl->conflicts);
+    else
+        hipLaunchKernelGGL(k_validate_tiles<0>, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
+                           (const int*)g->col, colors, c8, &g->ctl->uncolored, &g->ctl->conflicts);
     GC_HIP(hipGetLastError());
     return GC_OK;
 }

@@ -224,3 +224,34 @@ def test_resume_rejects_out_of_range_frontier():
         with pytest.raises(nat.GcolorError, match="out of range"):
             dg.resume(c.data_ptr(), f.data_ptr(), 2, 0)
         assert dg.color("A").status == 0  # the handle is still usable
+
+
+# --- validation from the byte mirror (GC_VALIDATE_C8=1, the resident colouring) -------------
+def test_validate_c8_matches(monkeypatch):
+    """The resident colouring validated from c8 counts what the int colours count: after a full
+    run, after a failed bounded run (uncoloured vertices), and after a resume from a state with
+    planted conflicts (colours < 254 and >= 254, the byte mirror's BIG case)."""
+    import torch
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(12, 16, seed=9) as dg:
+        rp, col = dg.export()
+        for k in (None, 3):
+            g = dg.color("A", num_colors=k)
+            monkeypatch.delenv("GC_VALIDATE_C8", raising=False)
+            ref = dg.validate()
+            monkeypatch.setenv("GC_VALIDATE_C8", "1")
+            assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
+        u = int(col[rp[0]]) if rp[1] > rp[0] else 1
+        c = np.full(dg.n, -1, np.int32)
+        c[0], c[u] = 300, 300  # a conflict past the byte mirror
+        w = int(col[rp[u]]) if rp[u + 1] > rp[u] else 2
+        c[w] = 5
+        front = np.array(sorted(set(int(x) for x in col[rp[0]:rp[1]]) - {0, u}), np.int32)
+        ct, ft = torch.from_numpy(c).cuda(), torch.from_numpy(front if len(front) else np.zeros(1, np.int32)).cuda()
+        torch.cuda.synchronize()
+        g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), 0)
+        monkeypatch.delenv("GC_VALIDATE_C8", raising=False)
+        ref = dg.validate()
+        monkeypatch.setenv("GC_VALIDATE_C8", "1")
+        assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
+        assert ref[1] > 0
