@@ -246,7 +246,7 @@ def test_validate_c8_matches(monkeypatch):
         c[0], c[u] = 300, 300  # a conflict past the byte mirror
         w = int(col[rp[u]]) if rp[u + 1] > rp[u] else 2
         c[w] = 5
-        front = np.array(sorted(set(int(x) for x in col[rp[0]:rp[1]]) - {0, u}), np.int32)
+        front = np.array(sorted(x for x in set(int(x) for x in col[rp[0]:rp[1]]) if c[x] < 0), np.int32)
         ct, ft = torch.from_numpy(c).cuda(), torch.from_numpy(front if len(front) else np.zeros(1, np.int32)).cuda()
         torch.cuda.synchronize()
         g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), 0)
