@@ -2047,6 +2047,50 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         }
         gc_stage_push(st, pred, val, next, next_cnt);
     };
+    // a winner's in-row [ts, te) strided over the calling threads (a wave, or the workgroup):
+    // every in-neighbour marked (big round) or claimed into the next frontier.  With
+    // GC_MARK_SLOTS > 1 a thread takes that many entries per step -- their tcol loads, then
+    // their claim words, then the atomics -- instead of one entry's three dependent memory
+    // trips at a time (a hub winner's in-row of up to GC_BIGROW entries walked by one wave)
+    auto walk_claims = [&](long long ts, long long te, int t0, int step) {
+#if GC_MARK_SLOTS > 1
+        for (long long e0 = ts + t0; e0 - t0 < te; e0 += (long long)GC_MARK_SLOTS * step) {
+            int xs[GC_MARK_SLOTS];
+            unsigned cw[GC_MARK_SLOTS];
+            bool cl[GC_MARK_SLOTS];
+#pragma unroll
+            for (int k = 0; k < GC_MARK_SLOTS; ++k) {
+                const long long e = e0 + (long long)k * step;
+                xs[k] = e < te ? g.tcol[e] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_MARK_SLOTS; ++k) cw[k] = (xs[k] >= 0 && !mark) ? g.inF[xs[k] >> 5] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_MARK_SLOTS; ++k) {
+                cl[k] = false;
+                if (xs[k] >= 0) {
+                    const unsigned bit = 1u << (xs[k] & 31);
+                    if (mark) g.mark[xs[k]] = 1;
+                    else if (!(cw[k] & bit)) cl[k] = !(atomicOr(&g.inF[xs[k] >> 5], bit) & bit);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < GC_MARK_SLOTS; ++k) push(cl[k], xs[k] < 0 ? 0 : xs[k]);
+        }
+#else
+        for (long long e0 = ts; e0 < te; e0 += step) {
+            const long long e = e0 + t0;
+            bool claim = false;
+            int x = 0;
+            if (e < te) {
+                x = g.tcol[e];
+                if (mark) g.mark[x] = 1;
+                else claim = gc_claim(g.inF, x);
+            }
+            push(claim, x);
+        }
+#endif
+    };
     // hubs on: a wave per hub (in-rows past bigrow are deferred to k_commit_big)
     if (g.hub_w) {
         for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
@@ -2074,17 +2118,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 gc_hub_mark_row(g, v, cc, lane, GC_WAVE);  // gc_hubs.hip
                 if (mark || !big) {
                     const long long ts = g.trp[v], te = g.trp[v + 1];
-                    for (long long e0 = ts; e0 < te; e0 += GC_WAVE) {
-                        const long long e = e0 + lane;
-                        bool claim = false;
-                        int x = 0;
-                        if (e < te) {
-                            x = g.tcol[e];
-                            if (mark) g.mark[x] = 1;
-                            else claim = gc_claim(g.inF, x);
-                        }
-                        push(claim, x);
-                    }
+                    walk_claims(ts, te, lane, GC_WAVE);
                 }
             }
         }
@@ -2115,20 +2149,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         __syncthreads();
         if (w == 0) push(lane == 0 && s_lose, v);  // losers stay
         if (s_acc && g.hbits_w) gc_hub_mark_row(g, v, s_accc, threadIdx.x, blockDim.x);  // gc_hubs.hip
-        if (s_acc && (mark || !big)) {
-            const long long ts = g.trp[v], te = g.trp[v + 1];
-            for (long long e0 = ts; e0 < te; e0 += blockDim.x) {
-                const long long e = e0 + threadIdx.x;
-                bool claim = false;
-                int x = 0;
-                if (e < te) {
-                    x = g.tcol[e];
-                    if (mark) g.mark[x] = 1;
-                    else claim = gc_claim(g.inF, x);
-                }
-                push(claim, x);
-            }
-        }
+        if (s_acc && (mark || !big)) walk_claims(g.trp[v], g.trp[v + 1], threadIdx.x, blockDim.x);
         __syncthreads();
     }
     // light vertices: wave chunks
