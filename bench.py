@@ -124,9 +124,10 @@ def pmc_file(workload, variant):
 
 
 def lib_sha16():
-    """First 16 hex digits of sha256(libgcolor.so): the build a PMC summary describes."""
+    """First 16 hex digits of sha256(libgcolor.so) -- the library gcolor_amd loads (GC_LIB_PATH for
+    a variant build): the build a PMC summary describes."""
     import hashlib
-    p = os.path.join(PKG_DIR, "gcolor_amd", "lib", "libgcolor.so")
+    p = os.environ.get("GC_LIB_PATH") or os.path.join(PKG_DIR, "gcolor_amd", "lib", "libgcolor.so")
     if not os.path.exists(p):
         return None
     return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
