@@ -255,3 +255,46 @@ def test_validate_c8_matches(monkeypatch):
         monkeypatch.setenv("GC_VALIDATE_C8", "1")
         assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
         assert ref[1] > 0
+
+
+def _hybrid_gpu_worker(rank, world, port, out_dir):
+    import json
+    import torch
+    import torch.distributed as dist
+    sys.path[:0] = [sg.PKG_DIR, sg.REPO]
+    torch.cuda.set_device(0)
+    from gcolor_amd.engine import DeviceGraph
+    from gcolor_amd import shard as sh
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    out = {}
+    with DeviceGraph.rmat(12, 16, seed=9) as dg:
+        rp, _ = dg.export(col=False)
+        lo, hi = sh.balanced_ranges(rp, world)[rank]
+        ops = sh.HipShard(dg, lo, hi)
+        for sw in (256, 10**9):
+            res = sh.hybrid_color(ops, sh.TorchTransport(), sh.engine_resume(dg), sw, track_rounds=True)
+            out[str(sw)] = {"colors": res.colors.tolist(), "cround": res.colored_round.tolist(), "U": res.round_U,
+                            "acc": res.round_accepted, "switch": res.switch_round}
+        ops.close()
+    with open(os.path.join(out_dir, f"h{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def test_hybrid_two_processes(tmp_path):
+    """The hybrid as two processes over torch.distributed (gloo; both ranks on the one GPU):
+    sharded rounds, the frontier parts all-gathered, each rank resuming its own engine."""
+    import json
+    import random
+    import torch
+    from gcolor_amd.engine import DeviceGraph
+    port = 33000 + random.randint(0, 2000)
+    torch.multiprocessing.spawn(_hybrid_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    with DeviceGraph.rmat(12, 16, seed=9) as dg:
+        one = dg.color("A")
+    for r in range(2):
+        got = json.load(open(tmp_path / f"h{r}.json"))
+        for sw, res in got.items():
+            assert res["colors"] == list(one.colors) and res["cround"] == list(one.colored_round), sw
+            assert res["U"] == list(one.round_U) and res["acc"] == list(one.round_accepted), sw
+        assert got["1000000000"]["switch"] == 0
