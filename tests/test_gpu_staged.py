@@ -241,12 +241,16 @@ def test_validate_c8_matches(monkeypatch):
             ref = dg.validate()
             monkeypatch.setenv("GC_VALIDATE_C8", "1")
             assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
-        u = int(col[rp[0]]) if rp[1] > rp[0] else 1
+        v = int(np.argmax(np.diff(rp)))  # the largest row: it has neighbours
+        u = int(col[rp[v]])
         c = np.full(dg.n, -1, np.int32)
-        c[0], c[u] = 300, 300  # a conflict past the byte mirror
-        w = int(col[rp[u]]) if rp[u + 1] > rp[u] else 2
+        c[v], c[u] = 300, 300  # a conflict past the byte mirror
+        w = next(int(x) for x in col[rp[u]:rp[u + 1]] if int(x) not in (u, v))
+        x = next((int(y) for y in col[rp[w]:rp[w + 1]] if int(y) not in (u, v, w)), None)
         c[w] = 5
-        front = np.array(sorted(x for x in set(int(x) for x in col[rp[0]:rp[1]]) if c[x] < 0), np.int32)
+        if x is not None:
+            c[x] = 5  # a conflict below 254
+        front = np.array(sorted(y for y in set(int(y) for y in col[rp[v]:rp[v + 1]]) if c[y] < 0), np.int32)
         ct, ft = torch.from_numpy(c).cuda(), torch.from_numpy(front if len(front) else np.zeros(1, np.int32)).cuda()
         torch.cuda.synchronize()
         g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), 0)
