@@ -14,6 +14,8 @@
 #   py:SCRIPT[:ARGS]  python SCRIPT [ARGS, comma-separated] (a tools/ script; 600 s limit)
 #   env:NAME=VALUE    export NAME=VALUE for the steps after it (env:NAME= unsets it)
 #   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
+#   rounds:WL         per-round kernel cost by frontier size (tools/round_cost.py under
+#                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
 # Output: gpurun_out/TAG/ (merged back by gpurun).
 set -uo pipefail
 TAG=$1
@@ -69,6 +71,13 @@ for st in "$@"; do
       nm=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       hipcc --offload-arch=gfx950 -O3 "tools/ubench/$nm.hip" -o "$O/$nm" > "$log" 2>&1 &&
         timeout -k 10 120 "$O/$nm" ${a//,/ } >> "$log" 2>&1 ;;
+    rounds)
+      mkdir -p "$O/rounds_$rest"
+      ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/rounds_$rest" -o run -- \
+          python "$ROOT/tools/round_cost.py" run "$rest" "$O/rounds_$rest/records.json" 2 ) > "$log" 2>&1 &&
+        python tools/round_cost.py analyze "$O/rounds_$rest/run_kernel_trace.csv" "$O/rounds_$rest/records.json" \
+          > "$O/rounds_$rest/round_cost.txt" 2>> "$log" &&
+        rm -f "$O/rounds_$rest/run_kernel_trace.csv" && cat "$O/rounds_$rest/round_cost.txt" >> "$log" ;;
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
