@@ -490,6 +490,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
                                       + (f"; hybrid: from the first round with a frontier below {switch_below} "
                                          f"every rank finishes on its own one-GPU engine" if hybrid else ""),
                        "multi": "hybrid" if hybrid else "sharded", "switch_round": res.switch_round,
+                       "step": "the colouring of a resident, partitioned graph (creation and validation outside the "
+                               "timed region, unlike the one-GPU / replicated step)",
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
                        "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2),
