@@ -404,7 +404,7 @@ extern "C" int gc_json_read_graph(const char* path, gc_csr** out) {
         return GC_ENOMEM;
     }
     memcpy(c->row_ptr, rp.data(), sizeof(int64_t) * (size_t)(n + 1));
-    memcpy(c->ids, ids.data(), sizeof(int64_t) * (size_t)n);
+    if (n) memcpy(c->ids, ids.data(), sizeof(int64_t) * (size_t)n);  // (an empty vector's data() may be null)
     bool identity = true;  // ids == 0..n-1 in order: positions are the ids
     for (int64_t i = 0; i < n && identity; ++i) identity = ids[(size_t)i] == i;
     IdMap map;
@@ -533,7 +533,8 @@ extern "C" int gc_csr_read(const char* path, gc_csr** out) {
     memcpy(&nnz, m.p + 16, 8);
     memcpy(&flags, m.p + 24, 4);
     memcpy(&has_ids, m.p + 28, 4);
-    if (n < 0 || n > INT32_MAX || nnz < 0 || has_ids > 1) {
+    // (nnz bounded by the file size first: 4 * nnz must not wrap the size arithmetic below)
+    if (n < 0 || n > INT32_MAX || nnz < 0 || nnz > (int64_t)(m.len / 4) || has_ids > 1) {
         gc_set_error("%s: bad GCSR header (n=%lld nnz=%lld)", path, (long long)n, (long long)nnz);
         return GC_EINVAL;
     }
