@@ -95,7 +95,7 @@ static int buf_push(Buf* b, int32_t v) {
 static int64_t merge(Buf* bufs, int nt, int32_t* out) {
     int64_t o = 0;
     for (int t = 0; t < nt; ++t) {
-        memcpy(out + o, bufs[t].a, sizeof(int32_t) * (size_t)bufs[t].n);
+        if (bufs[t].n) memcpy(out + o, bufs[t].a, sizeof(int32_t) * (size_t)bufs[t].n);  /* (a may be NULL) */
         o += bufs[t].n;
         bufs[t].n = 0;
     }

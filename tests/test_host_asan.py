@@ -149,3 +149,20 @@ def test_gcsr_corruptions(driver, tmp_path):
 def test_generator(driver, n, d, seed):
     (st, nnz, _), = _run(driver, "gen", str(n), str(d), str(seed))
     assert int(st) == 0 and 0 <= int(nnz) <= n * d
+
+
+def test_oracles_under_sanitizers(tmp_path):
+    """The CPU oracles (oracle/gcolor_oracle.c every mode, oracle/gcolor_omp.c on 1-4 threads)
+    under ASan+UBSan on 60 seeded random directed / symmetric multigraphs with self-loops and
+    hubs, the OpenMP restatement cross-checked against the single-thread oracle (colours, rounds
+    of colouring, every per-round record) inside the driver."""
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    exe = str(tmp_path / "orc_asan")
+    cmd = ["gcc", "-std=c11", "-O1", "-g", "-fopenmp", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", os.path.join(REPO, "tests", "host_asan", "oracle_driver.c"),
+           os.path.join(REPO, "oracle", "gcolor_oracle.c"), os.path.join(REPO, "oracle", "gcolor_omp.c"), "-o", exe, "-lm"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _run(exe, "60")
+    assert out[-1] == ["ok", "60", "graphs"]
