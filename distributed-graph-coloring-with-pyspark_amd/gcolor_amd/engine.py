@@ -185,6 +185,7 @@ class DeviceGraph:
     def resume(self, colors_dev, front_dev, nfront, round0, cround_dev=None, num_colors=None, e1=True,
                want_rounds=True, want_colors=True, kernel_timing=False):
         """The colouring continued from round ``round0`` of a run in progress (gc_color_resume):
+        the rest of graph_coloring's loop (coloring.py:85-132) from a round start.
         ``colors_dev`` / ``cround_dev`` / ``front_dev`` are DEVICE pointers (ints) of int32 arrays
         -- the colours so far (-1 uncoloured), the round each was coloured in (or None), and the
         ``nfront`` uncoloured vertices with a coloured listed neighbour.  Variant A, reference
@@ -230,7 +231,8 @@ class DeviceGraph:
                            kernels=kernels, async_aborts=int(st.async_aborts))
 
     def validate(self, colors=None):
-        """validate_graph_coloring counts on the device: (#uncoloured, #conflicting listed pairs).
+        """validate_graph_coloring counts on the device (coloring.py:149-162): (#uncoloured,
+        #conflicting listed pairs).
         ``colors=None`` validates the last colouring still resident on the device."""
         u, c = ctypes.c_int64(), ctypes.c_int64()
         arr = None if colors is None else np.ascontiguousarray(colors, dtype=np.int32)
