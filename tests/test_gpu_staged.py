@@ -20,7 +20,6 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import test_gpu_variant_b as vb  # noqa: E402
-from conftest import golden_names, load_golden  # noqa: E402
 
 # selected only by `-m gpu_staged` with GC_RUN_STAGED=1 (the CPU suite's -m "not gpu" skips them)
 pytestmark = [pytest.mark.gpu_staged,

@@ -5,11 +5,9 @@ import sys, random, json
 sys.path.insert(0,'.'); sys.path.insert(0,'tests'); sys.path.insert(0,'distributed-graph-coloring-with-pyspark_amd')
 import numpy as np
 from oracle import oracle
-from conftest import fixture_csr, golden_names, load_golden
 from test_oracle_omp import rmat_csr
 from gcolor_amd.generators import reference_csr
 def mesh(nx,ny,nz):
-    n=nx*ny*nz; rows=[]
     idx=lambda x,y,z: x+nx*(y+ny*z)
     rp=[0]; col=[]
     for z in range(nz):
