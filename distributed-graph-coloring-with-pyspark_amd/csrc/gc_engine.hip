@@ -299,7 +299,9 @@ struct Run {
         // Only with the hub JP's resumable scan (R-MAT and the like, validated at full size).
         // Graphs with no hub (uniform, meshes) keep the full-grid sweeps and the tail: a
         // 10M-vertex uniform graph with k_sweep_async on faulted in the following k_commit
-        // (round 3; DESIGN §5, open), and their JP chains are short anyway (C2: 15 rounds).
+        // (round 3; DESIGN §5: a mid-launch stage flush under the ticket close, fixed since
+        // (GC_COUNT_MASK), to be re-validated at that size before this turns on), and their JP
+        // chains are short anyway (C2: 15 rounds).
         if ((!d.hub_w && !force) || (d.hub_w && !d.hub_scan) || d.heavy_wg || L.delta) return;
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)

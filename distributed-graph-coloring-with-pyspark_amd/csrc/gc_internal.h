@@ -244,11 +244,18 @@ struct GcStage {
     int cnt;  // wave-uniform
 };
 
+// A commit that closes its own round (k_commit with tclose) counts arrivals in the high bits
+// of the next frontier's counter (gc_stage_flush_ticket: + 2^40 per workgroup), so a wave
+// whose stage overflows mid-launch reads back a count that carries the tickets of the
+// workgroups already done: the flushes take the entry count from the low bits only.
+#define GC_TICKET_SHIFT 40
+#define GC_COUNT_MASK ((1ull << GC_TICKET_SHIFT) - 1ull)
+
 __device__ __forceinline__ void gc_stage_flush(GcStage& s, int* out, ull* out_cnt) {
     gc_wave_sync();
     if (s.cnt == 0) return;
     ull base = 0;
-    if (gc_lane() == 0) base = atomicAdd(out_cnt, (ull)s.cnt);
+    if (gc_lane() == 0) base = atomicAdd(out_cnt, (ull)s.cnt) & GC_COUNT_MASK;
     base = __shfl(base, 0, GC_WAVE);
 #pragma unroll 1
     for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
@@ -270,7 +277,7 @@ __device__ __forceinline__ void gc_stage_flush_block(GcStage& s, int* out, ull* 
     if (threadIdx.x == 0) {
         int t = 0;
         for (int i = 0; i < NW; ++i) t += s_cnt[i];
-        s_base = t ? atomicAdd(out_cnt, (ull)t) : 0ull;
+        s_base = t ? atomicAdd(out_cnt, (ull)t) & GC_COUNT_MASK : 0ull;
     }
     __syncthreads();
     ull base = s_base;

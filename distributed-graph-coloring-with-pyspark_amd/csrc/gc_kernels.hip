@@ -1859,8 +1859,8 @@ __device__ void gc_snap_copy(DevCtl* c, DevCtl* snap) {
 // ticket in its high bits (count + 2^40), so the workgroup that sees every other arrival
 // knows it is last, with every counter atomic of the launch performed before its ticket
 // (each wave waits for its own atomics before the workgroup barrier that precedes it).
-// Returns true in the last workgroup; *fnext = the next frontier's size.
-#define GC_TICKET_SHIFT 40
+// Returns true in the last workgroup; *fnext = the next frontier's size.  (Waves whose stage
+// filled up flushed earlier with gc_stage_flush, which masks the tickets: GC_COUNT_MASK.)
 __device__ __forceinline__ bool gc_stage_flush_ticket(GcStage& s, int* out, ull* out_cnt, ull* fnext) {
     __shared__ int s_cnt[GC_WAVES_PER_BLOCK];
     __shared__ ull s_base, s_fin;
@@ -1873,7 +1873,7 @@ __device__ __forceinline__ bool gc_stage_flush_ticket(GcStage& s, int* out, ull*
         int t = 0;
         for (int i = 0; i < GC_WAVES_PER_BLOCK; ++i) t += s_cnt[i];
         const ull old = atomicAdd(out_cnt, (1ull << GC_TICKET_SHIFT) | (ull)t);
-        s_base = old & ((1ull << GC_TICKET_SHIFT) - 1);
+        s_base = old & GC_COUNT_MASK;
         s_fin = s_base + (ull)t;
         s_last = (old >> GC_TICKET_SHIFT) == (ull)gridDim.x - 1;
     }
@@ -2018,7 +2018,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
 #if GC_CHECKS
-    if (cnt > g.n || hcnt > g.n || (long long)(*next_cnt & ((1ull << GC_TICKET_SHIFT) - 1)) > g.n) {
+    if (cnt > g.n || hcnt > g.n || (long long)(*next_cnt & GC_COUNT_MASK) > g.n) {
         if (threadIdx.x == 0) gc_dbg(c, 10 + mode, cnt, hcnt, (long long)*next_cnt);
         return;
     }

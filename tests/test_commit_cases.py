@@ -1,0 +1,28 @@
+"""The k_commit corner-case states of tests/commit_cases.py, checked on CPU against the numpy
+restatement of the round loop (tests/shard_numpy.py, the stand-in for gc_color_resume): the
+expected colours and records the GPU tests assert are the reference's."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from commit_cases import stage_overflow_case  # noqa: E402
+from shard_numpy import numpy_resume  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle  # noqa: E402
+
+
+@pytest.mark.parametrize("K,leaves,n", [(8, 3, 40), (64, 9, 1000), (130, 40, 6000)])
+def test_stage_overflow_case_expectation(K, leaves, n):
+    rp, col, colors, front, exp = stage_overflow_case(K, leaves, n)
+    assert np.array_equal(np.diff(rp)[:K], np.full(K, leaves + 1))
+    res = numpy_resume(rp, col)(torch.from_numpy(colors), None, torch.from_numpy(front), 3, None, True, True, True)
+    assert res.status == 0
+    assert np.array_equal(res.colors, exp["colors"])
+    assert list(res.round_F[:2]) == exp["F"] and list(res.round_accepted[:2]) == exp["accepted"]
+    assert list(res.round_U[:2]) == exp["U"]
+    assert tuple(oracle.c_validate(rp, col, res.colors)) == (0, 0)

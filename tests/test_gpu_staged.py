@@ -209,6 +209,30 @@ def test_hybrid_threads(switch_below):
 
 
 
+@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}, {"GC_ASYNC": "2"}], ids=["fused", "unfused", "async_nohub"])
+def test_commit_stage_overflow_under_ticket_close(env, monkeypatch):
+    """tests/commit_cases.py: 32768 winners in the first 2048 wave chunks of a 16M-vertex graph
+    (frontier < n/256: the commit closes its own round with arrival tickets), each claiming 40
+    leaves -- 640 pushes per busy wave, past the 512-entry stage, after the 1024 idle waves have
+    taken their tickets.  Round 3's build took the mid-launch flush's base from the ticketed
+    counter (the 10M uniform fault); the colours and records must be exact."""
+    import torch
+    from commit_cases import stage_overflow_case
+    from gcolor_amd.engine import DeviceGraph
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rp, col, c, front, exp = stage_overflow_case(32768, 40, 1 << 24)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        ct, ft = torch.from_numpy(c).cuda(), torch.from_numpy(front).cuda()
+        torch.cuda.synchronize()
+        g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), 5)
+        assert g.status == 0
+        assert list(g.round_F[:2]) == exp["F"] and list(g.round_accepted[:2]) == exp["accepted"]
+        assert list(g.round_U[:2]) == exp["U"]
+        assert np.array_equal(g.colors, exp["colors"])
+        assert dg.validate() == (0, 0)
+
+
 def test_resume_rejects_out_of_range_frontier():
     """A frontier entry outside [0, n) stops gc_color_resume before any round (GC_EINVAL)."""
     import torch
