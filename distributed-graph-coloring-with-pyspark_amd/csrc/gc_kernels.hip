@@ -1813,9 +1813,127 @@ __device__ GC_CLOSE_ATTR void gc_close_round(const GLists& L, DevCtl* c, int mod
     gc_precheck(L, c, U, (long long)pre.fnext);
 }
 
+// GC_CLOSE_BATCH (build knob, staged in round 3, default 0): the close as ONE batch of loads
+// and then the stores.  gc_close_round interleaves them (each "store one field, then read
+// the next" waits for the store: a wave's loads and stores retire through one counter), so
+// the one thread that closes a round walks ~15 dependent L2 round trips -- k_close averaged
+// 8.2 us for one wave in round 2 (profiles/latest/rmat24/kernel_stats.csv), on the critical
+// path of every round (k_close, or the last workgroup of a ticket-closing commit).  Same
+// values, same records, same halts: every field is read before the close writes it, except
+// `round`, which is carried in a register across the records it advances.
+#ifndef GC_CLOSE_BATCH
+#define GC_CLOSE_BATCH 0
+#endif
+struct GcCloseCtl {  // the control words the close reads, as they were when it started
+    int halt, cur, e1;
+    ull f0, f1, seedkey;
+    long long U, sw, swt, maxd, bigs, huges, maxmex, round, rbase, rcap;
+};
+__device__ __forceinline__ GcCloseCtl gc_close_load(const DevCtl* c) {
+    GcCloseCtl k;
+    k.halt = c->halt;
+    k.cur = c->cur;
+    k.e1 = c->e1;
+    k.f0 = c->fcnt[0];
+    k.f1 = c->fcnt[1];
+    k.seedkey = c->seedkey;
+    k.U = c->U;
+    k.sw = c->sweeps;
+    k.swt = c->sweep_total;
+    k.maxd = c->maxdepth;
+    k.bigs = c->bigsweeps;
+    k.huges = c->hugesweeps;
+    k.maxmex = c->maxmex;
+    k.round = c->round;
+    k.rbase = c->rbase;
+    k.rcap = c->rcap;
+    return k;
+}
+// gc_close_body's `sorted` + gc_close_round + gc_precheck from the loaded words
+__device__ __forceinline__ void gc_close_batched(const GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big,
+                                                 int fused, const GcClosePre& pre, const GcCloseCtl& k) {
+    const long long acc = (long long)pre.accepted;
+    const ull fcur = k.cur ? k.f1 : k.f0;
+    long long U = k.U, round = k.round;
+    int cur = k.cur;
+    auto record = [&](long long u, long long f, long long mm, long long a, long long sd, long long sw) {
+        RoundRec* rec = L.rec + (round - k.rbase);
+        rec->U = u;
+        rec->F = f;
+        rec->maxmex = mm;
+        rec->accepted = a;
+        rec->seeds = sd;
+        rec->sweeps = sw;
+        ++round;
+    };
+    // next list built in order (gc_front_on on the round's own frontier)
+    c->sorted = mode == GC_CM_ROUND && allow_big && !k.halt && (long long)fcur * 64 >= (long long)g.n && fcur > 0;
+    if (mode == GC_CM_ROUND) {
+        gc_st(&c->sweep_total, k.swt + (k.sw > 0 ? k.sw - 1 : 0));
+        if (k.sw > k.maxd) gc_st(&c->maxdepth, k.sw);
+        gc_st(&c->lastdepth, k.sw);
+        gc_st(&c->lastbig, k.bigs);
+        gc_st(&c->bigsweeps, 0ll);
+        gc_st(&c->lasthuge, k.huges);
+        gc_st(&c->hugesweeps, 0ll);
+        record(U, (long long)fcur, k.maxmex, acc, 0, k.sw);
+        U -= acc;
+        gc_st(&c->fcnt[cur], 0ull);  // becomes the next round's output slot
+        cur ^= 1;
+        gc_st(&c->cur, cur);
+    } else if (mode == GC_CM_INIT) {
+        U = (long long)pre.uncolored - (k.seedkey ? 1 : 0);
+    } else {  // GC_CM_RESEED
+        record(U, 0, -1, 0, acc, 0);
+        U -= acc;
+    }
+    gc_st(&c->U, U);
+    gc_st(&c->heavy_cnt, 0ull);
+    gc_st(&c->wide_cnt, 0ull);
+    gc_st(&c->failcnt, pre.nx_failcnt);
+    gc_st(&c->accepted, 0ull);
+    gc_st(&c->maxmex, pre.nx_maxmex);
+    gc_st(&c->nx_failcnt, 0ull);
+    gc_st(&c->nx_maxmex, -1ll);
+    gc_st(&c->proposed, mode == GC_CM_ROUND && fused ? 1 : 0);
+    gc_st(&c->sweeps, 0ll);
+    gc_st(&c->hub_start, GC_HUB_NOT_STARTED);
+    gc_st(&c->loop_last, 0ll);
+    for (int j = 0; j < 3; ++j) {
+        gc_st(&c->und_cnt[j], 0ull);
+        gc_st(&c->undh_cnt[j], 0ull);
+    }
+    gc_st(&c->seed_cnt[0], 0ull);
+    gc_st(&c->bigw_cnt, 0ull);
+    gc_st(&c->use_c4, 0);
+    gc_st(&c->seed_cnt[1], 0ull);
+    // gc_precheck, with the round counter advanced by the records above
+    const long long F = (long long)pre.fnext;
+    int halt = GC_RUN;
+    if (U == 0) {
+        record(0, 0, -1, 0, 0, 0);
+        halt = GC_H_DONE;
+    } else if (F == 0) {
+        if (!k.e1) {
+            record(U, 0, -1, 0, 0, 0);
+            halt = GC_H_STALLED;
+        } else {
+            halt = GC_H_RESEED;
+        }
+    } else if (round - k.rbase + 4 >= k.rcap) {
+        halt = GC_H_ROUNDCAP;
+    }
+    if (round != k.round) gc_st(&c->round, round);
+    if (halt != GC_RUN) gc_st(&c->halt, halt);
+}
+
 __device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* c, int mode, int allow_big, int fused) {
     if (threadIdx.x >= GC_WAVE) return;
     const int lane = threadIdx.x;
+#if GC_CLOSE_BATCH
+    GcCloseCtl k{};
+    if (lane == 0) k = gc_close_load(c);  // in flight with the counter reads below
+#endif
     ull a = 0;  // the commit's slotted winner counts
     if (g.accs)
         for (int k = lane; k < GC_ACC_SLOTS; k += GC_WAVE) a += atomicExch(&g.accs[k], 0ull);
@@ -1835,10 +1953,14 @@ __device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* 
     pre.nx_maxmex = __shfl((long long)x, 3, GC_WAVE);
     pre.uncolored = (ull)__shfl((long long)x, 4, GC_WAVE);
     pre.fnext = (ull)__shfl((long long)x, 5, GC_WAVE);
+#if GC_CLOSE_BATCH
+    if (lane == 0) gc_close_batched(g, L, c, mode, allow_big, fused, pre, k);
+#else
     if (lane == 0) {
         c->sorted = mode == GC_CM_ROUND && gc_front_on(g, c, allow_big);  // next list built in order
         gc_close_round(L, c, mode, fused, pre);
     }
+#endif
 }
 
 // The whole control block into the host-mapped snapshot slot (one workgroup, every thread
