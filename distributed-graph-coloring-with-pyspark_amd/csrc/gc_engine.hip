@@ -405,13 +405,15 @@ struct Run {
         // the commit's last workgroup closes the round unless k_pull / the big-round frontier
         // rebuild / k_commit_big must run between the commit and the close
         const bool tclose = mode == GC_CM_ROUND && !big && (fuse || !d.big_rows) && ticket_close;
+        // ... or, with big rows (GC_BIG_CLOSE=1, staged), k_commit_big's
+        const bool bclose = mode == GC_CM_ROUND && !big && !tclose && d.big_rows && ticket_close && big_close;
         DevCtl* snap = mode == GC_CM_ROUND ? snap_ptr : nullptr;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
         gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0, tclose ? snap : nullptr,
-                   tclose ? 1 : 0);
+                   tclose ? 1 : 0, bclose ? snap : nullptr, bclose ? 1 : 0);
         kt.end();
         if (mode == GC_CM_ROUND) snap_ptr = nullptr;
-        if (tclose) {
+        if (tclose || bclose) {
             kt.close();
             proposed = fuse;
             return;
@@ -478,6 +480,9 @@ struct Run {
     DevCtl* snap_ptr = nullptr;  // handed to the next round's k_close (or closing commit)
     // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
     const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
+    // GC_BIG_CLOSE=1 (staged, round 3): graphs with big rows close the round in k_commit_big
+    // (no k_close launch per round: ~900 per R-MAT-24 colouring)
+    const bool big_close = getenv("GC_BIG_CLOSE") && atoi(getenv("GC_BIG_CLOSE")) > 0;
     int enqueue_batch(int B, int S, int slot) {
         for (int b = 0; b < B; ++b) {
             if (b == B - 1 && !snap_copy) snap_ptr = g->hsnap_dev + slot;

@@ -2428,11 +2428,26 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
 // 256 winners per tile (their row offsets prefix-summed in LDS, owner by binary search).
 // Walking the winners one after another cost ~5 dependent memory round trips per winner
 // on every workgroup: 1.8 ms for the ~400 hub winners of an R-MAT-26 round.
-__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big) {
+// tclose (GC_BIG_CLOSE=1, staged; ROUND mode, no big-round rebuild): this launch closes the
+// round instead of a k_close launch after it -- workgroup 0 when no winner was deferred, else
+// the last workgroup to arrive (arrival tickets on the next frontier's counter, as k_commit's
+// gc_stage_flush_ticket) -- and, with snap, writes the snapshot; on a halt it only writes the
+// snapshot (k_close's behaviour).
+__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big, DevCtl* snap,
+                                                         int tclose) {
     DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) return;
+    if (mode == GC_CM_ROUND && c->halt) {
+        if (tclose && snap && blockIdx.x == 0) gc_snap_copy(c, snap);
+        return;
+    }
     const long long nb = (long long)c->bigw_cnt;
-    if (nb == 0) return;
+    if (nb == 0) {
+        if (tclose && blockIdx.x == 0) {
+            gc_close_body(g, L, c, mode, 0, 0);
+            if (snap) gc_snap_copy(c, snap);
+        }
+        return;
+    }
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_off[GC_BLOCK + 1];  // exclusive prefix of the tile's per-winner work
     __shared__ long long s_hs[GC_BLOCK], s_ts[GC_BLOCK];
@@ -2502,7 +2517,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
         }
         __syncthreads();  // the tile's LDS is rewritten next
     }
-    gc_stage_flush_block(st, next, next_cnt);
+    if (!tclose) {
+        gc_stage_flush_block(st, next, next_cnt);
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's frontier entries have landed
+    ull fnext = 0;
+    if (gc_stage_flush_ticket(st, next, next_cnt, &fnext)) {  // the last workgroup closes the round
+        if (threadIdx.x == 0) gc_st(next_cnt, fnext);            // without the tickets
+        __syncthreads();
+        gc_close_body(g, L, c, mode, 0, 0);
+        if (snap) gc_snap_copy(c, snap);
+    }
 }
 
 // Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
@@ -3359,7 +3385,7 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused,
-                DevCtl* snap, int tclose) {
+                DevCtl* snap, int tclose, DevCtl* bsnap, int bclose) {
     if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
         hipLaunchKernelGGL(k_commit<1>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap,
                            tclose);
@@ -3367,7 +3393,7 @@ void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream
     }
     hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
+        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big, bsnap, bclose);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

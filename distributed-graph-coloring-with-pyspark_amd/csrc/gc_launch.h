@@ -109,9 +109,10 @@ int gcl_sweep_async_blocks_per_cu();
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
 // tclose: the commit's last workgroup also closes the round (no k_close; ROUND mode only,
-// never with allow_big or when k_commit_big follows); snap: its snapshot slot, or null
+// never with allow_big or when k_commit_big follows); snap: its snapshot slot, or null.
+// bclose / bsnap: the same for k_commit_big (graphs with big rows, GC_BIG_CLOSE=1)
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0,
-                int fused = 0, DevCtl* snap = nullptr, int tclose = 0);
+                int fused = 0, DevCtl* snap = nullptr, int tclose = 0, DevCtl* bsnap = nullptr, int bclose = 0);
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0, int fused = 0,
                DevCtl* snap = nullptr);
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s);  // see gc_hub_push_wave

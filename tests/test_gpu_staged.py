@@ -138,6 +138,52 @@ def test_async_resolve_rmat24_matches(monkeypatch):
         assert g.kernels["resolve"]["bytes"] == ref.kernels["resolve"]["bytes"]  # the first sweep's §8d credit
 
 
+# --- the round closed by k_commit_big (GC_BIG_CLOSE=1: no k_close launch on graphs with big rows) ---
+B_ENVS = [{"GC_BIG_CLOSE": "1"}, {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8"}, {"GC_BIG_CLOSE": "1", "GC_HUB_T": "0"},
+          {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8", "GC_BATCH_MAX": "1"}]
+B_IDS = ["bclose", "bclose_row8", "bclose_nohub", "bclose_row8_batch1"]
+
+
+@pytest.fixture(params=B_ENVS, ids=B_IDS)
+def benv(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_big_close_generator_graphs(benv):
+    hubs.test_reference_generator_graphs(benv)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_big_close_directed(benv, seed):
+    hubs.test_directed_multigraphs(benv, seed)
+
+
+@pytest.mark.parametrize("scale", [9, 12])
+def test_big_close_rmat(benv, scale):
+    hubs.test_rmat(benv, scale)
+
+
+@pytest.mark.parametrize("bigrow", ["0", "8", "64"])
+@pytest.mark.parametrize("hub_t", ["0", "4", "1024"])
+def test_big_close_commit_big_tiles(monkeypatch, bigrow, hub_t):
+    monkeypatch.setenv("GC_BIG_CLOSE", "1")
+    hubs.test_commit_big_tiles(monkeypatch, bigrow, hub_t)
+
+
+def test_big_close_rmat24_matches(monkeypatch):
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(24, 16, seed=1) as dg:
+        ref = dg.color("A")
+        monkeypatch.setenv("GC_BIG_CLOSE", "1")
+        g = dg.color("A")
+        assert np.array_equal(g.colors, ref.colors)
+        for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
+            assert list(getattr(g, k)) == list(getattr(ref, k)), k
+        assert dg.validate() == (0, 0)
+
+
 # --- gc_color_resume and the multi-GPU hybrid -----------------------------------------------
 import test_shard_gpu as sg  # noqa: E402
 
