@@ -505,6 +505,12 @@ extern "C" int gc_graph_info(const gc_graph* g, int64_t* n, int64_t* nnz, int64_
     return GC_OK;
 }
 
+extern "C" int gc_graph_device(const gc_graph* g, int32_t* device) {
+    if (!g || !device) { gc_set_error("null graph or output"); return GC_EINVAL; }
+    *device = g->device;
+    return GC_OK;
+}
+
 extern "C" int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col) {
     if (!g) { gc_set_error("null graph"); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));

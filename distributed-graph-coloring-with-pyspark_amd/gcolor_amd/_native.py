@@ -27,7 +27,7 @@ KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "va
 
 # Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
 EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
-           "gc_graph_destroy", "gc_graph_info", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate",
+           "gc_graph_destroy", "gc_graph_info", "gc_graph_device", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate",
            "gc_gen_uniform", "gc_last_error", "gc_release_cache", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
            "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors", "gc_shard_set_stream",
@@ -99,6 +99,7 @@ def load():
         "gc_graph_create_mesh": ([I64, I64, I64, PP], ctypes.c_int),
         "gc_graph_destroy": ([P], None),
         "gc_graph_info": ([P, _I64P, _I64P, _I64P, ctypes.POINTER(U32)], ctypes.c_int),
+        "gc_graph_device": ([P, ctypes.POINTER(I32)], ctypes.c_int),
         "gc_graph_export": ([P, P, P], ctypes.c_int),
         "gc_graph_export_device": ([P, P, P], ctypes.c_int),
         "gc_graph_lower_counts": ([P, P], ctypes.c_int),

@@ -77,6 +77,9 @@ class DeviceGraph:
         nat.check("gc_graph_info", self._lib.gc_graph_info(self._h, ctypes.byref(n), ctypes.byref(nnz),
                                                             ctypes.byref(md), ctypes.byref(fl)))
         self.n, self.nnz, self.max_degree, self.flags = n.value, nnz.value, md.value, fl.value
+        dev = ctypes.c_int32()
+        nat.check("gc_graph_device", self._lib.gc_graph_device(self._h, ctypes.byref(dev)))
+        self.device_index = dev.value  # the HIP device the graph lives on
 
     # ---- construction -------------------------------------------------------------------
     @classmethod

@@ -177,7 +177,12 @@ class HipShard:
         self._ct = ctypes
         self._lib = nat.load()
         self.dg, self.lo, self.hi, self.n = dg, int(lo), int(hi), dg.n
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        # the shard's kernels run on the graph's device, so its stream and buffers live there
+        self.device = torch.device("cuda", dg.device_index) if device is None else torch.device(device)
+        if self.device.type != "cuda" or self.device.index not in (None, dg.device_index):
+            raise ValueError(f"HipShard on {self.device}: the graph lives on cuda:{dg.device_index}")
+        if self.device.index is None:
+            self.device = torch.device("cuda", dg.device_index)
         h = ctypes.c_void_p()
         nat.check("gc_shard_create", self._lib.gc_shard_create(dg._h, self.lo, self.hi, ctypes.byref(h)))
         self._h = h

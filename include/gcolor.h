@@ -64,6 +64,8 @@ int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a, double b,
 int gc_graph_create_mesh(int64_t nx, int64_t ny, int64_t nz, gc_graph** out);
 void gc_graph_destroy(gc_graph* g);
 int gc_graph_info(const gc_graph* g, int64_t* n, int64_t* nnz, int64_t* max_degree, uint32_t* flags);
+/* The HIP device the graph lives on (the current device when it was created).        */
+int gc_graph_device(const gc_graph* g, int32_t* device);
 /* Copy the device CSR back (row_ptr int64[n+1], col int32[nnz]); either may be NULL.
    Rows come back in the engine's order: each row lists its lower-rank neighbours
    (rank = (deg, pos), coloring.py:64) first -- the same multiset as the input row.   */

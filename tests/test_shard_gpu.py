@@ -125,6 +125,21 @@ def test_seeded_colour_between_sharded_runs():
         same_as_single(dg, 3)
 
 
+def test_shard_follows_the_graph_device():
+    """A shard runs on its graph's device (gc_graph_device): its stream and buffers default
+    there, and another device is refused before anything is created."""
+    import torch
+    from gcolor_amd import shard as sh
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(8, 8, seed=1) as dg:
+        assert dg.device_index == torch.cuda.current_device()
+        ops = sh.HipShard(dg, 0, dg.n)
+        assert ops.device == torch.device("cuda", dg.device_index) and ops.delta.device == ops.device
+        ops.close()
+        with pytest.raises(ValueError, match="lives on"):
+            sh.HipShard(dg, 0, dg.n, device=f"cuda:{dg.device_index + 1}")
+
+
 @pytest.mark.parametrize("seed", range(2))
 def test_replicated_hubs_sharded(seed, monkeypatch):
     """A low hub threshold makes most proposers replicated hubs: every rank proposes,
