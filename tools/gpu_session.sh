@@ -74,10 +74,11 @@ for st in "$@"; do
     rounds)
       mkdir -p "$O/rounds_$rest"
       ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/rounds_$rest" -o run -- \
-          python "$ROOT/tools/round_cost.py" run "$rest" "$O/rounds_$rest/records.json" 2 ) > "$log" 2>&1 &&
-        python tools/round_cost.py analyze "$O/rounds_$rest/run_kernel_trace.csv" "$O/rounds_$rest/records.json" \
+          python3 "$ROOT/tools/round_cost.py" run "$rest" "$O/rounds_$rest/records.json" 2 ) > "$log" 2>&1 &&
+        tr=$(find "$O/rounds_$rest" -name '*kernel_trace.csv' -print -quit) && [ -n "$tr" ] &&
+        python tools/round_cost.py analyze "$tr" "$O/rounds_$rest/records.json" \
           > "$O/rounds_$rest/round_cost.txt" 2>> "$log" &&
-        rm -f "$O/rounds_$rest/run_kernel_trace.csv" && cat "$O/rounds_$rest/round_cost.txt" >> "$log" ;;
+        rm -f "$tr" && cat "$O/rounds_$rest/round_cost.txt" >> "$log" ;;
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
