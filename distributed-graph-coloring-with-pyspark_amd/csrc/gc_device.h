@@ -77,8 +77,8 @@ __device__ __forceinline__ void gc_commit_colour_keep(GDev& g, int v, int cc) {
 
 // counters shared across workgroups: read with an atomic RMW, written agent-scope
 __device__ __forceinline__ ull gc_aread(ull* p) { return atomicAdd(p, 0ull); }
-template <typename T>
-__device__ __forceinline__ void gc_st(T* p, T v) {
+template <typename T>  // (host too: tests/host_close runs the round close on the CPU)
+__host__ __device__ __forceinline__ void gc_st(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
