@@ -1710,8 +1710,8 @@ __device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* 
     if (threadIdx.x >= GC_WAVE) return;
     const int lane = threadIdx.x;
 #if GC_CLOSE_BATCH
-    GcCloseCtl k{};
-    if (lane == 0) k = gc_close_load(c);  // in flight with the counter reads below
+    GcCloseCtl kc{};
+    if (lane == 0) kc = gc_close_load(c);  // in flight with the counter reads below
 #endif
     ull a = 0;  // the commit's slotted winner counts
     if (g.accs)
@@ -1733,7 +1733,7 @@ __device__ __forceinline__ void gc_close_body(GDev& g, const GLists& L, DevCtl* 
     pre.uncolored = (ull)__shfl((long long)x, 4, GC_WAVE);
     pre.fnext = (ull)__shfl((long long)x, 5, GC_WAVE);
 #if GC_CLOSE_BATCH
-    if (lane == 0) gc_close_batched(g, L, c, mode, allow_big, fused, pre, k);
+    if (lane == 0) gc_close_batched(g, L, c, mode, allow_big, fused, pre, kc);
 #else
     if (lane == 0) gc_close_interleaved(g, L, c, mode, allow_big, fused, pre);
 #endif
