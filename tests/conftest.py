@@ -7,6 +7,7 @@ import glob
 import gzip
 import json
 import os
+import socket
 import sys
 
 import numpy as np
@@ -25,6 +26,14 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
     config.addinivalue_line("markers", "gpu_staged: GPU test of an opt-in path not yet validated on the GPU "
                                        "(run with -m gpu_staged; promoted to gpu once green)")
+
+
+def free_port():
+    """A TCP port on 127.0.0.1 that was free a moment ago (the OS picks it): rendezvous ports
+    for the multi-process tests, instead of random ones that parallel workers can share."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def golden_names():

@@ -139,30 +139,30 @@ def test_async_resolve_rmat24_matches(monkeypatch):
 
 
 # --- the round closed by k_commit_big (GC_BIG_CLOSE=1: no k_close launch on graphs with big rows) ---
-B_ENVS = [{"GC_BIG_CLOSE": "1"}, {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8"}, {"GC_BIG_CLOSE": "1", "GC_HUB_T": "0"},
-          {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8", "GC_BATCH_MAX": "1"}]
-B_IDS = ["bclose", "bclose_row8", "bclose_nohub", "bclose_row8_batch1"]
+BC_ENVS = [{"GC_BIG_CLOSE": "1"}, {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8"}, {"GC_BIG_CLOSE": "1", "GC_HUB_T": "0"},
+           {"GC_BIG_CLOSE": "1", "GC_BIGROW": "8", "GC_BATCH_MAX": "1"}]
+BC_IDS = ["bclose", "bclose_row8", "bclose_nohub", "bclose_row8_batch1"]
 
 
-@pytest.fixture(params=B_ENVS, ids=B_IDS)
-def benv(request, monkeypatch):
+@pytest.fixture(params=BC_ENVS, ids=BC_IDS)
+def bcenv(request, monkeypatch):
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
     return request.param
 
 
-def test_big_close_generator_graphs(benv):
-    hubs.test_reference_generator_graphs(benv)
+def test_big_close_generator_graphs(bcenv):
+    hubs.test_reference_generator_graphs(bcenv)
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_big_close_directed(benv, seed):
-    hubs.test_directed_multigraphs(benv, seed)
+def test_big_close_directed(bcenv, seed):
+    hubs.test_directed_multigraphs(bcenv, seed)
 
 
 @pytest.mark.parametrize("scale", [9, 12])
-def test_big_close_rmat(benv, scale):
-    hubs.test_rmat(benv, scale)
+def test_big_close_rmat(bcenv, scale):
+    hubs.test_rmat(bcenv, scale)
 
 
 @pytest.mark.parametrize("bigrow", ["0", "8", "64"])
@@ -358,10 +358,10 @@ def test_hybrid_two_processes(tmp_path):
     """The hybrid as two processes over torch.distributed (gloo; both ranks on the one GPU):
     sharded rounds, the frontier parts all-gathered, each rank resuming its own engine."""
     import json
-    import random
     import torch
+    from conftest import free_port
     from gcolor_amd.engine import DeviceGraph
-    port = 33000 + random.randint(0, 2000)
+    port = free_port()
     torch.multiprocessing.spawn(_hybrid_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     with DeviceGraph.rmat(12, 16, seed=9) as dg:
         one = dg.color("A")

@@ -7,7 +7,6 @@ Results must equal the single-partition oracle bit for bit: LFMIS under the glob
 """
 import json
 import os
-import random
 import sys
 import threading
 
@@ -15,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
+from conftest import PKG_DIR, REPO, fixture_csr, free_port, golden_names, load_golden
 
 sys.path.insert(0, REPO)
 from oracle import oracle  # noqa: E402
@@ -266,7 +265,7 @@ def test_gloo_world_size_2(case, dense, inline, deferred_ops, switch_below, tmp_
     ids, adj, rp, col = fixture_csr(load_golden(case))
     path = str(tmp_path / "g.npz")
     np.savez(path, rp=rp, col=col)
-    port = 29500 + random.randint(0, 2000)
+    port = free_port()
     torch.multiprocessing.spawn(_gloo_worker,
                                 args=(2, port, path, str(tmp_path), dense, inline, deferred_ops, switch_below),
                                 nprocs=2, join=True)

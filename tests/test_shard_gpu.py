@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import PKG_DIR, REPO, fixture_csr, golden_names, load_golden
+from conftest import PKG_DIR, REPO, fixture_csr, free_port, golden_names, load_golden
 
 sys.path.insert(0, REPO)
 from oracle import oracle  # noqa: E402
@@ -225,7 +225,7 @@ def _gloo_gpu_worker(rank, world, port, out_dir):
 
 def test_two_processes_over_torch_distributed(tmp_path):
     from gcolor_amd.engine import DeviceGraph
-    port = 31000 + random.randint(0, 2000)
+    port = free_port()
     torch.multiprocessing.spawn(_gloo_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     with DeviceGraph.rmat(11, 16, seed=9) as dg:
         one = dg.color("A")
