@@ -38,3 +38,38 @@ def stage_overflow_case(K, leaves, n):
     expected = {"colors": final, "F": [K, K * leaves], "accepted": [K, K * leaves],
                 "U": [K + K * leaves, K * leaves]}
     return rp, col, colors, front, expected
+
+
+def _csr(n, src, dst):
+    order = np.lexsort((dst, src))
+    src, dst = src[order], dst[order]
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    return np.cumsum(rp), dst.astype(np.int32)
+
+
+def stage_overflow_tree(fanout, levels, n):
+    """The same corner from a plain colouring (no resume): a rooted tree -- the root with
+    fanout + 2 children, every other inner vertex with fanout children (degree fanout + 1, so
+    the root is the unique seed) -- padded with isolated vertices to n.  Round k's frontier is
+    level k + 1: every vertex wins (siblings are never adjacent) and claims its children, so a
+    wave holding a chunk of one level pushes chunk x fanout entries.  Vertex ids: the root 0,
+    then the levels in order.  Returns (rp, col, expected) with expected colours (level parity:
+    even levels and the isolated vertices 0, odd levels 1) and the per-round frontiers."""
+    sizes = [1, fanout + 2]
+    while len(sizes) < levels:
+        sizes.append(sizes[-1] * fanout)
+    starts = np.cumsum([0] + sizes)
+    assert starts[-1] <= n
+    src, dst = [], []
+    for lv in range(1, levels):
+        child = np.arange(starts[lv], starts[lv + 1], dtype=np.int64)
+        k = fanout + 2 if lv == 1 else fanout
+        parent = starts[lv - 1] + (child - starts[lv]) // k
+        src += [parent, child]
+        dst += [child, parent]
+    rp, col = _csr(n, np.concatenate(src), np.concatenate(dst))
+    colors = np.zeros(n, np.int32)
+    for lv in range(levels):
+        colors[starts[lv]:starts[lv + 1]] = lv & 1
+    return rp, col, {"colors": colors, "F": sizes[1:], "levels": sizes}

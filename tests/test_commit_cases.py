@@ -9,7 +9,7 @@ import pytest
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from commit_cases import stage_overflow_case  # noqa: E402
+from commit_cases import stage_overflow_case, stage_overflow_tree  # noqa: E402
 from shard_numpy import numpy_resume  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -26,3 +26,14 @@ def test_stage_overflow_case_expectation(K, leaves, n):
     assert list(res.round_F[:2]) == exp["F"] and list(res.round_accepted[:2]) == exp["accepted"]
     assert list(res.round_U[:2]) == exp["U"]
     assert tuple(oracle.c_validate(rp, col, res.colors)) == (0, 0)
+
+
+@pytest.mark.parametrize("fanout,levels,n", [(3, 4, 100), (5, 5, 5000), (61, 4, 300_000)])
+def test_stage_overflow_tree_expectation(fanout, levels, n):
+    rp, col, exp = stage_overflow_tree(fanout, levels, n)
+    deg = np.diff(rp)
+    assert deg[0] == fanout + 2 and deg.max() == fanout + 2 and (deg[1:] <= fanout + 1).all()
+    o = oracle.c_color(rp, col, "A")
+    assert o["status"] == 0 and np.array_equal(o["colors"], exp["colors"])
+    assert list(o["round_F"][:-1]) == exp["F"] and list(o["round_accepted"][:-1]) == exp["F"]
+    assert o["reseeds"] == 0

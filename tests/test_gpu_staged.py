@@ -279,6 +279,26 @@ def test_commit_stage_overflow_under_ticket_close(env, monkeypatch):
         assert dg.validate() == (0, 0)
 
 
+@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}, {"GC_ASYNC": "2"}], ids=["fused", "unfused", "async_nohub"])
+def test_commit_stage_overflow_tree(env, monkeypatch):
+    """The same corner from a plain colouring (no resume; tests/commit_cases.py): a fanout-61
+    tree padded to 2^26 vertices.  Round 2's frontier is its 234,423 level-3 vertices (< n/256:
+    a closing commit), 128 per busy wave x 61 claimed children = 7,808 pushes (15 mid-launch
+    flushes), while the 1,240 waves without a chunk take their tickets at once.  Candidate for
+    the default GPU suite once green (it runs the default path only)."""
+    from commit_cases import stage_overflow_tree
+    from gcolor_amd.engine import DeviceGraph
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rp, col, exp = stage_overflow_tree(61, 5, 1 << 26)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("A")
+        assert g.status == 0
+        assert list(g.round_F[:-1]) == exp["F"] and list(g.round_accepted[:-1]) == exp["F"]
+        assert np.array_equal(g.colors, exp["colors"])
+        assert dg.validate() == (0, 0)
+
+
 def test_resume_rejects_out_of_range_frontier():
     """A frontier entry outside [0, n) stops gc_color_resume before any round (GC_EINVAL)."""
     import torch
