@@ -1,0 +1,147 @@
+"""Model of the asynchronous Jones-Plassmann round (csrc/gc_kernels.hip k_sweep_async's light
+passes) -- TEST INFRASTRUCTURE.
+
+A round's resolution (coloring.py:56-70) is the LFMIS of the proposers under the rank
+(deg asc, pos asc): v keeps its candidate iff no LISTED neighbour of lower rank that kept the
+same candidate exists.  k_sweep_async evaluates it with no barrier: every wave owns a static
+slice of the undecided vertices and passes over its pending ones, each from its cursor (the
+first lower-rank same-candidate neighbour it found undecided), until none is left, reading
+the other waves' states as they happen to be.  A state only moves UND -> IN / OUT, so a
+stale read only ever shows UND.  This model runs those rules vertex by vertex under a seeded
+random interleaving of waves, with every read of another vertex's state taken, at random,
+from an older snapshot, and colours whole graphs round by round (init, seed, E1 re-seeds as
+oracle/gcolor_oracle.c).  tests/test_jp_model.py checks it equals the oracle's variant A bit
+for bit: "staleness delays a decision, never changes it", the argument DESIGN §5 makes for
+the asynchronous JP -- with and without hubs (GC_ASYNC=2 is the hub-less case).
+"""
+import random
+
+UND, IN, OUT = 0, 1, 2
+
+
+def _mex(s):
+    m = 0
+    while m in s:
+        m += 1
+    return m
+
+
+def _seed(n, deg, colour):
+    """oracle seed_vertex: the uncoloured vertex of largest degree, ties -> later."""
+    best = None
+    for v in range(n):
+        if colour[v] == -1 and (best is None or deg[v] >= deg[best]):
+            best = v
+    return best
+
+
+def _e1(n, adj, deg, colour):
+    """oracle e1_reseed: per component of the uncoloured-induced subgraph (listed edges,
+    either direction), its argmax (deg, pos) vertex gets colour 0.  Returns the seeds."""
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    for v in range(n):
+        if colour[v] != -1:
+            continue
+        for u in adj[v]:
+            if colour[u] != -1:
+                continue
+            a, b = find(v), find(u)
+            if a != b:
+                parent[max(a, b)] = min(a, b)
+    best = {}
+    for v in range(n):
+        if colour[v] == -1:
+            r = find(v)
+            if r not in best or deg[v] >= deg[best[r]]:
+                best[r] = v
+    return sorted(best.values())
+
+
+def jp_round(adj, rank, cand, props, rng, waves=5, stale=0.3, snap_every=3):
+    """One round's resolution over the proposers `props` as the asynchronous waves evaluate
+    it; returns the set that keeps its candidate."""
+    st = {v: UND for v in props}
+    # the lower-rank listed neighbours proposing the same candidate, in row order (the
+    # engine's rows list them first; a cursor resumes at the first one found undecided)
+    low = {v: [u for u in adj[v] if u in st and u != v and rank[u] < rank[v] and cand[u] == cand[v]] for v in props}
+    cur = {v: 0 for v in props}
+    snaps = [dict(st)]
+
+    def read(x):
+        return rng.choice(snaps)[x] if rng.random() < stale else st[x]
+
+    order = list(props)
+    slices = [order[i * len(order) // waves:(i + 1) * len(order) // waves] for i in range(waves)]
+    pending = [list(sl) for sl in slices]
+    steps = 0
+    while any(pending):
+        w = rng.choice([i for i in range(waves) if pending[i]])
+        v = pending[w].pop(0)
+        row, out, first = low[v], False, None
+        for i in range(cur[v], len(row)):
+            s = read(row[i])
+            if s == IN:
+                out = True
+                break
+            if s == UND and first is None:
+                first = i
+        if out:
+            st[v] = OUT
+        elif first is not None:
+            cur[v] = first
+            pending[w].append(v)
+        else:
+            st[v] = IN
+        steps += 1
+        if steps % snap_every == 0:
+            snaps.append(dict(st))
+            if len(snaps) > 6:
+                snaps.pop(1)
+        if steps > 200 * (len(props) + 1) ** 2:
+            raise RuntimeError("the JP model does not converge")
+    return {v for v in props if st[v] == IN}
+
+
+def model_color_a(rp, col, seed=0, waves=5, stale=0.3):
+    """Variant A (coloring.py), unbounded, E1 on, every round's resolution by jp_round.
+    Returns (colours, per-round (U, F, accepted, seeds))."""
+    rng = random.Random(seed)
+    n = len(rp) - 1
+    adj = [[int(u) for u in col[rp[v]:rp[v + 1]]] for v in range(n)]
+    deg = [len(a) for a in adj]
+    rank = {v: (deg[v], v) for v in range(n)}
+    colour = [0 if deg[v] == 0 else -1 for v in range(n)]
+    s = _seed(n, deg, colour)
+    if s is not None:
+        colour[s] = 0
+    recs = []
+    while True:
+        unc = [v for v in range(n) if colour[v] == -1]
+        if not unc:
+            recs.append((0, 0, 0, 0))
+            return colour, recs
+        cand, props = {}, []
+        for v in unc:
+            cs = {colour[u] for u in adj[v] if colour[u] >= 0}
+            if cs:
+                cand[v] = _mex(cs)
+                props.append(v)
+        if not props:  # E1 re-seed round
+            seeds = _e1(n, adj, deg, colour)
+            for x in seeds:
+                colour[x] = 0
+            recs.append((len(unc), 0, 0, len(seeds)))
+            continue
+        keep = jp_round(adj, rank, cand, props, rng, waves, stale)
+        for v in keep:
+            colour[v] = cand[v]
+        recs.append((len(unc), len(props), len(keep), 0))
+        if len(recs) > 4 * n + 16:
+            raise RuntimeError("round limit")
