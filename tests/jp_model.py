@@ -64,9 +64,13 @@ def _e1(n, adj, deg, colour):
     return sorted(best.values())
 
 
-def jp_round(adj, rank, cand, props, rng, waves=5, stale=0.3, snap_every=3):
+def jp_round(adj, rank, cand, props, rng, waves=5, stale=0.3, snap_every=3, hubs=frozenset()):
     """One round's resolution over the proposers `props` as the asynchronous waves evaluate
-    it; returns the set that keeps its candidate."""
+    it; returns the set that keeps its candidate.  With `hubs` (the hub JP, gc_hubs.hip):
+    the lights resolve first -- no light ever looks at a hub, every hub ranks above every
+    light -- and each light winner raises the kill flag of every hub that lists it and
+    proposes its colour; once every light has decided, a killed hub is OUT and the others
+    resolve among themselves the same way (their lower-rank listed hubs, stale reads)."""
     st = {v: UND for v in props}
     # the lower-rank listed neighbours proposing the same candidate, in row order (the
     # engine's rows list them first; a cursor resumes at the first one found undecided)
@@ -77,41 +81,58 @@ def jp_round(adj, rank, cand, props, rng, waves=5, stale=0.3, snap_every=3):
     def read(x):
         return rng.choice(snaps)[x] if rng.random() < stale else st[x]
 
-    order = list(props)
-    slices = [order[i * len(order) // waves:(i + 1) * len(order) // waves] for i in range(waves)]
-    pending = [list(sl) for sl in slices]
-    steps = 0
-    while any(pending):
-        w = rng.choice([i for i in range(waves) if pending[i]])
-        v = pending[w].pop(0)
-        row, out, first = low[v], False, None
-        for i in range(cur[v], len(row)):
-            s = read(row[i])
-            if s == IN:
-                out = True
-                break
-            if s == UND and first is None:
-                first = i
-        if out:
-            st[v] = OUT
-        elif first is not None:
-            cur[v] = first
-            pending[w].append(v)
-        else:
-            st[v] = IN
-        steps += 1
-        if steps % snap_every == 0:
-            snaps.append(dict(st))
-            if len(snaps) > 6:
-                snaps.pop(1)
-        if steps > 200 * (len(props) + 1) ** 2:
-            raise RuntimeError("the JP model does not converge")
+    def settle(order):
+        nonlocal snaps
+        slices = [order[i * len(order) // waves:(i + 1) * len(order) // waves] for i in range(waves)]
+        pending = [list(sl) for sl in slices]
+        steps = 0
+        while any(pending):
+            w = rng.choice([i for i in range(waves) if pending[i]])
+            v = pending[w].pop(0)
+            row, out, first = low[v], False, None
+            for i in range(cur[v], len(row)):
+                s = read(row[i])
+                if s == IN:
+                    out = True
+                    break
+                if s == UND and first is None:
+                    first = i
+            if out:
+                st[v] = OUT
+            elif first is not None:
+                cur[v] = first
+                pending[w].append(v)
+            else:
+                st[v] = IN
+            steps += 1
+            if steps % snap_every == 0:
+                snaps.append(dict(st))
+                if len(snaps) > 6:
+                    snaps.pop(1)
+            if steps > 200 * (len(props) + 1) ** 2:
+                raise RuntimeError("the JP model does not converge")
+
+    lights = [v for v in props if v not in hubs]
+    hub_props = [v for v in props if v in hubs]
+    settle(lights)
+    if hub_props:
+        # every light has decided (the hubs wait for the lights' counter): kill flags
+        killed = {x for x in hub_props if any(u in st and u not in hubs and st[u] == IN and cand[u] == cand[x]
+                                              for u in adj[x])}
+        for x in killed:
+            st[x] = OUT
+        # a hub's scan covers its lower-rank listed hubs only (hlow); lights are the flags' part
+        for x in hub_props:
+            low[x] = [u for u in low[x] if u in hubs]
+        snaps = [dict(st)]
+        settle([x for x in hub_props if x not in killed])
     return {v for v in props if st[v] == IN}
 
 
-def model_color_a(rp, col, seed=0, waves=5, stale=0.3):
-    """Variant A (coloring.py), unbounded, E1 on, every round's resolution by jp_round.
-    Returns (colours, per-round (U, F, accepted, seeds))."""
+def model_color_a(rp, col, seed=0, waves=5, stale=0.3, hub_t=None):
+    """Variant A (coloring.py), unbounded, E1 on, every round's resolution by jp_round
+    (hubs: deg > hub_t, None = no hub JP).  Returns (colours, per-round (U, F, accepted,
+    seeds))."""
     rng = random.Random(seed)
     n = len(rp) - 1
     adj = [[int(u) for u in col[rp[v]:rp[v + 1]]] for v in range(n)]
@@ -139,7 +160,8 @@ def model_color_a(rp, col, seed=0, waves=5, stale=0.3):
                 colour[x] = 0
             recs.append((len(unc), 0, 0, len(seeds)))
             continue
-        keep = jp_round(adj, rank, cand, props, rng, waves, stale)
+        hubs = frozenset(v for v in props if hub_t is not None and deg[v] > hub_t)
+        keep = jp_round(adj, rank, cand, props, rng, waves, stale, hubs=hubs)
         for v in keep:
             colour[v] = cand[v]
         recs.append((len(unc), len(props), len(keep), 0))

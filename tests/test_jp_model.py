@@ -55,3 +55,12 @@ def test_jp_model_dense_conflicts(seed):
     """Few candidates, long same-candidate chains: the deepest JP chains per round."""
     rp, col = _random_directed(80, 1600, 200 + seed)
     _same(rp, col, seed=seed, waves=6, stale=0.8)
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("hub_t", [0, 4, 9])
+def test_jp_model_hub_jp(seed, hub_t):
+    """The hub JP: lights first, light winners kill the hubs listing them that propose their
+    colour, then the hubs resolve among themselves -- under stale reads, against the oracle."""
+    rp, col = _random_directed(150, 900, 300 + seed)
+    _same(rp, col, seed=seed, waves=5, stale=0.6, hub_t=hub_t)
