@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 
 #include "gc_engine.h"
 
@@ -439,7 +440,83 @@ struct Run {
             kt.end();
         }
     }
+    // GC_GRAPHS=1 (staged, round 3): each round's launch sequence is captured once per shape
+    // into a hipGraph and replayed -- a round enqueues one graph launch instead of ~7 kernel
+    // launches.  The shape is everything the sequence depends on (sweeps, whether the last
+    // commit proposed, the re-sort / nibble hints, the tail, the asynchronous JP's launch
+    // parity, the snapshot slot); the host state a round changes is re-applied on replay.
+    // Off with kernel timing or GC_DEBUG_SYNC (they need the per-launch host calls).
+    struct GKey {
+        int S, proposed, resort, c4, skip_tail, par;
+        const DevCtl* snap;
+        bool operator<(const GKey& o) const {
+            const long long a[7] = {S, proposed, resort, c4, skip_tail, par, (long long)(intptr_t)snap};
+            const long long b[7] = {o.S, o.proposed, o.resort, o.c4, o.skip_tail, o.par, (long long)(intptr_t)o.snap};
+            return std::lexicographical_compare(a, a + 7, b, b + 7);
+        }
+    };
+    struct GEntry {
+        hipGraphExec_t ex;
+        long long launches[GC_NKERNELS];  // the kernel-class counts one replay adds to the stats
+    };
+    std::map<GKey, GEntry> graphs;
+    bool graphs_on = getenv("GC_GRAPHS") && atoi(getenv("GC_GRAPHS")) > 0;
+    ~Run() {
+        for (auto& kv : graphs) hipGraphExecDestroy(kv.second.ex);
+    }
     void enqueue_round(int S) {
+        if (!graphs_on || kt.mask || kt.dbg_sync) {
+            enqueue_round_direct(S);
+            return;
+        }
+        const GKey key{S, proposed ? 1 : 0, resort_hint ? 1 : 0, c4_hint ? 1 : 0, skip_tail ? 1 : 0, async_par, snap_ptr};
+        auto it = graphs.find(key);
+        if (it == graphs.end()) {  // capture this shape (the host state moves as in a direct round)
+            long long before[GC_NKERNELS] = {};
+            if (st)
+                for (int k = 0; k < GC_NKERNELS; ++k) before[k] = st->k_launches[k];
+            const bool proposed0 = proposed;
+            const int par0 = async_par;
+            DevCtl* const snap0 = snap_ptr;
+            hipGraph_t gr = nullptr;
+            GEntry e{};
+            hipError_t err = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
+            if (err == hipSuccess) {
+                enqueue_round_direct(S);
+                const hipError_t e2 = hipStreamEndCapture(s, &gr);
+                err = e2;
+            }
+            if (err == hipSuccess) err = hipGraphInstantiate(&e.ex, gr, nullptr, nullptr, 0);
+            if (gr) hipGraphDestroy(gr);
+            if (err != hipSuccess) {  // nothing of the round ran: restore the host state, go direct
+                fprintf(stderr, "[gc] GC_GRAPHS: capture failed (%s); graphs off\n", hipGetErrorString(err));
+                graphs_on = false;
+                (void)hipGetLastError();
+                proposed = proposed0;
+                async_par = par0;
+                snap_ptr = snap0;
+                if (st)
+                    for (int k = 0; k < GC_NKERNELS; ++k) st->k_launches[k] = before[k];
+                enqueue_round_direct(S);
+                return;
+            }
+            if (st)
+                for (int k = 0; k < GC_NKERNELS; ++k) e.launches[k] = st->k_launches[k] - before[k];
+            it = graphs.emplace(key, e).first;
+            hipGraphLaunch(e.ex, s);
+            return;
+        }
+        // replay, and the host side of enqueue_round_direct for this shape
+        const bool fuse = fuse_now();
+        const bool tail = async_first || S > 0 || !skip_tail;
+        hipGraphLaunch(it->second.ex, s);
+        if (st)
+            for (int k = 0; k < GC_NKERNELS; ++k) st->k_launches[k] += it->second.launches[k];
+        if (tail && async_grid > 0) async_par ^= 1;
+        snap_ptr = nullptr;
+        proposed = fuse;
+    }
+    void enqueue_round_direct(int S) {
         const bool fuse = fuse_now();
         if (!proposed) enqueue_propose();
         if (async_first) {  // k_sweep_async makes the first sweep too

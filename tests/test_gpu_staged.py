@@ -19,7 +19,9 @@ import numpy as np
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import test_gpu_variant_b as vb  # noqa: E402
+from oracle import oracle  # noqa: E402
 
 # selected only by `-m gpu_staged` with GC_RUN_STAGED=1 (the CPU suite's -m "not gpu" skips them)
 pytestmark = [pytest.mark.gpu_staged,
@@ -182,6 +184,60 @@ def test_big_close_rmat24_matches(monkeypatch):
         for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
             assert list(getattr(g, k)) == list(getattr(ref, k)), k
         assert dg.validate() == (0, 0)
+
+
+# --- each round's launches captured once per shape in a hipGraph and replayed (GC_GRAPHS=1) ---
+G_ENVS = [{"GC_GRAPHS": "1"}, {"GC_GRAPHS": "1", "GC_BATCH_MAX": "1"}, {"GC_GRAPHS": "1", "GC_ASYNC": "0"},
+          {"GC_GRAPHS": "1", "GC_HUB_T": "off"}, {"GC_GRAPHS": "1", "GC_ASYNC_BUDGET_US": "0"}]
+G_IDS = ["graphs", "graphs_batch1", "graphs_sync_jp", "graphs_nohub", "graphs_abort"]
+
+
+@pytest.fixture(params=G_ENVS, ids=G_IDS)
+def genv(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_graphs_generator_graphs(genv):
+    hubs.test_reference_generator_graphs(genv)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_graphs_directed(genv, seed):
+    hubs.test_directed_multigraphs(genv, seed)
+
+
+@pytest.mark.parametrize("scale", [9, 12])
+def test_graphs_rmat(genv, scale):
+    hubs.test_rmat(genv, scale)
+
+
+def test_graphs_uniform_and_mesh(genv):
+    """Hub-less graphs: fused and closing commits, the big-round rebuild, E1 on the generator."""
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    rp, col = uniform_csr(300_000, 16, 7)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        o = oracle.c_color(rp, col, "A")
+        g = dg.color("A")
+        assert np.array_equal(g.colors, o["colors"]) and list(g.round_U) == list(o["round_U"])
+    with DeviceGraph.mesh(40, 32, 24) as dg:
+        rp, col = dg.export()
+        o = oracle.c_color(rp, col, "A")
+        g = dg.color("A")
+        assert np.array_equal(g.colors, o["colors"]) and list(g.round_U) == list(o["round_U"])
+
+
+def test_graphs_rmat24_matches(monkeypatch):
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(24, 16, seed=1) as dg:
+        ref = dg.color("A")
+        monkeypatch.setenv("GC_GRAPHS", "1")
+        g = dg.color("A")
+        assert np.array_equal(g.colors, ref.colors)
+        for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
+            assert list(getattr(g, k)) == list(getattr(ref, k)), k
+        print(f"R-MAT-24 device ms: direct {ref.device_ms:.1f}, graphs {g.device_ms:.1f}")
 
 
 # --- gc_color_resume and the multi-GPU hybrid -----------------------------------------------
