@@ -405,6 +405,15 @@ def scaled_workload(w, world, scaling):
     return w
 
 
+def replica_workload(w, world, rank):
+    """--multi replicas: rank `rank`'s own base-size graph (seed + rank: independent colourings)."""
+    w = scaled_workload(w, 1, "strong")
+    if "seed" in w:
+        w["seed"] += rank
+    w["desc"] += f" (one per GPU, seed + rank, {world} independent colourings)"
+    return w
+
+
 def sharded_graph(w, world, scaling):
     from gcolor_amd.engine import DeviceGraph, uniform_csr
     w = dict(w)
@@ -526,9 +535,11 @@ def main():
                     help="N > 1: weak grows the graph with N, strong keeps the workload's graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--multi", default="replicated", choices=["replicated", "sharded", "hybrid"],
+    ap.add_argument("--multi", default="replicated", choices=["replicated", "replicas", "sharded", "hybrid"],
                     help="N>1: replicated (default) -- every rank runs the one-GPU engine on the whole graph, no "
-                         "exchange, the job's time is the slowest rank's; sharded -- one graph cut into vertex-range "
+                         "exchange, the job's time is the slowest rank's; replicas -- N independent colourings, one "
+                         "base-size graph per rank (seed + rank), value = all ranks' edges / the slowest rank's time "
+                         "(throughput of many graphs, not of one); sharded -- one graph cut into vertex-range "
                          "shards with round seams over RCCL (gcolor_amd.shard; slower than one GPU, DESIGN.md §7); "
                          "hybrid -- sharded rounds while the frontier is large, then every rank resumes the one-GPU "
                          "engine from the replicated state (gcolor_amd.shard.hybrid_color)")
@@ -582,7 +593,9 @@ def main():
 
     from gcolor_amd import _native
     _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
-    w = scaled_workload(WORKLOADS[args.workload], world, args.scaling)
+    replicas = world > 1 and args.multi == "replicas"
+    w = replica_workload(WORKLOADS[args.workload], world, rank) if replicas else \
+        scaled_workload(WORKLOADS[args.workload], world, args.scaling)
     V = args.variant
     # north_star N1 modes (variant A only): seeded priorities / speculative first-fit
     mode = {"priority": args.priority_seed, "speculative": args.speculative}
@@ -615,10 +628,15 @@ def main():
     # HIP events on the engine's own stream (the roofline's launch durations).
     t, kern, r, phases = S.steps(args.steps, None, roctx=True)
     rounds, sweeps, reseeds, colours = r.rounds, r.jp_sweeps, r.reseeds, r.num_colors
+    m_all = m  # edges coloured per step by the whole job
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
+        if replicas:  # every rank coloured its own graph
+            mm = torch.tensor([float(m)], dtype=torch.float64, device="cuda")
+            dist.all_reduce(mm, op=dist.ReduceOp.SUM)
+            m_all = float(mm.item())
     t_ev = None
     if not args.no_event_timing:
         t_ev, kern, _, _ = S.steps(args.steps, dom_class)
@@ -674,7 +692,7 @@ def main():
     classes = class_table(probe.kernels, pmc)
     line = {
         "metric": METRIC,
-        "value": m / t,
+        "value": m_all / t,
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -688,8 +706,10 @@ def main():
         "config": {"workload": w["desc"], "n": info["n"], "m_undirected": m, "nnz": info["nnz"],
                    "max_degree": info["max_degree"], "variant": "A (coloring.py)" if V == "A" else
                    "B (coloring_optimized.py)",
-                   "parallelism": (f"replicated: each of the {world} ranks runs the one-GPU engine on the whole graph, "
-                                   "no exchange (the rounds are a latency chain: DESIGN.md §7); time = slowest rank")
+                   "parallelism": ((f"replicas: {world} independent colourings, one graph per rank, no exchange; "
+                                    "value = all ranks' edges / the slowest rank's time") if replicas else
+                                   (f"replicated: each of the {world} ranks runs the one-GPU engine on the whole graph, "
+                                    "no exchange (the rounds are a latency chain: DESIGN.md §7); time = slowest rank"))
                                   if world > 1 else "single",
                    "rank": ("(deg, pos) (coloring.py:64)" if args.priority_seed is None
                             else f"prio_hash(seed={args.priority_seed}, v), pos"),

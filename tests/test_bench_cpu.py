@@ -41,3 +41,11 @@ def test_capped_credit():
     kern = {"propose": {"bytes": 1e12, "ms": 10.0, "launches": 1}, "commit": {"bytes": 1e9, "ms": 10.0, "launches": 1}}
     cap = bench.capped_alg(kern, n=0, nnz=0)
     assert cap == 10e-3 * bench.HBM_PEAK_GBS * 1e9 + 1e9
+
+
+def test_replica_workload():
+    w = bench.WORKLOADS["rmat24"]
+    r3 = bench.replica_workload(w, 8, 3)
+    assert r3["scale"] == 24 and r3["seed"] == w["seed"] + 3 and "8 independent colourings" in r3["desc"]
+    assert bench.replica_workload(bench.WORKLOADS["mesh512"], 4, 2)["dims"] == (512, 512, 512)
+    assert w["seed"] == 1  # the table is not modified
