@@ -2459,8 +2459,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_apply(GDev g, int kind, const long
                     // another rank's light winner flags the hubs that list it and propose its
                     // colour, as a local one does in its sweep (gc_jp_sweep)
                     const int cv = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
-                    for (long long e = g.hin_rp[v]; e < g.hin_rp[v + 1]; ++e) {
-                        const int hx = g.hin_col[e];
+                    for (long long q = g.hin_rp[v]; q < g.hin_rp[v + 1]; ++q) {
+                        const int hx = g.hin_col[q];
                         if ((g.hk[hx] >> 2) == (unsigned)cv && !g.hkill[hx]) g.hkill[hx] = 1u;
                     }
                 }

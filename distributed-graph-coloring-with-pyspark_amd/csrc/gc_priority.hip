@@ -199,11 +199,15 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
             return GC_ENOMEM;
         }
         int rc = gc_partition(g, g->col, tmp, prio, seed, &g->ctl->conflicts);
-        if (rc == GC_OK) hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
+        hipError_t ec = hipSuccess;
+        if (rc == GC_OK) ec = hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);
         const hipError_t e = hipStreamSynchronize(s);
         gc_dfree(tmp);
         if (rc) return rc;
-        if (e != hipSuccess || hipGetLastError() != hipSuccess) { gc_set_error("row re-partition failed"); return GC_EHIP; }
+        if (ec != hipSuccess || e != hipSuccess || hipGetLastError() != hipSuccess) {
+            gc_set_error("row re-partition failed");
+            return GC_EHIP;
+        }
         // the in-neighbour lists of an asymmetric graph are sets: their order is unaffected
     }
     g->part_prio = prio;

@@ -168,8 +168,8 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     if (!rc) {  // hub lists on the parent (once), a bitmap replica (+ hub JP state) for this shard
         GDev pd = gc_view(g);
         rc = gc_hubs_prepare(g, pd);
-        const char* e = getenv("GC_SHARD_HUBS");
-        const bool want_repl = !(e && *e && atoi(e) == 0);
+        const char* env = getenv("GC_SHARD_HUBS");
+        const bool want_repl = !(env && *env && atoi(env) == 0);
         if (!rc && g->nhub > 0 && want_repl && g->hub_t >= 0) {  // every deg > hub_t vertex is a hub
             sh->parent = g;
             sh->hub_w = g->hub_w;
