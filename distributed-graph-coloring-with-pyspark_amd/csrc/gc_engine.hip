@@ -411,7 +411,7 @@ struct Run {
         DevCtl* snap = mode == GC_CM_ROUND ? snap_ptr : nullptr;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
         gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0, tclose ? snap : nullptr,
-                   tclose ? 1 : 0, bclose ? snap : nullptr, bclose ? 1 : 0);
+                   tclose ? 1 : 0, bclose ? snap : nullptr, bclose ? 1 : 0, mode == GC_CM_ROUND && !resort_hint ? 1 : 0);
         kt.end();
         if (mode == GC_CM_ROUND) snap_ptr = nullptr;
         if (tclose || bclose) {
@@ -524,7 +524,7 @@ struct Run {
             return;
         }
         kt.begin(GC_K_RESOLVE);
-        gcl_resolve(d, L, s);
+        gcl_resolve(d, L, s, resort_hint ? 0 : 1);
         kt.end();
         launch_sweeps(1, S);
         launch_commit(GC_CM_ROUND, S, fuse);

@@ -3022,6 +3022,11 @@ static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 // 216 -> 210 ms with the later sweeps on 256; the full grid stays for C2's big rounds)
 static const int kGridPS = round_grid("GC_GRID_PS", 512);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
+// GC_GRID_SMALL=N (staged, round 3; 0 = off): k_resolve, k_commit and k_commit_big on at most
+// N workgroups when the last snapshot's frontier was small (< n/256, as kGridPS) -- a small
+// round's 768-1024 mostly idle workgroups still cost their dispatch and end-of-kernel work
+static const int kGridSmall = round_grid("GC_GRID_SMALL", 0);
+static int small_grid(int dflt, int small) { return small && kGridSmall > 0 && kGridSmall < dflt ? kGridSmall : dflt; }
 static const int kGridC = round_grid("GC_GRID_C", 768);  // mesh 512^3 111 -> 106 ms (1024 -> 768; 1536: 158), R-MAT and C2 alike
 static const int kGridPB = round_grid("GC_GRID_PB", GC_BLOCK_GRID);  // k_propose_block
 static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit_big
@@ -3058,8 +3063,8 @@ void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small) {
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
-void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve, dim3(g.heavy_wg ? kGridRH : kGridR), dim3(GC_BLOCK), 0, s, g, L);
+void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s, int small) {
+    hipLaunchKernelGGL(k_resolve, dim3(small_grid(g.heavy_wg ? kGridRH : kGridR, small)), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep, dim3(g.heavy_wg ? kGridSH : kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
@@ -3157,15 +3162,16 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused,
-                DevCtl* snap, int tclose, DevCtl* bsnap, int bclose) {
+                DevCtl* snap, int tclose, DevCtl* bsnap, int bclose, int small) {
+    const int gc = small_grid(kGridC, small);
     if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
-        hipLaunchKernelGGL(k_commit<1>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap,
-                           tclose);
+        hipLaunchKernelGGL(k_commit<1>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
         return;
     }
-    hipLaunchKernelGGL(k_commit<0>, dim3(kGridC), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
+    hipLaunchKernelGGL(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big, bsnap, bclose);
+        hipLaunchKernelGGL(k_commit_big, dim3(small_grid(kGridCB, small)), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big,
+                           bsnap, bclose);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

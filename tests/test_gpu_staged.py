@@ -240,6 +240,50 @@ def test_graphs_rmat24_matches(monkeypatch):
         print(f"R-MAT-24 device ms: direct {ref.device_ms:.1f}, graphs {g.device_ms:.1f}")
 
 
+# --- small rounds on capped grids (GC_GRID_SMALL: resolve / commit / commit_big) ------------
+S_ENVS = [{"GC_GRID_SMALL": "64"}, {"GC_GRID_SMALL": "1"}, {"GC_GRID_SMALL": "8", "GC_BIG_CLOSE": "1"},
+          {"GC_GRID_SMALL": "8", "GC_HUB_T": "off", "GC_FUSE": "0"}]
+S_IDS = ["small64", "small1", "small8_bclose", "small8_nohub_unfused"]
+
+
+@pytest.fixture(params=S_ENVS, ids=S_IDS)
+def senv(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_small_grid_generator_graphs(senv):
+    hubs.test_reference_generator_graphs(senv)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_small_grid_directed(senv, seed):
+    hubs.test_directed_multigraphs(senv, seed)
+
+
+@pytest.mark.parametrize("scale", [9, 12])
+def test_small_grid_rmat(senv, scale):
+    hubs.test_rmat(senv, scale)
+
+
+def test_small_grid_uniform_and_mesh(senv):
+    test_graphs_uniform_and_mesh(senv)
+
+
+def test_small_grid_rmat24_matches(monkeypatch):
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(24, 16, seed=1) as dg:
+        ref = dg.color("A")
+        for grid in ("128", "256"):
+            monkeypatch.setenv("GC_GRID_SMALL", grid)
+            g = dg.color("A")
+            assert np.array_equal(g.colors, ref.colors)
+            for k in ("round_U", "round_F", "round_maxmex", "round_accepted", "round_seeds"):
+                assert list(getattr(g, k)) == list(getattr(ref, k)), k
+            print(f"R-MAT-24 device ms: default grids {ref.device_ms:.1f}, GC_GRID_SMALL={grid} {g.device_ms:.1f}")
+
+
 # --- gc_color_resume and the multi-GPU hybrid -----------------------------------------------
 import test_shard_gpu as sg  # noqa: E402
 

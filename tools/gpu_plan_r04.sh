@@ -5,7 +5,7 @@
 #   a: the default build -- GPU tests, smoke, the ticket-close corner (default path first), the
 #      bench line, the launch-gap microbenchmark and the per-round cost by frontier size
 #   b: staged paths I (resume / hybrid, k_commit_big closing the round, rounds replayed as hipGraphs)
-#   c: staged paths II (variant B's asynchronous fold, the asynchronous first sweep)
+#   c: staged paths II (variant B's asynchronous fold, the asynchronous first sweep, small-round grids)
 #   d: per-graph pass timing, the combined variant through the hub and parity suites, step
 #      timings; the hubs-off asynchronous JP (the path that faulted in round 3) last
 set -uo pipefail
@@ -13,7 +13,7 @@ cd "$(dirname "$0")/.."
 case ${1:-} in
   a) exec_steps=(tests smoke staged:overflow_tree staged:under_ticket_close bench:rmat24 ubench:launch_gap rounds:rmat24) ;;
   b) exec_steps=("staged:resume~or~hybrid" staged:big_close staged:test_graphs_) ;;
-  c) exec_steps=(staged:b_async staged:async_resolve) ;;
+  c) exec_steps=(staged:b_async staged:async_resolve staged:small_grid) ;;
   d) exec_steps=(env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING= env:GC_LIB_PATH=build_variants/all4/libgcolor.so
                  file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py step:rmat26 step:rmat24 step:mesh512
                  env:GC_LIB_PATH= staged:async_jp_without_hubs) ;;
