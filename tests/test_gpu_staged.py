@@ -1,16 +1,21 @@
 """Staged GPU tests (marker gpu_staged, NOT selected by -m gpu): opt-in paths written in a
 round whose GPU access had closed, to be run with `pytest -m gpu_staged` on the next box and
-promoted to `gpu` once green.
+promoted to `gpu` once green (tools/gpu_plan_r04.sh runs them in order).
+Run: GC_RUN_STAGED=1 python -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v [-k GROUP]
 
-* Variant B's asynchronous fold (GC_B_ASYNC=1, csrc/gc_variant_b.hip k_b_async): every
-  variant-B parity case of tests/test_gpu_variant_b.py, with the normal budget and with a zero
-  budget (every launch hands its items back to the host's passes).
-Run: GC_RUN_STAGED=1 python -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v
-* The asynchronous JP without hubs (GC_ASYNC=2): the uniform / mesh / directed cases that
+* b_async: variant B's asynchronous fold (GC_B_ASYNC=1, k_b_async) on every variant-B parity
+  case of tests/test_gpu_variant_b.py, with the normal budget and a zero one.
+* async_jp_without_hubs: the asynchronous JP on hub-less graphs (GC_ASYNC=2), the path that
   faulted at 10M vertices in round 3, small first, then C2.
-* The multi-GPU hybrid (gcolor_amd.shard.hybrid_color): gc_color_resume from the state at a
-  round start, against the uninterrupted run; sharded rounds then the one-GPU engine, against
-  one GPU.
+* async_resolve: the round's first JP sweep inside k_sweep_async (GC_ASYNC_RESOLVE=1).
+* big_close: k_commit_big closes the round (GC_BIG_CLOSE=1).
+* test_graphs_: each round's launches replayed as a hipGraph (GC_GRAPHS=1).
+* small_grid: small rounds' resolve / commit grids capped (GC_GRID_SMALL).
+* overflow_tree / under_ticket_close: the closing commit's mid-launch flush corner (the fault's
+  cause), from a plain colouring and from a resumed state.
+* resume / hybrid: gc_color_resume from the state at a round start, against the uninterrupted
+  run; sharded rounds then the one-GPU engine (threads and two processes), against one GPU.
+* validate_c8: the validation from the byte mirror (GC_VALIDATE_C8=1).
 """
 import os
 import sys
