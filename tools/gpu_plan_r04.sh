@@ -12,7 +12,7 @@ set -uo pipefail
 cd "$(dirname "$0")/.."
 case ${1:-} in
   a) exec_steps=(tests smoke staged:overflow_tree staged:under_ticket_close bench:rmat24 ubench:launch_gap rounds:rmat24) ;;
-  b) exec_steps=("staged:resume~or~hybrid" staged:big_close staged:test_graphs_) ;;
+  b) exec_steps=("staged:resume~or~hybrid" staged:validate_c8 staged:big_close staged:test_graphs_) ;;
   c) exec_steps=(staged:b_async staged:async_resolve staged:small_grid) ;;
   d) exec_steps=(env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING= env:GC_LIB_PATH=build_variants/all4/libgcolor.so
                  file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py step:rmat26 step:rmat24 step:mesh512
