@@ -80,6 +80,7 @@ struct gc_graph {
     bool borrowed = false;     // rp/col/deg/nlow belong to another handle (shard views)
     bool own_stream = true;    // false: the caller's stream (gc_shard_set_stream), not destroyed here
     int shard_refs = 0;        // live shards borrowing this graph's rows and hub lists (gc_shard_create)
+    bool destroy_pending = false;  // gc_graph_destroy ran while shards lived: the last gc_shard_destroy frees it
     int part_prio = 0;         // rank the rows are partitioned for (gc_set_priority)
     int hub_prio = 0;          // row partition the hub lists were built under
     uint64_t hub_seed = 0;

@@ -723,6 +723,7 @@ struct Run {
             gc_set_error("unexpected device halt code %d", halt);
             return GC_EHIP;
         }
+        if (h.loop_err == GC_LERR_LIST) { gc_set_error("a work-list append passed the list's capacity (round %lld)", h.round); return GC_EHIP; }
         if (h.loop_err == 2) { gc_set_error("k_sweep_async: undecided list count out of range"); return GC_EHIP; }
         if (h.loop_err == 4) { gc_set_error("gc_color_resume: a frontier entry is out of range"); return GC_EINVAL; }
         if (h.loop_err == 3) {
@@ -845,6 +846,10 @@ extern "C" int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t
         gc_set_error("gc_color_resume: bad argument");
         return GC_EINVAL;
     }
+    // the caller's device buffers may still be being written on another stream (torch's):
+    // the library's own stream is non-blocking, so order its first read after them
+    GC_HIP(hipSetDevice(g->device));
+    GC_HIP(hipDeviceSynchronize());
     const ResumeArgs rs{colors_dev, cround_dev, front_dev, (long long)nfront, (long long)round0};
     return color_impl(g, opt, colors_out, cround_out, stats, &rs);
 }

@@ -372,6 +372,9 @@ extern "C" int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64
 extern "C" int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                                       uint32_t flags, gc_graph** out) {
     if (!d_row_ptr || (nnz > 0 && !d_col)) { gc_set_error("gc_graph_create_device: null input"); return GC_EINVAL; }
+    // the caller's CSR may still be being written on another stream (torch's); the library's
+    // stream is non-blocking, so its first read is ordered after all work on the device
+    GC_HIP(hipDeviceSynchronize());
     gc_graph* g;
     int rc = new_graph(out, n, nnz, flags, &g);
     if (rc) return rc;
@@ -490,8 +493,15 @@ extern "C" int gc_graph_create_rmat(int32_t scale, int32_t edge_factor, double a
     return rc;
 }
 
+// A graph with live shards (gc_shard_create borrows its rows and hub lists) is freed by the
+// last gc_shard_destroy instead: freeing it here would leave the shards reading memory the
+// caching allocator may already have handed to another graph.
 extern "C" void gc_graph_destroy(gc_graph* g) {
     if (!g) return;
+    if (g->shard_refs > 0) {
+        g->destroy_pending = true;
+        return;
+    }
     gc_free_all(g);
     delete g;
 }

@@ -239,9 +239,15 @@ __device__ __forceinline__ int gc_vpw(long long cnt, long long waves) {
 
 // Per-wave append staging in LDS: one global atomic per GC_STAGE_CAP entries instead of
 // one per wave-instruction (a single counter saturates at ~88 returning atomics/us).
+// Every list a stage flushes into holds `cap` entries (int32[n]); a flush whose base + count
+// would pass it writes nothing and sets DevCtl.loop_err = GC_LERR_LIST, which the host
+// reports as GC_EHIP: a wrong base becomes a reported error, never an aperture fault.
+#define GC_LERR_LIST 5
 struct GcStage {
     int* buf;
     int cnt;  // wave-uniform
+    long long cap;  // entries of the destination list
+    int* err;       // DevCtl.loop_err
 };
 
 // A commit that closes its own round (k_commit with tclose) counts arrivals in the high bits
@@ -251,14 +257,23 @@ struct GcStage {
 #define GC_TICKET_SHIFT 40
 #define GC_COUNT_MASK ((1ull << GC_TICKET_SHIFT) - 1ull)
 
+// the bound of one wave's flush (base and count wave-uniform): false = overflow, reported
+__device__ __forceinline__ bool gc_stage_fits(const GcStage& s, ull base) {
+    if (base + (ull)s.cnt <= (ull)s.cap) return true;
+    if (gc_lane() == 0) __hip_atomic_store(s.err, GC_LERR_LIST, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+
 __device__ __forceinline__ void gc_stage_flush(GcStage& s, int* out, ull* out_cnt) {
     gc_wave_sync();
     if (s.cnt == 0) return;
     ull base = 0;
     if (gc_lane() == 0) base = atomicAdd(out_cnt, (ull)s.cnt) & GC_COUNT_MASK;
     base = __shfl(base, 0, GC_WAVE);
+    if (gc_stage_fits(s, base)) {
 #pragma unroll 1
-    for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+        for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+    }
     gc_wave_sync();
     s.cnt = 0;
 }
@@ -282,8 +297,10 @@ __device__ __forceinline__ void gc_stage_flush_block(GcStage& s, int* out, ull* 
     __syncthreads();
     ull base = s_base;
     for (int i = 0; i < w; ++i) base += (ull)s_cnt[i];
+    if (gc_stage_fits(s, base)) {
 #pragma unroll 1
-    for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+        for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+    }
     gc_wave_sync();
     s.cnt = 0;
     __syncthreads();

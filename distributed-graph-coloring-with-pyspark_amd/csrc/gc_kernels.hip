@@ -869,10 +869,10 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     const unsigned char* __restrict__ k8 = g.k8;
     // undecided appends staged in LDS: one atomic per 512 entries, not one per wave-chunk
     // (a single counter takes ~88 returning atomics/us; 86k chunks cost ~1 ms)
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     // heavy vertices first.  Hubs off: a workgroup each, undecided ones staged by wave 0
     __shared__ int s_hstage[GC_STAGE_CAP];
-    GcStage hst{s_hstage, 0};
+    GcStage hst{s_hstage, 0, g.n, &g.ctl->loop_err};
     long long* const hdout = g.hub_repl ? nullptr : dout;  // replicated hubs (shards) are never sent
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
         // a wave's hubs are i = wid + j * waves; lane l loads the state of hub j0 + l, so a
@@ -1778,8 +1778,10 @@ __device__ __forceinline__ bool gc_stage_flush_ticket(GcStage& s, int* out, ull*
     __syncthreads();
     ull base = s_base;
     for (int i = 0; i < w; ++i) base += (ull)s_cnt[i];
+    if (gc_stage_fits(s, base)) {
 #pragma unroll 1
-    for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+        for (int i = gc_lane(); i < s.cnt; i += GC_WAVE) out[base + i] = s.buf[i];
+    }
     s.cnt = 0;
     *fnext = s_fin;
     return s_last != 0;
@@ -1908,12 +1910,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     ull* next_cnt = &c->fcnt[nxt];
     const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);  // next list: k_front_*
     const bool mark = big && !gc_pull_on(c);                              // else k_pull claims
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
 #if GC_CHECKS
     if (cnt > g.n || hcnt > g.n || (long long)(*next_cnt & GC_COUNT_MASK) > g.n) {
-        if (threadIdx.x == 0) gc_dbg(c, 10 + mode, cnt, hcnt, (long long)*next_cnt);
+        // this workgroup takes no arrival ticket, so no closing workgroup would write the
+        // snapshot: halt the pipeline and write it here (loop_err 3 is in it)
+        if (threadIdx.x == 0) {
+            gc_dbg(c, 10 + mode, cnt, hcnt, (long long)*next_cnt);
+            __hip_atomic_store(&c->halt, GC_H_STALLED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tclose && snap) gc_snap_copy(c, snap);
         return;
     }
 #endif
@@ -2236,7 +2244,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
     const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);
     const bool mark = big && !gc_pull_on(c);
     const bool walk_t = mark || !big;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long j0 = 0; j0 < nb; j0 += GC_BLOCK) {
         const int tn = (int)(nb - j0 < GC_BLOCK ? nb - j0 : GC_BLOCK);
@@ -2491,7 +2499,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_list_commit(GDev g, GLists L
     ull* next_cnt = &c->fcnt[nxt];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     long long lmaxc = -1;
     ull lacc = 0;
     const long long cnt = (long long)c->rwin_cnt;
@@ -2558,7 +2566,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
     ull* next_cnt = &c->fcnt[nxt];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     long long lmaxc = -1;
     ull lacc = 0;
     const long long n = g.n;
@@ -2700,7 +2708,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_claim(GDev g, GLists L, 
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
     const int slot = slot_next ? (c->cur ^ 1) : c->cur;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const long long H = g.nhub_repl;
     const long long steps = (H + GC_WAVE - 1) / GC_WAVE;
     for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
@@ -2764,7 +2772,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_unc_compact(GDev g, int* list, ull
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v - lane < g.n; v += stride) {
         const bool u = v < g.n && g.c8[v] == GC_C8_NONE;

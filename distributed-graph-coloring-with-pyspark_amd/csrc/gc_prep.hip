@@ -868,32 +868,64 @@ int prep_grid(const gc_graph* g) {
 
 }  // namespace
 
+// The tiling is built into locals and published to g only once every allocation and
+// kernel succeeded: a failure leaves g without a tiling (the next call retries) instead of
+// a half-built one that later passes would launch with.
 int gc_build_tiling(gc_graph* g) {
     if (g->tile_r0) return GC_OK;
     const hipStream_t s = g->stream;
     const long long n = g->n, nnz = g->nnz;
-    g->ntiles = (nnz + n + GC_TW - 1) / GC_TW;
-    g->nseg_cap = nnz / GC_SEG + nnz / GC_TH + 1;
+    const long long ntiles = (nnz + n + GC_TW - 1) / GC_TW;
+    const long long nseg_cap = nnz / GC_SEG + nnz / GC_TH + 1;
+    int* tile_r0 = nullptr;
+    long long* seg_base = nullptr;
+    int *seg_row = nullptr, *seg_j = nullptr;
+    ull* seg_aux = nullptr;
+    unsigned* seg_cls = nullptr;
     long long* cnt = nullptr;
-    GC_HIP(gc_dmalloc((void**)&g->tile_r0, sizeof(int) * (size_t)(g->ntiles + 1)));
-    GC_HIP(gc_dmalloc((void**)&g->seg_base, sizeof(long long) * (size_t)(g->ntiles + 1)));
-    GC_HIP(gc_dmalloc((void**)&g->seg_row, sizeof(int) * (size_t)g->nseg_cap));
-    GC_HIP(gc_dmalloc((void**)&g->seg_j, sizeof(int) * (size_t)g->nseg_cap));
-    GC_HIP(gc_dmalloc((void**)&g->seg_aux, sizeof(ull) * (size_t)g->nseg_cap));
-    GC_HIP(gc_dmalloc((void**)&g->seg_cls, sizeof(unsigned) * (size_t)g->nseg_cap * GC_BLOCK));
-    GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(g->ntiles + 1)));
-    hipLaunchKernelGGL(k_tile_bounds, dim3(small_grid(g->ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp, n, g->ntiles,
-                       g->tile_r0);
-    hipLaunchKernelGGL(k_tile_nseg, dim3(small_grid(g->ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp,
-                       (const int*)g->tile_r0, g->ntiles, cnt);
-    int rc = scan_ll(cnt, g->seg_base, g->ntiles + 1, s);
+    auto release = [&]() {
+        for (void* p : {(void*)tile_r0, (void*)seg_base, (void*)seg_row, (void*)seg_j, (void*)seg_aux, (void*)seg_cls})
+            if (p) gc_dfree(p);
+    };
+    int rc = GC_OK;
+    if (gc_dmalloc((void**)&tile_r0, sizeof(int) * (size_t)(ntiles + 1)) != hipSuccess ||
+        gc_dmalloc((void**)&seg_base, sizeof(long long) * (size_t)(ntiles + 1)) != hipSuccess ||
+        gc_dmalloc((void**)&seg_row, sizeof(int) * (size_t)nseg_cap) != hipSuccess ||
+        gc_dmalloc((void**)&seg_j, sizeof(int) * (size_t)nseg_cap) != hipSuccess ||
+        gc_dmalloc((void**)&seg_aux, sizeof(ull) * (size_t)nseg_cap) != hipSuccess ||
+        gc_dmalloc((void**)&seg_cls, sizeof(unsigned) * (size_t)nseg_cap * GC_BLOCK) != hipSuccess ||
+        gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(ntiles + 1)) != hipSuccess) {
+        if (cnt) gc_dfree(cnt);
+        release();
+        gc_set_error("gc_build_tiling: device allocation failed");
+        return GC_ENOMEM;
+    }
+    hipLaunchKernelGGL(k_tile_bounds, dim3(small_grid(ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp, n, ntiles, tile_r0);
+    hipLaunchKernelGGL(k_tile_nseg, dim3(small_grid(ntiles + 1)), dim3(GC_BLOCK), 0, s, g->rp, (const int*)tile_r0,
+                       ntiles, cnt);
+    rc = scan_ll(cnt, seg_base, ntiles + 1, s);
     if (rc == GC_OK)
-        hipLaunchKernelGGL(k_tile_segs, dim3(small_grid(g->ntiles)), dim3(GC_BLOCK), 0, s, (const int*)g->tile_r0,
-                           g->ntiles, (const long long*)g->seg_base, g->seg_row, g->seg_j);
-    hipStreamSynchronize(s);
+        hipLaunchKernelGGL(k_tile_segs, dim3(small_grid(ntiles)), dim3(GC_BLOCK), 0, s, (const int*)tile_r0, ntiles,
+                           (const long long*)seg_base, seg_row, seg_j);
+    const hipError_t se = hipStreamSynchronize(s);
+    const hipError_t le = hipGetLastError();
     gc_dfree(cnt);
-    if (rc) return rc;
-    GC_HIP(hipGetLastError());
+    if (rc == GC_OK && (se != hipSuccess || le != hipSuccess)) {
+        gc_set_error("gc_build_tiling: %s", hipGetErrorString(se != hipSuccess ? se : le));
+        rc = GC_EHIP;
+    }
+    if (rc) {
+        release();
+        return rc;
+    }
+    g->ntiles = ntiles;
+    g->nseg_cap = nseg_cap;
+    g->tile_r0 = tile_r0;
+    g->seg_base = seg_base;
+    g->seg_row = seg_row;
+    g->seg_j = seg_j;
+    g->seg_aux = seg_aux;
+    g->seg_cls = seg_cls;
     return GC_OK;
 }
 

@@ -123,6 +123,10 @@ static int shard_sync(gc_shard* sh) {
     GC_HIP(hipGetLastError());
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));
+    if (g->hctl->loop_err == GC_LERR_LIST) {
+        gc_set_error("shard: a work-list append passed the list's capacity (round %lld)", g->hctl->round);
+        return GC_EHIP;
+    }
     return GC_OK;
 }
 
@@ -202,10 +206,11 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
 
 extern "C" void gc_shard_destroy(gc_shard* sh) {
     if (!sh) return;
-    if (sh->owner) sh->owner->shard_refs--;
+    gc_graph* owner = sh->owner;
     gc_free_all(&sh->v);
     shard_free_hubs(sh);
     delete sh;
+    if (owner && --owner->shard_refs == 0 && owner->destroy_pending) gc_graph_destroy(owner);
 }
 
 // init + seed on the replicated state (coloring.py:74-76); the seeds push into the

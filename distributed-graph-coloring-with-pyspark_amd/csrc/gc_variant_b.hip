@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B,
     DevCtl* c = g.ctl;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, BLists B, int* ev, in
     const int* __restrict__ list = B.l[2][rs];
     const long long cnt = (long long)*b_cnt(c, 2, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    GcStage st{s_stage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
     const int* __restrict__ list = B.l[0][rs];
     const long long cnt = (long long)*b_cnt(c, 0, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    GcStage st{s_stage[w], 0}, est{s_estage[w], 0};
+    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err}, est{s_estage[w], 0, g.n, &g.ctl->loop_err};
     const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -763,6 +763,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             recs.push_back(RoundRec{0, 0, -1, 0, 0, 0});
             break;
         }
+        if (h.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
         if (h.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
         const long long maxmex = h.maxmex;
         if (h.kbound >= 0 && h.failcnt > 0) {  // state at the round start is returned
