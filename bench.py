@@ -272,6 +272,23 @@ class StepRunner:
             assert unc == 0 and conf == 0
             return {"colors": res.colors, "csr": dg.export()}
 
+    def end_to_end(self, rp, col, reps=2):
+        """SURVEY.md §8d's "end-to-end time is also reported" (coloring.py:233-234's `Total
+        execution time`, without file parsing): the CSR in host memory (pageable numpy) ->
+        gc_graph_create (H2D + rank partition) -> gc_color -> gc_validate -> colours in host
+        memory -> destroy.  Best of `reps`, outside the timed region; never `value`."""
+        from gcolor_amd.engine import DeviceGraph
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            with DeviceGraph.from_csr(rp, col, symmetric=self.sym) as dg:
+                res = dg.color(self.V, want_colors=True, want_rounds=False, **self.mode)
+                unc, conf = dg.validate()
+            dt = time.perf_counter() - t0
+            assert unc == 0 and (conf == 0 or not self.sym) and len(res.colors) == self.n
+            best = dt if best is None else min(best, dt)
+        return best
+
     def close(self):
         self.d_rp = self.d_col = None
         self.torch.cuda.empty_cache()
@@ -490,7 +507,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
         achieved = balg / world / t / 1e9
         line = {
             "metric": METRIC, "value": m / t, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": t * 1e3, "higher_is_better": True, "scaling": args.scaling,
+            "warmup": args.warmup, "ms_per_step": t * 1e3, "higher_is_better": True,
+            "scaling": args.scaling if world > 1 else None,
             "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": desc, "n": dg.n, "m_undirected": m, "nnz": dg.nnz, "max_degree": dg.max_degree,
                        "variant": "A (coloring.py)",
@@ -560,6 +578,8 @@ def main():
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the R-MAT-26 measurement the default run adds (north_star object)")
     ap.add_argument("--north-star-steps", type=int, default=3)
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the end-to-end measurement (host CSR -> colours on host) the N=1 line adds")
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
@@ -627,6 +647,7 @@ def main():
     # events.  Then the same K steps again with the dominant class's launch runs bracketed by
     # HIP events on the engine's own stream (the roofline's launch durations).
     t, kern, r, phases = S.steps(args.steps, None, roctx=True)
+    t_self = t  # this rank's own step time: for replicated runs, the one-GPU time of the same work
     rounds, sweeps, reseeds, colours = r.rounds, r.jp_sweeps, r.reseeds, r.num_colors
     m_all = m  # edges coloured per step by the whole job
     if dist is not None:
@@ -681,6 +702,19 @@ def main():
         except Exception as e:  # noqa: BLE001 -- a failing baseline is reported, not the line lost
             cpu = {"error": f"{type(e).__name__}: {e}"}
             print(f"WARNING: cpu_baseline failed: {cpu['error']}", file=sys.stderr, flush=True)
+    e2e = None
+    if world == 1 and not args.no_end_to_end:
+        try:
+            csr = host_csr or (final["csr"] if final else S.final_colouring()["csr"])
+            e2e_s = S.end_to_end(*csr)
+            e2e = {"ms": round(e2e_s * 1e3, 3), "edges_per_s": m / e2e_s,
+                   "path": "CSR in pageable host memory -> gc_graph_create (H2D + rank partition) -> gc_color -> "
+                           "gc_validate -> colours in host memory -> destroy (best of 2; coloring.py:233-234 "
+                           "without the JSON parse)"}
+            del csr
+        except Exception as e:  # noqa: BLE001 -- context only
+            e2e = {"error": f"{type(e).__name__}: {e}"}
+    final = None
     ns = None
     if world == 1 and args.workload == "rmat24" and not args.no_north_star and V == "A" and not any(mode.values()):
         S.close()
@@ -699,7 +733,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t * 1e3,
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": args.scaling if world > 1 else None,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -711,6 +745,10 @@ def main():
                                    (f"replicated: each of the {world} ranks runs the one-GPU engine on the whole graph, "
                                     "no exchange (the rounds are a latency chain: DESIGN.md §7); time = slowest rank"))
                                   if world > 1 else "single",
+                   # every N > 1 line states the one-GPU time of its work: rank 0's own step time
+                   # (replicated: the same graph; replicas: rank 0's own graph)
+                   "single_gpu_ms": round(t_self * 1e3, 3) if world > 1 else None,
+                   "speedup_vs_single_gpu": round(t_self / t, 3) if world > 1 else None,
                    "rank": ("(deg, pos) (coloring.py:64)" if args.priority_seed is None
                             else f"prio_hash(seed={args.priority_seed}, v), pos"),
                    "resolution": "speculative first-fit, one-shot" if args.speculative else "Jones-Plassmann LFMIS",
@@ -720,6 +758,8 @@ def main():
                    "async_jp_aborts": r.async_aborts,
                    "graph_build_s": round(gen_s, 2),
                    "event_timed_class": None if args.no_event_timing else dom_class},
+        "end_to_end_ms": e2e and e2e.get("ms"),
+        "end_to_end": e2e,
         "colors_used": colours,
         "phases_ms": {k: round(v * 1e3, 3) for k, v in phases.items()},
         "recolour_ms": round(recolour_ms, 3),

@@ -16,6 +16,10 @@
 #   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
 #   rounds:WL         per-round kernel cost by frontier size (tools/round_cost.py under
 #                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
+#   ab:WL:REPS:CFGS   tools/ab_steps.py WL REPS CFG... (CFGS comma-separated, each NAME=VAR:val+VAR:val):
+#                     interleaved in-process A/B of environment knobs, colourings checked equal
+#   ?STEP             soft step: a plain test failure (pytest rc 1 with no GPU error in its log)
+#                     is recorded and the session goes on; anything else still ends it
 # Output: gpurun_out/TAG/ (merged back by gpurun).
 set -uo pipefail
 TAG=$1
@@ -27,6 +31,8 @@ cd "$ROOT"
 i=0
 for st in "$@"; do
   i=$((i + 1))
+  soft=0
+  if [ "${st:0:1}" = "?" ]; then soft=1; st=${st:1}; fi
   kind=${st%%:*}
   rest=${st#*:}
   [ "$rest" = "$st" ] && rest=""
@@ -82,11 +88,19 @@ for st in "$@"; do
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
+    ab)
+      wl=${rest%%:*}; a=${rest#*:}; reps=${a%%:*}; cf=${a#*:}
+      timeout -k 10 600 python -u tools/ab_steps.py "$wl" "$reps" ${cf//,/ } > "$log" 2>&1 ;;
     *)
       echo "unknown step $st" > "$log"; false ;;
   esac
   rc=$?
   tail -3 "$log" | cut -c1-400 | tee -a "$O/session.log"
+  if [ $rc -eq 1 ] && [ $soft -eq 1 ] && ! grep -qE "HSA_STATUS_ERROR|Memory access fault|GPU core dump|hipError|GcolorError|status -2" "$log"; then
+    echo "== step $i ($st) FAILED (soft: test failures only, session goes on)" | tee -a "$O/session.log"
+    grep -E "^(FAILED|ERROR) " "$log" | head -20 | tee -a "$O/session.log"
+    continue
+  fi
   if [ $rc -ne 0 ]; then
     echo "== step $i ($st) failed: rc=$rc" | tee -a "$O/session.log"
     tail -40 "$log"
