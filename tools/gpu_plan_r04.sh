@@ -9,6 +9,16 @@ set -uo pipefail
 cd "$(dirname "$0")/.."
 case ${1:-} in
   a) exec_steps=(staged:overflow_tree staged:under_ticket_close tests smoke profile:rmat24 staged:async_jp_without_hubs) ;;
-  *) echo "usage: $0 a" >&2; exit 2 ;;
+  # b: every staged path's parity tests, each a soft step (a plain test failure is recorded and
+  #    the session goes on; a GPU error still ends it), then the per-round cost by frontier size
+  b) exec_steps=("?staged:resume~or~hybrid" "?staged:b_async" "?staged:async_resolve" "?staged:big_close"
+                 "?staged:test_graphs_" "?staged:small_grid" "?staged:validate_c8" rounds:rmat24) ;;
+  # c: interleaved in-process A/Bs of the environment knobs, then the compile-time variants
+  c) exec_steps=(ab:rmat24:6:base,ares=GC_ASYNC_RESOLVE:1,bclose=GC_BIG_CLOSE:1,graphs=GC_GRAPHS:1,small=GC_GRID_SMALL:256,bpc4=GC_ASYNC_BPC:4
+                 ab:uniform10M:8:base,async2=GC_ASYNC:2,graphs=GC_GRAPHS:1,small=GC_GRID_SMALL:256
+                 ab:mesh512:4:base,graphs=GC_GRAPHS:1,async2=GC_ASYNC:2
+                 env:AB_VARIANT=B ab:rmat24:3:base,basync=GC_B_ASYNC:1 env:AB_VARIANT=
+                 abl:rmat24:4:2:base=-,marks4=variants/marks4/libgcolor.so,claim4=variants/claim4/libgcolor.so,all4=variants/all4/libgcolor.so,hinhoist=variants/hinhoist/libgcolor.so,closeint=variants/close_interleaved/libgcolor.so,closecall=variants/close_call/libgcolor.so,tile8=variants/tile8/libgcolor.so) ;;
+  *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"

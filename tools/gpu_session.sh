@@ -18,6 +18,8 @@
 #                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
 #   ab:WL:REPS:CFGS   tools/ab_steps.py WL REPS CFG... (CFGS comma-separated, each NAME=VAR:val+VAR:val):
 #                     interleaved in-process A/B of environment knobs, colourings checked equal
+#   abl:WL:REPS:CYCLES:VARS  tools/ab_libs.sh: compile-time variants, a process each, alternated
+#                     (VARS comma-separated NAME=PATH, PATH - = the in-tree build)
 #   ?STEP             soft step: a plain test failure (pytest rc 1 with no GPU error in its log)
 #                     is recorded and the session goes on; anything else still ends it
 # Output: gpurun_out/TAG/ (merged back by gpurun).
@@ -88,6 +90,10 @@ for st in "$@"; do
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
+    abl)
+      wl=${rest%%:*}; a=${rest#*:}; reps=${a%%:*}; a=${a#*:}; cyc=${a%%:*}; vs=${a#*:}
+      timeout -k 10 1100 bash tools/ab_libs.sh "$wl" "$reps" "$cyc" ${vs//,/ } > "$log" 2>&1 &&
+        grep "^== " "$log" | grep -v "interleaved" >> "$log.summary"; cat "$log.summary" >> "$log" ;;
     ab)
       wl=${rest%%:*}; a=${rest#*:}; reps=${a%%:*}; cf=${a#*:}
       timeout -k 10 600 python -u tools/ab_steps.py "$wl" "$reps" ${cf//,/ } > "$log" 2>&1 ;;
