@@ -12,7 +12,7 @@ case ${1:-} in
   # b: every staged path's parity tests, each a soft step (a plain test failure is recorded and
   #    the session goes on; a GPU error still ends it), then the per-round cost by frontier size
   b) exec_steps=("?staged:resume~or~hybrid" "?staged:b_async" "?staged:async_resolve" "?staged:big_close"
-                 "?staged:test_graphs_" "?staged:small_grid" "?staged:validate_c8" rounds:rmat24) ;;
+                 "?staged:test_graphs_" "?staged:small_grid" "?staged:validate_c8" ubench:launch_gap rounds:rmat24) ;;
   # c: interleaved in-process A/Bs of the environment knobs, then the compile-time variants
   c) exec_steps=(ab:rmat24:6:base,ares=GC_ASYNC_RESOLVE:1,bclose=GC_BIG_CLOSE:1,graphs=GC_GRAPHS:1,small=GC_GRID_SMALL:256,bpc4=GC_ASYNC_BPC:4
                  ab:uniform10M:8:base,async2=GC_ASYNC:2,graphs=GC_GRAPHS:1,small=GC_GRID_SMALL:256
