@@ -91,76 +91,24 @@ __device__ __forceinline__ void gc_hub_mark(const GDev& g, int x, int cc) {
     const unsigned bit = 1u << (cc & 31);
     if (!(*p & bit)) atomicOr(p, bit);
 }
-// GC_MARK_SLOTS > 1 (build knob, staged in round 3): the marks of a list go GC_MARK_SLOTS
-// entries per thread and step -- every entry's hub index, then every bitmap word, then the
-// atomics.  One entry at a time (1, the measured default), a step's loads wait for the
-// previous step's atomic (they may alias as far as the compiler knows): two dependent
-// memory trips per entry per thread, e.g. 2 x 32 for a wave walking a 2048-hub list.
-#ifndef GC_MARK_SLOTS
-#define GC_MARK_SLOTS 1
-#endif
-// marks of hub x[k] with colour cc[k] (x[k] < 0: none), loads before any store
-template <int S>
-__device__ __forceinline__ void gc_hub_mark_n(const GDev& g, const int* x, const int* cc) {
-    unsigned* p[S];
-    unsigned wv[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-        const bool ok = x[k] >= 0 && cc[k] < 32 * g.hbits_w;
-        p[k] = ok ? g.hbits + (long long)x[k] * g.hbits_w + (cc[k] >> 5) : nullptr;
-        wv[k] = ok ? *p[k] : 0xFFFFFFFFu;
-    }
-    if (g.hseen) {  // shards: the hub now belongs to a frontier
-        unsigned char sn[S];
-#pragma unroll
-        for (int k = 0; k < S; ++k) sn[k] = x[k] >= 0 ? g.hseen[x[k]] : 1;
-#pragma unroll
-        for (int k = 0; k < S; ++k)
-            if (!sn[k]) g.hseen[x[k]] = 1;
-    }
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-        const unsigned bit = 1u << (cc[k] & 31);
-        if (p[k] && !(wv[k] & bit)) atomicOr(p[k], bit);
-    }
-}
 // every hub listing v, strided over the calling threads
 __device__ __forceinline__ void gc_hub_mark_row(const GDev& g, int v, int cc, int t0, int step) {
     const long long e1 = g.hin_rp[v + 1];
-#if GC_MARK_SLOTS > 1
-    for (long long e = g.hin_rp[v] + t0; e < e1; e += (long long)GC_MARK_SLOTS * step) {
-        int x[GC_MARK_SLOTS], c[GC_MARK_SLOTS];
-#pragma unroll
-        for (int k = 0; k < GC_MARK_SLOTS; ++k) {
-            const long long ek = e + (long long)k * step;
-            x[k] = ek < e1 ? g.hin_col[ek] : -1;
-            c[k] = cc;
-        }
-        gc_hub_mark_n<GC_MARK_SLOTS>(g, x, c);
-    }
-#else
     for (long long e = g.hin_rp[v] + t0; e < e1; e += step) gc_hub_mark(g, g.hin_col[e], cc);
-#endif
 }
 // the marks of a wave's flat range [0, total) of hub entries; entry(e, &x, &cc) gives entry
 // e's hub index and colour (all 64 lanes call it: it may shuffle; x = -1 past total)
+// (round 3's GC_MARK_SLOTS=4 -- four entries per thread and step, loads before the atomics --
+// measured within noise on R-MAT-24 in round 4, 171.3-171.9 vs 171.2-173.5 ms, profiles/r04/c:
+// removed, with GC_CLAIM_HOIST and GC_HIN_HOIST)
 template <typename Entry>
 __device__ __forceinline__ void gc_hub_mark_flat(const GDev& g, int total, Entry entry) {
     const int lane = gc_lane();
-#if GC_MARK_SLOTS > 1
-    for (int base = 0; base < total; base += GC_MARK_SLOTS * GC_WAVE) {
-        int x[GC_MARK_SLOTS], c[GC_MARK_SLOTS];
-#pragma unroll
-        for (int k = 0; k < GC_MARK_SLOTS; ++k) entry(base + k * GC_WAVE + lane, &x[k], &c[k]);
-        gc_hub_mark_n<GC_MARK_SLOTS>(g, x, c);
-    }
-#else
     for (int base = 0; base < total; base += GC_WAVE) {
         int x, c;
         entry(base + lane, &x, &c);
         if (x >= 0) gc_hub_mark(g, x, c);
     }
-#endif
 }
 // Pushes of this wave's winners' colours into the hub bitmaps (hbits_w), the wave walking
 // its lanes' hub lists as one flat range; a list longer than GC_PUSH_FLAT is appended to

@@ -290,20 +290,15 @@ struct Run {
     int async_grid = 0;
     int async_par = 0;
     long long async_budget = 0;
-    // GC_ASYNC_RESOLVE=1 (opt-in, staged): k_sweep_async also makes the round's first sweep
-    // (no k_resolve launch; one kernel boundary less per round)
-    bool async_first = false;
     void init_async() {
         const char* e = getenv("GC_ASYNC");
         if (e && atoi(e) == 0) return;
-        const bool force = e && atoi(e) == 2;  // GC_ASYNC=2: also without hubs (staged tests, tests/test_gpu_staged.py)
-        // Only with the hub JP's resumable scan (R-MAT and the like, validated at full size).
-        // Graphs with no hub (uniform, meshes) keep the full-grid sweeps and the tail: a
-        // 10M-vertex uniform graph with k_sweep_async on faulted in the following k_commit
-        // (round 3; DESIGN §5: a mid-launch stage flush under the ticket close, fixed since
-        // (GC_COUNT_MASK), to be re-validated at that size before this turns on), and their JP
-        // chains are short anyway (C2: 15 rounds).
-        if ((!d.hub_w && !force) || (d.hub_w && !d.hub_scan) || d.heavy_wg || L.delta) return;
+        // Only with the hub JP's resumable scan (R-MAT and the like).  Graphs with no hub keep
+        // the full-grid sweeps and the one-workgroup tail: round 4 measured the asynchronous
+        // JP on them (bit-exact, profiles/r04/b) at C2 12.1 -> 18.8 ms and mesh 512^3 111.6 ->
+        // 111.6 ms (profiles/r04/c), so it stays off there -- their JP chains are short (C2:
+        // 15 rounds, meshes depth 1) and a resident grid has a quarter of the full grid's waves.
+        if (!d.hub_w || !d.hub_scan || d.heavy_wg || L.delta) return;
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
             return;
@@ -316,7 +311,6 @@ struct Run {
         const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
         async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
         async_grid = cus * bpc;
-        async_first = getenv("GC_ASYNC_RESOLVE") && atoi(getenv("GC_ASYNC_RESOLVE")) > 0;
     }
     void init_loop() {
         const char* e = getenv("GC_SWEEP_LOOP");
@@ -382,15 +376,15 @@ struct Run {
 
     // big = the host also enqueues the big-round frontier build (k_pull, k_front_*): the
     // device then decides per round (gc_big_on) whether the commit pushes or marks.
-    void launch_commit(int mode, int nsweeps, bool fuse = false, bool first = false) {
+    void launch_commit(int mode, int nsweeps, bool fuse = false) {
         const int big = mode == GC_CM_ROUND && resort_hint && !fuse;
         // no sweeps enqueued and >= 16 rounds so far all decided by their first sweep (meshes):
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
-        const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail || first);
+        const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
         if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
-            kt.begin(first ? GC_K_RESOLVE : GC_K_SWEEP);
-            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s, first ? 1 : 0);
+            kt.begin(GC_K_SWEEP);
+            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
             async_par ^= 1;
             kt.end();
         } else if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch
@@ -405,16 +399,17 @@ struct Run {
         }
         // the commit's last workgroup closes the round unless k_pull / the big-round frontier
         // rebuild / k_commit_big must run between the commit and the close
+        // (graphs with big rows keep a k_close launch: closing in k_commit_big's last workgroup
+        // measured slower, R-MAT-24 172.7 -> 176.8 ms, profiles/r04/c: its workgroups then wait
+        // for the arrival ticket instead of returning at once when no winner was deferred)
         const bool tclose = mode == GC_CM_ROUND && !big && (fuse || !d.big_rows) && ticket_close;
-        // ... or, with big rows (GC_BIG_CLOSE=1, staged), k_commit_big's
-        const bool bclose = mode == GC_CM_ROUND && !big && !tclose && d.big_rows && ticket_close && big_close;
         DevCtl* snap = mode == GC_CM_ROUND ? snap_ptr : nullptr;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
         gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0, tclose ? snap : nullptr,
-                   tclose ? 1 : 0, bclose ? snap : nullptr, bclose ? 1 : 0, mode == GC_CM_ROUND && !resort_hint ? 1 : 0);
+                   tclose ? 1 : 0);
         kt.end();
         if (mode == GC_CM_ROUND) snap_ptr = nullptr;
-        if (tclose || bclose) {
+        if (tclose) {
             kt.close();
             proposed = fuse;
             return;
@@ -440,91 +435,13 @@ struct Run {
             kt.end();
         }
     }
-    // GC_GRAPHS=1 (staged, round 3): each round's launch sequence is captured once per shape
-    // into a hipGraph and replayed -- a round enqueues one graph launch instead of ~7 kernel
-    // launches.  The shape is everything the sequence depends on (sweeps, whether the last
-    // commit proposed, the re-sort / nibble hints, the tail, the asynchronous JP's launch
-    // parity, the snapshot slot); the host state a round changes is re-applied on replay.
-    // Off with kernel timing or GC_DEBUG_SYNC (they need the per-launch host calls).
-    struct GKey {
-        int S, proposed, resort, c4, skip_tail, par;
-        const DevCtl* snap;
-        bool operator<(const GKey& o) const {
-            const long long a[7] = {S, proposed, resort, c4, skip_tail, par, (long long)(intptr_t)snap};
-            const long long b[7] = {o.S, o.proposed, o.resort, o.c4, o.skip_tail, o.par, (long long)(intptr_t)o.snap};
-            return std::lexicographical_compare(a, a + 7, b, b + 7);
-        }
-    };
-    struct GEntry {
-        hipGraphExec_t ex;
-        long long launches[GC_NKERNELS];  // the kernel-class counts one replay adds to the stats
-    };
-    std::map<GKey, GEntry> graphs;
-    bool graphs_on = getenv("GC_GRAPHS") && atoi(getenv("GC_GRAPHS")) > 0;
-    ~Run() {
-        for (auto& kv : graphs) hipGraphExecDestroy(kv.second.ex);
-    }
+    // (round 3's GC_GRAPHS -- each round's launches replayed from a hipGraph -- measured slower
+    // in round 4: R-MAT-24 +2.4%, C2 +3.7%, mesh 512^3 +7.3%, profiles/r04/c; removed)
     void enqueue_round(int S) {
-        if (!graphs_on || kt.mask || kt.dbg_sync) {
-            enqueue_round_direct(S);
-            return;
-        }
-        const GKey key{S, proposed ? 1 : 0, resort_hint ? 1 : 0, c4_hint ? 1 : 0, skip_tail ? 1 : 0, async_par, snap_ptr};
-        auto it = graphs.find(key);
-        if (it == graphs.end()) {  // capture this shape (the host state moves as in a direct round)
-            long long before[GC_NKERNELS] = {};
-            if (st)
-                for (int k = 0; k < GC_NKERNELS; ++k) before[k] = st->k_launches[k];
-            const bool proposed0 = proposed;
-            const int par0 = async_par;
-            DevCtl* const snap0 = snap_ptr;
-            hipGraph_t gr = nullptr;
-            GEntry e{};
-            hipError_t err = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
-            if (err == hipSuccess) {
-                enqueue_round_direct(S);
-                const hipError_t e2 = hipStreamEndCapture(s, &gr);
-                err = e2;
-            }
-            if (err == hipSuccess) err = hipGraphInstantiate(&e.ex, gr, nullptr, nullptr, 0);
-            if (gr) hipGraphDestroy(gr);
-            if (err != hipSuccess) {  // nothing of the round ran: restore the host state, go direct
-                fprintf(stderr, "[gc] GC_GRAPHS: capture failed (%s); graphs off\n", hipGetErrorString(err));
-                graphs_on = false;
-                (void)hipGetLastError();
-                proposed = proposed0;
-                async_par = par0;
-                snap_ptr = snap0;
-                if (st)
-                    for (int k = 0; k < GC_NKERNELS; ++k) st->k_launches[k] = before[k];
-                enqueue_round_direct(S);
-                return;
-            }
-            if (st)
-                for (int k = 0; k < GC_NKERNELS; ++k) e.launches[k] = st->k_launches[k] - before[k];
-            it = graphs.emplace(key, e).first;
-            hipGraphLaunch(e.ex, s);
-            return;
-        }
-        // replay, and the host side of enqueue_round_direct for this shape
-        const bool fuse = fuse_now();
-        const bool tail = async_first || S > 0 || !skip_tail;
-        hipGraphLaunch(it->second.ex, s);
-        if (st)
-            for (int k = 0; k < GC_NKERNELS; ++k) st->k_launches[k] += it->second.launches[k];
-        if (tail && async_grid > 0) async_par ^= 1;
-        snap_ptr = nullptr;
-        proposed = fuse;
-    }
-    void enqueue_round_direct(int S) {
         const bool fuse = fuse_now();
         if (!proposed) enqueue_propose();
-        if (async_first) {  // k_sweep_async makes the first sweep too
-            launch_commit(GC_CM_ROUND, 0, fuse, true);
-            return;
-        }
         kt.begin(GC_K_RESOLVE);
-        gcl_resolve(d, L, s, resort_hint ? 0 : 1);
+        gcl_resolve(d, L, s);
         kt.end();
         launch_sweeps(1, S);
         launch_commit(GC_CM_ROUND, S, fuse);
@@ -557,9 +474,6 @@ struct Run {
     DevCtl* snap_ptr = nullptr;  // handed to the next round's k_close (or closing commit)
     // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
     const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
-    // GC_BIG_CLOSE=1 (staged, round 3): graphs with big rows close the round in k_commit_big
-    // (no k_close launch per round: ~900 per R-MAT-24 colouring)
-    const bool big_close = getenv("GC_BIG_CLOSE") && atoi(getenv("GC_BIG_CLOSE")) > 0;
     int enqueue_batch(int B, int S, int slot) {
         for (int b = 0; b < B; ++b) {
             if (b == B - 1 && !snap_copy) snap_ptr = g->hsnap_dev + slot;
@@ -665,7 +579,7 @@ struct Run {
         // Pipelined: batch k+1 is enqueued before the host waits on batch k's snapshot, so
         // the device never idles on the host.  Any halt drains the stream and is handled on
         // the synchronous path below, then the pipeline restarts.
-        int batch = 1, S = async_first ? 0 : 1;
+        int batch = 1, S = 1;
         for (;;) {
             int slot = 0;
             if ((rc = enqueue_batch(batch, S, slot))) return rc;

@@ -1502,48 +1502,24 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 // spills to slot (S + 1) % 3 (cleared by sweep S), clears slot (S + 2) % 3 and sets
 // tail_last = S + 1, the slot the commit checks -- exactly what a tail that ran one more
 // sweep leaves.  `par` alternates per launch (the counters of the next launch are zeroed
-// here); `budget` is in wall-clock ticks.
-// first = 1 (GC_ASYNC_RESOLVE, opt-in): the launch also makes the round's first sweep in place
-// of k_resolve -- its lights are the frontier's (F[cur] minus the heavy proposers, first
-// evaluated from the start of their low rows), copied to slot 0 as the waves' lists, the
-// bounded-attempt check and the first sweep's §8d credit are k_resolve's -- and S is 0.
-__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget,
-                                                          int first) {
+// here); `budget` is in wall-clock ticks.  (Round 3's variant that also made the round's
+// first sweep, in place of k_resolve, measured R-MAT-24 172.7 -> 190.4 ms in round 4,
+// profiles/r04/c: removed.)
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
-    if (first && c->kbound >= 0 && c->failcnt > 0) {  // coloring.py:104-108 (as k_resolve)
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            const long long r = c->round;
-            RoundRec* rec = L.rec + (r - c->rbase);
-            rec->U = c->U;
-            rec->F = (long long)c->fcnt[c->cur];
-            rec->maxmex = c->maxmex;
-            rec->accepted = 0;
-            rec->seeds = 0;
-            rec->sweeps = 0;
-            c->fail_round = r;
-            c->fail_count = (long long)c->failcnt;
-            c->round = r + 1;
-            c->halt = GC_H_FAILED;
-        }
-        return;
-    }
     __shared__ GcAsyncLds s_w[GC_WAVES_PER_BLOCK];
     const int w = threadIdx.x / GC_WAVE;
-    const long long j = first ? 0 : S;
+    const long long j = S;
     const int in = (int)(j % 3), out = (int)((j + 1) % 3), z = (int)((j + 2) % 3);
-    const int cur = c->cur;
-    // first: the slices run over the frontier (cf entries); cl = its lights (every heavy
-    // proposer of F is on L.heavy once: k_propose)
-    const long long cf = first ? (long long)c->fcnt[cur] : 0ll;
-    const long long cl = first ? cf - (long long)c->heavy_cnt : (long long)c->und_cnt[in];
+    const long long cl = (long long)c->und_cnt[in];
     // hubs already started by an earlier sweep of the round: their undecided list; else every
     // hub proposer, once the lights have converged.  (hub_start moves during the launch only
     // from "not started" to S + 1 > S: every reader takes the same branch.)
     const bool started = g.hub_w && __hip_atomic_load(&c->hub_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j;
     const int* hsrc = started ? L.undH[in] : L.heavy;
     const long long ch = g.hub_w ? (long long)(started ? c->undh_cnt[in] : c->heavy_cnt) : 0ll;
-    if (cl > g.n || ch > g.n || cl < 0 || cf > g.n) {  // never expected: report (the host turns it into an error), touch nothing
+    if (cl > g.n || ch > g.n || cl < 0) {  // never expected: report (the host turns it into an error), touch nothing
         if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&c->loop_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
@@ -1551,8 +1527,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         c->und_cnt[z] = 0;
         c->undh_cnt[z] = 0;
         c->tail_last = j + 1;
-        if (first) c->sweeps = 1 + (cl + ch > 0 ? 1 : 0);
-        else if (cl + ch > 0) c->sweeps += 1;
+        if (cl + ch > 0) c->sweeps += 1;
         c->async_done[par ^ 1] = 0;
         c->async_abort[par ^ 1] = 0;
         if (!started && ch > 0 && cl == 0) gc_st(&c->hub_start, j + 1);
@@ -1566,38 +1541,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     bool stop = false;
     // lights: the wave's static slice of the list, compacted in place pass after pass
     {
-        const long long span = first ? cf : cl;
-        const long long la = span * wid / W, lb = span * (wid + 1) / W;
+        const long long la = cl * wid / W, lb = cl * (wid + 1) / W;
         int np = (int)(lb - la);
         int* lst = L.undL[in] + la;
-        if (first) {  // the slice's lights, compacted into slot 0, each from the start of its low row
-            const int* fl = L.F[cur] + la;
-            const int lane = gc_lane();
-            int nl = 0;
-            ull lsum = 0, lnv = 0;
-            for (int i0 = 0; i0 < np; i0 += GC_WAVE) {
-                const int v = i0 + lane < np ? fl[i0 + lane] : -1;
-                const int d = v >= 0 ? g.deg[v] : 0;
-                const bool light = v >= 0 && d <= g.heavy_t;
-                const ull m = __ballot(light);
-                if (light) {
-                    lst[nl + __popcll(m & gc_lanemask_lt())] = v;
-                    g.lcur[v] = 0;
-                    lsum += (ull)d;  // the first sweep's §8d credit (k_resolve's)
-                    lnv++;
-                }
-                nl += __popcll(m);
-            }
-            np = nl;
-            lsum = gc_wave_sum(lsum);  // per wave into the stats slots (gc_stat_add's GC_STAT_WAVE form)
-            lnv = gc_wave_sum(lnv);
-            if (lane == 0) {
-                ull* slot = g.bstat + (wid % GC_STAT_SLOTS) * 16;
-                if (lsum) atomicAdd(slot + GC_K_RESOLVE, lsum);
-                if (lnv) atomicAdd(slot + 8 + GC_K_RESOLVE, lnv);
-            }
-            gc_wave_sync();
-        }
         ull decided = 0;
         int idle = 0;
         while (np > 0) {
@@ -1695,11 +1641,6 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
 }
 #ifndef GC_CSLOTS
 #define GC_CSLOTS 2
-#endif
-// GC_CLAIM_HOIST (build knob, staged in round 3): k_commit's claim check-loads of all
-// GC_CSLOTS slots before their atomics (see the claim loop)
-#ifndef GC_CLAIM_HOIST
-#define GC_CLAIM_HOIST 0
 #endif
 #ifndef GC_PREFETCH_ROW
 #define GC_PREFETCH_ROW 1
@@ -1950,36 +1891,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         gc_stage_push(st, pred, val, next, next_cnt);
     };
     // a winner's in-row [ts, te) strided over the calling threads (a wave, or the workgroup):
-    // every in-neighbour marked (big round) or claimed into the next frontier.  With
-    // GC_MARK_SLOTS > 1 a thread takes that many entries per step -- their tcol loads, then
-    // their claim words, then the atomics -- instead of one entry's three dependent memory
-    // trips at a time (a hub winner's in-row of up to GC_BIGROW entries walked by one wave)
+    // every in-neighbour marked (big round) or claimed into the next frontier
     auto walk_claims = [&](long long ts, long long te, int t0, int step) {
-#if GC_MARK_SLOTS > 1
-        for (long long e0 = ts + t0; e0 - t0 < te; e0 += (long long)GC_MARK_SLOTS * step) {
-            int xs[GC_MARK_SLOTS];
-            unsigned cw[GC_MARK_SLOTS];
-            bool cl[GC_MARK_SLOTS];
-#pragma unroll
-            for (int k = 0; k < GC_MARK_SLOTS; ++k) {
-                const long long e = e0 + (long long)k * step;
-                xs[k] = e < te ? g.tcol[e] : -1;
-            }
-#pragma unroll
-            for (int k = 0; k < GC_MARK_SLOTS; ++k) cw[k] = (xs[k] >= 0 && !mark) ? g.inF[xs[k] >> 5] : 0u;
-#pragma unroll
-            for (int k = 0; k < GC_MARK_SLOTS; ++k) {
-                cl[k] = false;
-                if (xs[k] >= 0) {
-                    const unsigned bit = 1u << (xs[k] & 31);
-                    if (mark) g.mark[xs[k]] = 1;
-                    else if (!(cw[k] & bit)) cl[k] = !(atomicOr(&g.inF[xs[k] >> 5], bit) & bit);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < GC_MARK_SLOTS; ++k) push(cl[k], xs[k] < 0 ? 0 : xs[k]);
-        }
-#else
         for (long long e0 = ts; e0 < te; e0 += step) {
             const long long e = e0 + t0;
             bool claim = false;
@@ -1991,7 +1904,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             }
             push(claim, x);
         }
-#endif
     };
     // hubs on: a wave per hub (in-rows past bigrow are deferred to k_commit_big)
     if (g.hub_w) {
@@ -2122,23 +2034,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                 }
 #endif
             }
-#if GC_CLAIM_HOIST
-            // every slot's claim word first, then the atomics: in the loop below a slot's
-            // check-load waits for the previous slot's returning atomic (it may alias)
-            unsigned cw[GC_CSLOTS];
-#pragma unroll
-            for (int k = 0; k < GC_CSLOTS; ++k) cw[k] = (ok[k] && !mark) ? g.inF[x[k] >> 5] : 0u;
-#pragma unroll
-            for (int k = 0; k < GC_CSLOTS; ++k) {
-                claim[k] = false;
-                if (ok[k]) {
-                    const unsigned bit = 1u << (x[k] & 31);
-                    if (mark) g.mark[x[k]] = 1;
-                    else if ((FUSE && g.claim_direct) || !(cw[k] & bit))
-                        claim[k] = !(atomicOr(&g.inF[x[k] >> 5], bit) & bit);
-                }
-            }
-#else
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) {
                 claim[k] = false;
@@ -2148,7 +2043,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
                     else claim[k] = gc_claim(g.inF, x[k]);
                 }
             }
-#endif
 #pragma unroll
             for (int k = 0; k < GC_CSLOTS; ++k) push(claim[k], x[k]);
         }
@@ -2208,26 +2102,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
 // 256 winners per tile (their row offsets prefix-summed in LDS, owner by binary search).
 // Walking the winners one after another cost ~5 dependent memory round trips per winner
 // on every workgroup: 1.8 ms for the ~400 hub winners of an R-MAT-26 round.
-// tclose (GC_BIG_CLOSE=1, staged; ROUND mode, no big-round rebuild): this launch closes the
-// round instead of a k_close launch after it -- workgroup 0 when no winner was deferred, else
-// the last workgroup to arrive (arrival tickets on the next frontier's counter, as k_commit's
-// gc_stage_flush_ticket) -- and, with snap, writes the snapshot; on a halt it only writes the
-// snapshot (k_close's behaviour).
-__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big, DevCtl* snap,
-                                                         int tclose) {
+__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big) {
     DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) {
-        if (tclose && snap && blockIdx.x == 0) gc_snap_copy(c, snap);
-        return;
-    }
+    if (mode == GC_CM_ROUND && c->halt) return;
     const long long nb = (long long)c->bigw_cnt;
-    if (nb == 0) {
-        if (tclose && blockIdx.x == 0) {
-            gc_close_body(g, L, c, mode, 0, 0);
-            if (snap) gc_snap_copy(c, snap);
-        }
-        return;
-    }
+    if (nb == 0) return;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_off[GC_BLOCK + 1];  // exclusive prefix of the tile's per-winner work
     __shared__ long long s_hs[GC_BLOCK], s_ts[GC_BLOCK];
@@ -2297,18 +2176,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
         }
         __syncthreads();  // the tile's LDS is rewritten next
     }
-    if (!tclose) {
-        gc_stage_flush_block(st, next, next_cnt);
-        return;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's frontier entries have landed
-    ull fnext = 0;
-    if (gc_stage_flush_ticket(st, next, next_cnt, &fnext)) {  // the last workgroup closes the round
-        if (threadIdx.x == 0) gc_st(next_cnt, fnext);            // without the tickets
-        __syncthreads();
-        gc_close_body(g, L, c, mode, 0, 0);
-        if (snap) gc_snap_copy(c, snap);
-    }
+    gc_stage_flush_block(st, next, next_cnt);
 }
 
 // Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
@@ -3030,11 +2898,8 @@ static const int kGridP = round_grid("GC_GRID_P", GC_ROUND_GRID);
 // 216 -> 210 ms with the later sweeps on 256; the full grid stays for C2's big rounds)
 static const int kGridPS = round_grid("GC_GRID_PS", 512);
 static const int kGridR = round_grid("GC_GRID_R", GC_ROUND_GRID);
-// GC_GRID_SMALL=N (staged, round 3; 0 = off): k_resolve, k_commit and k_commit_big on at most
-// N workgroups when the last snapshot's frontier was small (< n/256, as kGridPS) -- a small
-// round's 768-1024 mostly idle workgroups still cost their dispatch and end-of-kernel work
-static const int kGridSmall = round_grid("GC_GRID_SMALL", 0);
-static int small_grid(int dflt, int small) { return small && kGridSmall > 0 && kGridSmall < dflt ? kGridSmall : dflt; }
+// (round 3's GC_GRID_SMALL -- resolve / commit / commit_big capped to 256 workgroups in small
+// rounds -- measured R-MAT-24 -0.1%, C2 +2% in round 4, profiles/r04/c: removed)
 static const int kGridC = round_grid("GC_GRID_C", 768);  // mesh 512^3 111 -> 106 ms (1024 -> 768; 1536: 158), R-MAT and C2 alike
 static const int kGridPB = round_grid("GC_GRID_PB", GC_BLOCK_GRID);  // k_propose_block
 static const int kGridCB = round_grid("GC_GRID_CB", GC_ROUND_GRID);  // k_commit_big
@@ -3071,8 +2936,8 @@ void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small) {
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
-void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s, int small) {
-    hipLaunchKernelGGL(k_resolve, dim3(small_grid(g.heavy_wg ? kGridRH : kGridR, small)), dim3(GC_BLOCK), 0, s, g, L);
+void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
+    hipLaunchKernelGGL(k_resolve, dim3(g.heavy_wg ? kGridRH : kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep, dim3(g.heavy_wg ? kGridSH : kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
@@ -3157,9 +3022,8 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
     else if (g.tail_nw == 8) hipLaunchKernelGGL(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
     else hipLaunchKernelGGL(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
 }
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
-                     int first) {
-    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget, first);
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
 }
 int gcl_sweep_async_blocks_per_cu() {
     int b = 0;
@@ -3170,16 +3034,15 @@ void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused,
-                DevCtl* snap, int tclose, DevCtl* bsnap, int bclose, int small) {
-    const int gc = small_grid(kGridC, small);
+                DevCtl* snap, int tclose) {
+    const int gc = kGridC;
     if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
         hipLaunchKernelGGL(k_commit<1>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
         return;
     }
     hipLaunchKernelGGL(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        hipLaunchKernelGGL(k_commit_big, dim3(small_grid(kGridCB, small)), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big,
-                           bsnap, bclose);
+        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

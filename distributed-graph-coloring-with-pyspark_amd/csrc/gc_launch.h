@@ -97,24 +97,19 @@ void gcl_pack_c4(const GDev& g, hipStream_t s);
 void gcl_stat_reduce(const GDev& g, hipStream_t s);
 void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small = 0);  // small: the last frontier was < n/256
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
-void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s, int small = 0);  // small: as gcl_commit
+void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // one-workgroup tail sweeps
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 // asynchronous JP after sweep S on a resident grid (budget in wall-clock ticks; par alternates per launch)
-// first = 1: the launch also makes the round's first sweep (no k_resolve before it; S = 0)
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
-                     int first = 0);
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s);
 int gcl_sweep_async_blocks_per_cu();
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
 // tclose: the commit's last workgroup also closes the round (no k_close; ROUND mode only,
 // never with allow_big or when k_commit_big follows); snap: its snapshot slot, or null.
-// bclose / bsnap: the same for k_commit_big (graphs with big rows, GC_BIG_CLOSE=1)
-// small: the last snapshot's frontier was small (GC_GRID_SMALL caps the grids then)
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big = 0,
-                int fused = 0, DevCtl* snap = nullptr, int tclose = 0, DevCtl* bsnap = nullptr, int bclose = 0,
-                int small = 0);
+                int fused = 0, DevCtl* snap = nullptr, int tclose = 0);
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big = 0, int fused = 0,
                DevCtl* snap = nullptr);
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s);  // see gc_hub_push_wave

@@ -707,31 +707,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_count(HubArgs a) {
     }
 }
 
-// GC_HIN_HOIST (build knob, staged in round 3): the hub index of every hub entry of a
-// thread is looked up BEFORE any hin_col store.  In the interleaved form each store may
-// alias the lookup tables as far as the compiler knows, so each entry's two dependent
-// gathers (hubpre / hubmap, then hperm) wait for the previous entry's store: up to 16 x 2
-// memory round trips per thread and tile (R-MAT-26: hin fill 51 ms for 1.5e9 entries).
-#ifndef GC_HIN_HOIST
-#define GC_HIN_HOIST 0
-#endif
-#if GC_HIN_HOIST
-__device__ __forceinline__ void hub_index_of(const HubArgs& a, const int* u, unsigned mk, int* hx) {
-    unsigned pre[GC_PER], wd[GC_PER];
-#pragma unroll
-    for (int k = 0; k < GC_PER; ++k) {
-        const bool h = (mk >> k) & 1u;
-        pre[k] = h ? a.hubpre[u[k] >> 5] : 0u;
-        wd[k] = h ? a.hubmap[u[k] >> 5] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < GC_PER; ++k) {
-        const bool h = (mk >> k) & 1u;
-        hx[k] = h ? a.hperm[pre[k] + __popc(wd[k] & ((1u << (u[k] & 31)) - 1u))] : 0;
-    }
-}
-#endif
-
 __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
     __shared__ TileLdsP S;
     const long long nt = a.T.ntiles, ns = nseg_of(a.T);
@@ -753,21 +728,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
             const ull prefix = block_excl_scan(pack3(__popc(mk), 0, 0), S.w, &total);
             record_bases(S, R, NE, nv, prefix, total, mk, 0u, 0u);
             __syncthreads();
-#if GC_HIN_HOIST
-            int hx[GC_PER];
-            long long dst[GC_PER];
-            hub_index_of(a, u, mk, hx);
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) {  // the row starts, also before any store
-                const int r = rk[k];
-                dst[k] = ((mk >> k) & 1u) ? a.hin_rp[r0 + r] + (long long)(f16(prefix, 0) + __popc(mk & ((1u << k) - 1u)) -
-                                                                          f16(S.base[r], 0))
-                                          : 0ll;
-            }
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k)
-                if ((mk >> k) & 1u) a.hin_col[dst[k]] = hx[k];
-#else
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {
                 if (!((mk >> k) & 1u)) continue;
@@ -776,7 +736,6 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
                 const unsigned bit = 1u << (u[k] & 31);
                 a.hin_col[a.hin_rp[r0 + r] + rank] = a.hperm[a.hubpre[u[k] >> 5] + __popc(a.hubmap[u[k] >> 5] & (bit - 1u))];
             }
-#endif
         } else {
             const long long s = it - nt;
             const int v = a.T.seg_row[s], j = a.T.seg_j[s];
@@ -805,20 +764,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
             const ull prefix = block_excl_scan((ull)__popc(mk), S.w, &tot);
             const long long base = a.hin_rp[v] + (long long)S.misc[0] + (long long)prefix;
             int o = 0;
-#if GC_HIN_HOIST
-            int hx[GC_PER];
-            hub_index_of(a, uu, mk, hx);
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k)
-                if ((mk >> k) & 1u) a.hin_col[base + o++] = hx[k];
-#else
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k)
                 if ((mk >> k) & 1u) {
                     const unsigned bit = 1u << (uu[k] & 31);
                     a.hin_col[base + o++] = a.hperm[a.hubpre[uu[k] >> 5] + __popc(w[k] & (bit - 1u))];
                 }
-#endif
         }
         __syncthreads();
     }

@@ -67,7 +67,6 @@ __global__ void k_b_reset(GDev g, long long round) {
     c->fsort_all = 1;
     for (int k = 0; k < 3; ++k) c->und_cnt[k] = 0;
     for (int k = 0; k < 9; ++k) c->bcnt[k] = 0;
-    c->async_abort[0] = 0;  // k_b_async's give-up flag (GC_B_ASYNC)
 }
 
 // bounded attempt with k = 0: only proposers WITH a coloured neighbour fail
@@ -377,256 +376,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
     gc_stat_add(g, GC_K_COMMIT, lsum, lacc, scratch);
 }
 
-// ------------------------------------------------------------------------------------
-// Asynchronous fold (GC_B_ASYNC=1; round 3, opt-in until measured on the GPU).  The same
-// fixpoint as the passes above, in ONE launch per round on a resident grid, with no host
-// round trip between passes: every wave owns a static slice of the round's work items --
-// light admissions and eviction times (edge-balanced wave chunks, as k_b_adm / k_b_ev) and
-// heavy admissions (a wave each, a resumable scan that stops at the first refusing or
-// undecided entry) -- and passes over its unsettled items until none is left.  An admitted
-// vertex becomes an eviction item of the same wave.  Every decision is monotone (UND ->
-// IN / OUT; eviction times only grow and are final once the evictor is admitted or there is
-// none), and the earliest unsettled item in arrival order can always settle, so the waves
-// converge without waiting on each other.  k8 and ev are read and written agent-scope (sc1).
-// A wave past the budget hands its unsettled items to the pass lists of the next slot and
-// the host's passes finish them.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ bool gc_async_stop_b(DevCtl* c, ull t0, long long budget) {
-    int stop = 0;
-    if (gc_lane() == 0) {
-        stop = __hip_atomic_load(&c->async_abort[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!stop && (long long)(wall_clock64() - t0) > budget) {
-            stop = 1;
-            if (atomicCAS(&c->async_abort[0], 0, 1) == 0) atomicAdd(&c->async_aborts, 1ull);
-        }
-    }
-    return __shfl(stop, 0, GC_WAVE) != 0;
-}
-
-// a work item is v | kind << GC_BI_SHIFT (kind 0 admission, 2 eviction time): non-negative
-// for n < 2^29 (-1 marks an empty lane), so the host runs k_b_async only below that
-#define GC_BI_SHIFT 29
-#define GC_BI_MASK ((1 << GC_BI_SHIFT) - 1)
-
-// b_adm_flag with agent-scope loads of the states and eviction times other waves write
-__device__ __forceinline__ unsigned b_adm_flag_a(const GDev& g, int vo, int u, unsigned ku, unsigned c6, int cv,
-                                                 const int* ev) {
-    if (u >= vo) return 0u;
-    const unsigned st = gc_k8_state(ku);
-    if (st == GC_JP_OUT || !b_same(g, u, ku, c6, cv)) return 0u;
-    if (st != GC_JP_IN) return 2u;
-    const int e = gc_aldi(ev + u);
-    if (e > vo) return 1u;
-    if (e >= 0 && gc_k8_state(gc_ald8(g.k8 + e)) == GC_JP_IN) return 0u;
-    return 2u;
-}
-
-struct BAsyncLds {  // one wave's rows
-    long long start[GC_WAVE];
-    unsigned flag[GC_WAVE];
-    int first[GC_WAVE];
-    int minv[GC_WAVE];
-    int v[GC_WAVE];
-    int d[GC_WAVE];
-    unsigned c6[GC_WAVE];
-    int cv[GC_WAVE];
-    int kind[GC_WAVE];
-};
-
-// one pass over the wave's light admission / eviction items l1[0, n1) (item = v | kind << GC_BI_SHIFT);
-// the unsettled ones are compacted to the front (an admitted vertex comes back as an
-// eviction item); returns their number
-__device__ int b_async_chunk_pass(GDev& g, int* l1, int n1, int* ev, BAsyncLds& s) {
-    const int lane = gc_lane();
-    int nw = 0;
-    for (int c0 = 0; c0 < n1; c0 += GC_WAVE) {
-        const int it = c0 + lane < n1 ? l1[c0 + lane] : -1;
-        const int v = it >= 0 ? (it & GC_BI_MASK) : -1;
-        const int kind = it >= 0 ? (it >> GC_BI_SHIFT) : -1;
-        const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte: only this wave changes it
-        const int d = v >= 0 ? g.deg[v] : 0;
-        int lo = 0;
-        if (kind == 0) lo = g.lcur[v];
-        else if (kind == 2) lo = g.nlow[v];
-        const int len = v >= 0 ? d - lo : 0;
-        s.start[lane] = v >= 0 ? g.rp[v] + lo : 0;
-        s.flag[lane] = 0;
-        s.first[lane] = 0x7FFFFFFF;
-        s.minv[lane] = GC_B_INF;
-        s.v[lane] = v;
-        s.d[lane] = d;
-        s.c6[lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
-        s.cv[lane] = v >= 0 ? b_cand(g, v, kv) : -1;
-        s.kind[lane] = kind;
-        const int incl = gc_wave_incl_scan(len);
-        const int excl = incl - len;
-        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
-        gc_wave_sync();
-        gc_chunk_edges_at(
-            g.col, s.start, excl, total,
-            [&](int u) { return ((ull)(unsigned)g.deg[u] << 32) | (ull)gc_ald8(g.k8 + u); },
-            [&](int o, int u, ull du, int slot) {
-                const unsigned ku = (unsigned)du & 0xFFu;
-                if (s.kind[o] == 0) {  // admission (k_b_adm)
-                    const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
-                    if (f) atomicOr(&s.flag[o], f);
-                    if (f == 2u) atomicMin(&s.first[o], slot);
-                } else {  // eviction time (k_b_ev): the earliest not-refused later higher-degree evictor
-                    if (u <= s.v[o] || gc_k8_state(ku) == GC_JP_OUT) return;
-                    if ((int)(du >> 32) <= s.d[o]) return;
-                    if (!b_same(g, u, ku, s.c6[o], s.cv[o])) return;
-                    atomicMin(&s.minv[o], u);
-                }
-            });
-        gc_wave_sync();
-        int keep = -1;  // the item that stays (-1: settled)
-        if (kind == 0) {
-            const unsigned f = s.flag[lane];
-            if (f & 1u) {
-                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
-            } else if (f & 2u) {
-                g.lcur[v] = lo + s.first[lane];
-                keep = it;
-            } else {
-                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_IN);
-                keep = v | (2 << GC_BI_SHIFT);  // admitted: its eviction time next
-            }
-        } else if (kind == 2) {
-            const int e = s.minv[lane];
-            gc_asti(ev + v, e);
-            if (e != GC_B_INF && gc_k8_state(gc_ald8(g.k8 + e)) != GC_JP_IN) keep = it;
-        }
-        const ull km = __ballot(keep >= 0);
-        if (keep >= 0) l1[nw + __popcll(km & gc_lanemask_lt())] = keep;
-        nw += __popcll(km);
-        gc_wave_sync();
-    }
-    return nw;
-}
-
-// one pass over the wave's heavy admissions l2[0, n2), one vertex at a time (the wave's
-// lanes over its row, GC_HUB_UNR entries each in flight): a refusing entry settles it OUT,
-// the first undecided entry is its new cursor, the end of the row admits it (appended to
-// l1 as an eviction item at *n1).  Returns the heavy items left.
-__device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, int* ev) {
-    const int lane = gc_lane();
-    int nw = 0;
-    for (int i = 0; i < n2; ++i) {
-        const int v = l2[i];
-        const unsigned kv = g.k8[v];
-        const unsigned c6 = gc_k8_cand(kv);
-        const int cv = b_cand(g, v, kv);
-        const int d = g.deg[v];
-        const long long base = g.rp[v];
-        int pos = g.lcur[v];
-        bool refused = false;
-        int pend = -1;
-        while (pos < d && !refused && pend < 0) {
-            int u[GC_HUB_UNR];
-            unsigned f[GC_HUB_UNR];
-#pragma unroll
-            for (int k = 0; k < GC_HUB_UNR; ++k) {
-                const int e = pos + k * GC_WAVE + lane;
-                u[k] = e < d ? g.col[base + e] : -1;
-            }
-#pragma unroll
-            for (int k = 0; k < GC_HUB_UNR; ++k) f[k] = u[k] >= 0 ? b_adm_flag_a(g, v, u[k], gc_ald8(g.k8 + u[k]), c6, cv, ev) : 0u;
-#pragma unroll
-            for (int k = 0; k < GC_HUB_UNR; ++k) {
-                if (__ballot(f[k] == 1u)) refused = true;
-                const ull mb = __ballot(f[k] == 2u);
-                if (mb && pend < 0) pend = pos + k * GC_WAVE + __builtin_ctzll(mb);
-            }
-            pos += GC_HUB_UNR * GC_WAVE;
-        }
-        if (refused) {
-            if (lane == 0) gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
-        } else if (pend >= 0) {
-            if (lane == 0) {
-                g.lcur[v] = pend;
-                l2[nw] = v;
-            }
-            ++nw;
-        } else {
-            if (lane == 0) {
-                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_IN);
-                l1[*n1] = v | (2 << GC_BI_SHIFT);
-            }
-            ++*n1;
-        }
-        gc_wave_sync();
-    }
-    return nw;
-}
-
-// pass `pass` of the round as one asynchronous launch: reads the three lists of slot
-// pass % 3, spills to slot (pass + 1) % 3, uses the arrays of slot (pass + 2) % 3 as the
-// waves' scratch and clears that slot's counts (as k_b_ev does)
-__global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev, int pass, long long budget) {
-    DevCtl* c = g.ctl;
-    const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
-    __shared__ BAsyncLds s_w[GC_WAVES_PER_BLOCK];
-    const int lane = gc_lane();
-    const int w = threadIdx.x / GC_WAVE;
-    const long long nA = (long long)*b_cnt(c, 0, rs), nH = (long long)*b_cnt(c, 1, rs), nE = (long long)*b_cnt(c, 2, rs);
-    const long long T = nA + nH + nE;
-    if (T > g.n) {  // never expected: report, touch nothing
-        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&c->loop_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 3) *b_cnt(c, threadIdx.x, zs) = 0ull;
-    const ull t0 = wall_clock64();
-    budget += 2 * T;
-    const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
-    const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
-    const long long a = T * wid / W, b = T * (wid + 1) / W;
-    if (a >= b) return;
-    int* l1 = B.l[0][zs] + a;  // light admissions and eviction times
-    int* l2 = B.l[1][zs] + a;  // heavy admissions
-    int n1 = 0, n2 = 0;
-    for (long long i0 = a; i0 < b; i0 += GC_WAVE) {
-        const long long i = i0 + lane;
-        int v = -1, kind = -1;
-        if (i < b) {
-            if (i < nA) { v = B.l[0][rs][i]; kind = 0; }
-            else if (i < nA + nH) { v = B.l[1][rs][i - nA]; kind = 1; }
-            else { v = B.l[2][rs][i - nA - nH]; kind = 2; }
-        }
-        const ull m1 = __ballot(kind == 0 || kind == 2), m2 = __ballot(kind == 1);
-        if (kind == 0 || kind == 2) l1[n1 + __popcll(m1 & gc_lanemask_lt())] = v | (kind << GC_BI_SHIFT);
-        if (kind == 1) l2[n2 + __popcll(m2 & gc_lanemask_lt())] = v;
-        n1 += __popcll(m1);
-        n2 += __popcll(m2);
-    }
-    gc_wave_sync();
-    bool stop = false;
-    int idle = 0;
-    while (n1 + n2 > 0) {
-        const int before = n1 + n2;
-        n1 = b_async_chunk_pass(g, l1, n1, ev, s_w[w]);
-        if (n2) n2 = b_async_heavy_pass(g, l2, n2, l1, &n1, ev);
-        if (n1 + n2 == 0) break;
-        if ((stop = gc_async_stop_b(c, t0, budget))) break;
-        if (n1 + n2 == before) {
-            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
-        } else {
-            idle = 0;
-        }
-    }
-    if (!stop) return;
-    // hand the unsettled items to the host's passes (slot ws), by kind
-    for (int i0 = 0; i0 < n1; i0 += GC_WAVE) {
-        const int it = i0 + lane < n1 ? l1[i0 + lane] : -1;
-        const int kind = it >= 0 ? (it >> GC_BI_SHIFT) : -1;
-        gc_wave_append(kind == 0, it & GC_BI_MASK, B.l[0][ws], b_cnt(c, 0, ws));
-        gc_wave_append(kind == 2, it & GC_BI_MASK, B.l[2][ws], b_cnt(c, 2, ws));
-    }
-    for (int i0 = 0; i0 < n2; i0 += GC_WAVE) {
-        const int v = i0 + lane < n2 ? l2[i0 + lane] : -1;
-        gc_wave_append(v >= 0, v, B.l[1][ws], b_cnt(c, 1, ws));
-    }
-}
-
+// (Round 3's asynchronous fold -- the round's passes in one launch on a resident grid,
+// GC_B_ASYNC=1 -- measured R-MAT-24 855.6 -> 1036.9 ms in round 4, profiles/r04/c: removed.)
 
 struct RunB {
     gc_graph* g;
@@ -699,22 +450,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     int* const wl[9] = {g->undL[0], g->undL[1], g->undL[2], g->seeds[0], g->seeds[1], g->bigw,
                         g->undH[0], g->undH[1], g->undH[2]};
     for (int k = 0; k < 9; ++k) B.l[k / 3][k % 3] = wl[k];
-    // GC_B_ASYNC=1: the round's fold as one asynchronous launch (k_b_async) on a resident grid
-    // (CUs x 2 workgroups), the host's passes only for what it hands back; budget per launch
-    // GC_ASYNC_BUDGET_US (20 ms) plus 20 ns per work item
-    int b_async_grid = 0;
-    long long b_async_budget = 0;
-    // (its work items pack the vertex in GC_BI_SHIFT bits: n < 2^29)
-    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0 && g->n < (1ll << GC_BI_SHIFT)) {
-        int cus = 0, rate_khz = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
-            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
-            rate_khz > 0) {
-            b_async_grid = 2 * cus;
-            const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
-            b_async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
-        }
-    }
     std::vector<RoundRec> recs;
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;
@@ -747,12 +482,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
                 hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
         };
-        if (b_async_grid > 0) {  // pass 0 as one asynchronous launch; the host's passes resume at pass 1
-            hipLaunchKernelGGL(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, 0, b_async_budget);
-            passes = 1;
-        } else {
-            enqueue_passes(std::max(2ll, std::min(prev_passes, 24ll)));
-        }
+        enqueue_passes(std::max(2ll, std::min(prev_passes, 24ll)));
         if ((rc = R.sync())) return rc;
         if (r > 0) {
             recs.push_back(RoundRec{prevU, prevU, prev_maxmex, (long long)h.dcnt, 0, prev_passes});
@@ -764,7 +494,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             break;
         }
         if (h.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
-        if (h.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
         const long long maxmex = h.maxmex;
         if (h.kbound >= 0 && h.failcnt > 0) {  // state at the round start is returned
             recs.push_back(RoundRec{U, U, maxmex, 0, 0, 0});

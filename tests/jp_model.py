@@ -12,7 +12,7 @@ random interleaving of waves, with every read of another vertex's state taken, a
 from an older snapshot, and colours whole graphs round by round (init, seed, E1 re-seeds as
 oracle/gcolor_oracle.c).  tests/test_jp_model.py checks it equals the oracle's variant A bit
 for bit: "staleness delays a decision, never changes it", the argument DESIGN §5 makes for
-the asynchronous JP -- with and without hubs (GC_ASYNC=2 is the hub-less case).
+the asynchronous JP -- with hubs (the engine's case) and without (the lights-only rules).
 """
 import random
 

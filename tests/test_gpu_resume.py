@@ -94,7 +94,7 @@ def test_hybrid_threads(switch_below):
 
 
 
-@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}, {"GC_ASYNC": "2"}], ids=["fused", "unfused", "async_nohub"])
+@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}], ids=["fused", "unfused"])
 def test_commit_stage_overflow_under_ticket_close(env, monkeypatch):
     """tests/commit_cases.py: 32768 winners in the first 2048 wave chunks of a 16M-vertex graph
     (frontier < n/256: the commit closes its own round with arrival tickets), each claiming 40
@@ -118,7 +118,7 @@ def test_commit_stage_overflow_under_ticket_close(env, monkeypatch):
         assert dg.validate() == (0, 0)
 
 
-@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}, {"GC_ASYNC": "2"}], ids=["fused", "unfused", "async_nohub"])
+@pytest.mark.parametrize("env", [{}, {"GC_FUSE": "0"}], ids=["fused", "unfused"])
 def test_commit_stage_overflow_tree(env, monkeypatch):
     """The same corner from a plain colouring (no resume; tests/commit_cases.py): a fanout-61
     tree padded to 2^26 vertices.  Round 2's frontier is its 234,423 level-3 vertices (< n/256:

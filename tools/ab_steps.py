@@ -6,7 +6,7 @@ effects fall on every configuration alike.  Every configuration's colouring must
 first one's (colours, rounds): a knob that changes the result is reported and stops the run.
 
   python tools/ab_steps.py WORKLOAD REPS NAME=VAR:val+VAR:val ...   ("base" = no variables)
-  e.g. tools/ab_steps.py rmat24 5 base async_resolve=GC_ASYNC_RESOLVE:1
+  e.g. tools/ab_steps.py rmat24 5 base c8=GC_VALIDATE_C8:1
 
 Prints one line per step and a summary (median / min ms per configuration, and the median's
 ratio to the first configuration).  Compile-time variants need a process each (GC_LIB_PATH).

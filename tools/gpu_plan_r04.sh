@@ -19,6 +19,16 @@ case ${1:-} in
                  ab:mesh512:4:base,graphs=GC_GRAPHS:1,async2=GC_ASYNC:2
                  env:AB_VARIANT=B ab:rmat24:3:base,basync=GC_B_ASYNC:1 env:AB_VARIANT=
                  abl:rmat24:4:2:base=-,marks4=variants/marks4/libgcolor.so,claim4=variants/claim4/libgcolor.so,all4=variants/all4/libgcolor.so,hinhoist=variants/hinhoist/libgcolor.so,closeint=variants/close_interleaved/libgcolor.so,closecall=variants/close_call/libgcolor.so,tile8=variants/tile8/libgcolor.so) ;;
-  *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
+  # d: variant B's profile (PMC of this build), the tile size on the other workloads, the
+  #    validation from the byte mirror, and the hybrid's switch point at P = 1
+  d) exec_steps=("profile:rmat24:--variant,B"
+                 abl:rmat26:3:1:base=-,tile8=variants/tile8/libgcolor.so,base2=-
+                 abl:uniform10M:6:1:base=-,tile8=variants/tile8/libgcolor.so
+                 abl:mesh512:3:1:base=-,tile8=variants/tile8/libgcolor.so
+                 ab:rmat26:3:base,c8=GC_VALIDATE_C8:1 ab:rmat24:5:base,c8=GC_VALIDATE_C8:1
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,1000000000,--steps,3,--warmup,1"
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,262144,--steps,3,--warmup,1"
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,16384,--steps,3,--warmup,1") ;;
+  *) echo "usage: $0 a|b|c|d" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
