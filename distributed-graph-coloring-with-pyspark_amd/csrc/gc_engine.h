@@ -103,6 +103,8 @@ struct gc_graph {
     unsigned* hubmap = nullptr;   // bit per vertex: hid >= 0
     unsigned* hubpre = nullptr;   // hubs in the words before (id-order index of a hub = hubpre + rank in its word)
     int* hperm = nullptr;         // id-order index -> hub index (rank order)
+    ull* hb_bits = nullptr;       // hub-transpose build only: bit per entry (col[e] is a hub)
+    long long* hb_wpre = nullptr; //   and the exclusive prefix of the words' popcounts
 };
 
 // caching allocator (gc_alloc.hip): every device / pinned-host buffer of the library
@@ -123,8 +125,9 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
 int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8 = nullptr);
 // symmetric graphs: hub transpose (hin_rp / hin_col: the hubs listed in each row) and the
 // lower-rank hubs of every hub row (hlow counts -> klow[x]); hubmap / hid / hub_v ready
-int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow);
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow);
 int gc_hub_transpose_fill(gc_graph* g, long long H);
+void gc_hub_bits_free(gc_graph* g);
 
 void gc_set_error(const char* fmt, ...);
 

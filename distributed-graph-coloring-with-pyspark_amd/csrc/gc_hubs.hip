@@ -267,18 +267,19 @@ int build(gc_graph* g, int T, int W) {
     long long E = 0, EL = 0;
     const bool sym = (g->flags & GC_GRAPH_SYMMETRIC) != 0;
     long long* klow = nullptr;
+    GC_HIP(gc_dmalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
     if (sym) {
-        // symmetric: every row filtered for its hub entries (gc_prep.hip, edge-balanced tiles):
-        // hin counts into pos, each hub row's lower-rank hubs (a prefix of its hin row) into klow
+        // symmetric: every row filtered for its hub entries (gc_prep.hip, a rank structure over
+        // the entries): hin_rp directly, each hub row's lower-rank hubs (a prefix of its hin
+        // row) into klow
         GC_HIP(gc_dmalloc((void**)&klow, sizeof(long long) * (size_t)(H + 1)));
-        if ((rc = gc_hub_transpose_sym(g, H, pos, klow))) { gc_dfree(pos); gc_dfree(klow); return rc; }
+        if ((rc = gc_hub_transpose_sym(g, H, g->hin_rp, klow))) { gc_dfree(pos); gc_dfree(klow); return rc; }
     } else {
         // hub transpose: reuse pos as the per-target counter
         GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
         hipLaunchKernelGGL(k_hub_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, (ull*)pos);
+        if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { gc_dfree(pos); return rc; }
     }
-    GC_HIP(gc_dmalloc((void**)&g->hin_rp, sizeof(long long) * (size_t)(n + 1)));
-    if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { gc_dfree(pos); gc_dfree(klow); return rc; }
     GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
     pc.mark("hin count", s);
     hipMemGetInfo(&freeb, &totalb);
@@ -287,6 +288,7 @@ int build(gc_graph* g, int T, int W) {
     if (need2 > 0.6 * (double)freeb) {
         gc_dfree(pos);
         gc_dfree(klow);
+        gc_hub_bits_free(g);
         gc_hubs_free(g);
         g->hub_t = T;
         g->nhub = 0;
@@ -371,6 +373,7 @@ void gc_hubs_free(gc_graph* g) {
                     g->hch_rp, g->hch_own, g->hkcnt, g->hk};
     for (void* p : ptrs)
         if (p) gc_dfree(p);
+    gc_hub_bits_free(g);
     g->hubpre = nullptr;
     g->hperm = nullptr;
     g->hid = g->hub_v = g->hin_col = g->hlow_col = g->hcur = g->hpc = g->hpend[0] = g->hpend[1] = nullptr;

@@ -604,174 +604,112 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
 // hubs each row u lists (hin, pushed into by u's commits) are u's entries that are hubs --
 // a filter of every row, no atomics on targets.  A hub row's lower-rank hubs (hlow) are the
 // entries of its hin row that lie in its low part: a prefix of that row (klow of them).
-// ------------------------------------------------------------------------------------
-struct HubArgs {
-    Tiles T;
-    const int* col;
-    const int* nlow;
-    const int* hid;
-    const unsigned* hubmap;
-    const unsigned* hubpre;  // hub index of u = hperm[hubpre[u >> 5] + rank of u in its word]
-    const int* hperm;
-    long long* hin_cnt;  // count pass: per row
-    long long* klow;     // count pass: per hub
-    const long long* hin_rp;  // fill pass
-    int* hin_col;
-    ull* seg_aux;        // per segment: hub entries (count pass)
-};
+//
+// Round 4: a rank structure over the entries instead of edge-balanced tiles.  Bit e of
+// `hb_bits` says whether entry e (col[e]) is a hub; `hb_wpre` is the exclusive prefix of the
+// words' popcounts, so rank(e) = the hub entries before position e = wpre[e/64] +
+// popc(bits[e/64] below e).  Then hin_rp[u] = rank(rp[u]) (rows in order, entries in row
+// order: the same hin rows as a per-row filter), klow[x] = rank(rp[v] + nlow[v]) -
+// rank(rp[v]) for hub v = hub_v[x], and entry e goes to hin_col[rank(e)].  Two coalesced
+// streams over col (bits; fill) instead of two passes of LDS-staged tiles with a row search
+// per thread (round 3: R-MAT-26 hin count 24 ms + fill 51 ms, ~0.04 of the HBM peak).
+// Per entry: 4 B of col (both passes) + one hubmap gather (bits pass); per hub entry: 4 B
+// written + the hub-index gathers (hubpre / hubmap / hperm: 2 x n/8 + 4 H bytes, L2/MALL).
 
-// hub entries of this thread's tile entries (mask) and those inside their row's low part
-template <class Lds>
-__device__ __forceinline__ void hub_masks(const HubArgs& a, const Lds& S, int nv, const int* u, const int* rk,
-                                          unsigned* mk, unsigned* ml) {
-    const int j0 = threadIdx.x * GC_PER;
-    unsigned words[GC_PER];
+// bits of 64 consecutive words per wave and iteration; lane k keeps word w0 + k (coalesced
+// stores), 8 entry loads per lane in flight
+__global__ void __launch_bounds__(GC_BLOCK) k_hbit(const int* col, long long nnz, long long n, const unsigned* hubmap,
+                                                  ull* bits, long long* wcnt, long long nw) {
+    const int lane = gc_lane();
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE;
+    const long long nwaves = (long long)gridDim.x * blockDim.x / GC_WAVE;
+    for (long long w0 = wave * GC_WAVE; w0 < nw; w0 += nwaves * GC_WAVE) {
+        ull mine = 0;
+#pragma unroll 1
+        for (int k0 = 0; k0 < GC_WAVE; k0 += 8) {
+            int u[8];
+            unsigned hw[8];
 #pragma unroll
-    for (int k = 0; k < GC_PER; ++k) words[k] = k < nv ? a.hubmap[u[k] >> 5] : 0u;
-    unsigned m = 0, l = 0;
-#pragma unroll
-    for (int k = 0; k < GC_PER; ++k) {
-        const bool h = k < nv && ((words[k] >> (u[k] & 31)) & 1u);
-        m |= (h ? 1u : 0u) << k;
-        const int r = rk[k];
-        const bool low = h && (j0 + k - S.off[r]) < (int)S.key[r];  // index in row < nlow
-        l |= (low ? 1u : 0u) << k;
-    }
-    *mk = m;
-    *ml = l;
-}
-
-__global__ void __launch_bounds__(GC_BLOCK) k_hin_count(HubArgs a) {
-    __shared__ TileLds S;
-    const long long nt = a.T.ntiles, ns = nseg_of(a.T);
-    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
-        if (it < nt) {
-            int r0, NE;
-            long long eb;
-            bool hl;
-            const int R = tile_rows(a.T, it, S, &r0, &eb, &NE, &hl);
-            if (R == 0) continue;
-            for (int i = threadIdx.x; i < R; i += blockDim.x) {
-                S.key[i] = (unsigned)a.nlow[r0 + i];
-                S.aux[i] = a.hid[r0 + i];
-            }
-            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = a.col[eb + i];
-            __syncthreads();
-            int u[GC_PER], rk[GC_PER];
-            const int nv = thread_entries(S, R, NE, u, rk);
-            unsigned mk = 0, ml = 0;
-            hub_masks(a, S, nv, u, rk, &mk, &ml);
-            ull total;
-            const ull prefix = block_excl_scan(pack3(__popc(mk), __popc(ml), 0), S.w, &total);
-            record_bases(S, R, NE, nv, prefix, total, mk, ml, 0u);
-            __syncthreads();
-            for (int r = threadIdx.x; r < R; r += blockDim.x) {
-                if (hl && r == R - 1) continue;
-                const ull b = S.base[r], b1 = S.base[r + 1];
-                a.hin_cnt[r0 + r] = f16(b1, 0) - f16(b, 0);
-                if (S.aux[r] >= 0) a.klow[S.aux[r]] = f16(b1, 1) - f16(b, 1);
-            }
-        } else {
-            const long long s = it - nt;
-            const int v = a.T.seg_row[s], j = a.T.seg_j[s];
-            const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
-            const long long e0 = rs + (long long)j * GC_SEG;
-            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
-            const int nl = a.nlow[v];
-            ull ck = 0, cl = 0;
-            unsigned w[GC_PER];
-            int uu[GC_PER];
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) {
-                const int i = threadIdx.x + k * GC_BLOCK;
-                uu[k] = i < len ? a.col[e0 + i] : 0;
+            for (int k = 0; k < 8; ++k) {
+                const long long e = (w0 + k0 + k) * GC_WAVE + lane;
+                u[k] = e < nnz ? col[e] : -1;
             }
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) w[k] = threadIdx.x + k * GC_BLOCK < len ? a.hubmap[uu[k] >> 5] : 0u;
+            for (int k = 0; k < 8; ++k) hw[k] = (u[k] >= 0 && (long long)u[k] < n) ? hubmap[u[k] >> 5] : 0u;
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) {
-                const int i = threadIdx.x + k * GC_BLOCK;
-                const bool h = i < len && ((w[k] >> (uu[k] & 31)) & 1u);
-                ck += h;
-                cl += h && ((long long)j * GC_SEG + i < nl);
-            }
-            const ull tot = block_sum(pack3((unsigned)ck, (unsigned)cl, 0), S.w);
-            if (threadIdx.x == 0) {
-                a.seg_aux[s] = tot;
-                atomicAdd((ull*)&a.hin_cnt[v], (ull)f16(tot, 0));
-                const int x = a.hid[v];
-                if (x >= 0 && f16(tot, 1)) atomicAdd((ull*)&a.klow[x], (ull)f16(tot, 1));
+            for (int k = 0; k < 8; ++k) {
+                const ull m = __ballot(u[k] >= 0 && ((hw[k] >> (u[k] & 31)) & 1u));
+                if (lane == k0 + k) mine = m;
             }
         }
-        __syncthreads();
+        const long long w = w0 + lane;
+        if (w < nw) {
+            bits[w] = mine;
+            wcnt[w] = (long long)__popcll(mine);
+        }
     }
 }
 
-__global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(HubArgs a) {
-    __shared__ TileLdsP S;
-    const long long nt = a.T.ntiles, ns = nseg_of(a.T);
-    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
-        if (it < nt) {
-            int r0, NE;
-            long long eb;
-            bool hl;
-            const int R = tile_rows(a.T, it, S, &r0, &eb, &NE, &hl);
-            if (R == 0) continue;
-            for (int i = threadIdx.x; i < R; i += blockDim.x) S.key[i] = 0x7FFFFFFFu;  // low part unused here
-            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = a.col[eb + i];
-            __syncthreads();
-            int u[GC_PER], rk[GC_PER];
-            const int nv = thread_entries(S, R, NE, u, rk);
-            unsigned mk = 0, ml = 0;
-            hub_masks(a, S, nv, u, rk, &mk, &ml);
-            ull total;
-            const ull prefix = block_excl_scan(pack3(__popc(mk), 0, 0), S.w, &total);
-            record_bases(S, R, NE, nv, prefix, total, mk, 0u, 0u);
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) {
-                if (!((mk >> k) & 1u)) continue;
-                const int r = rk[k];
-                const unsigned rank = f16(prefix, 0) + __popc(mk & ((1u << k) - 1u)) - f16(S.base[r], 0);
-                const unsigned bit = 1u << (u[k] & 31);
-                a.hin_col[a.hin_rp[r0 + r] + rank] = a.hperm[a.hubpre[u[k] >> 5] + __popc(a.hubmap[u[k] >> 5] & (bit - 1u))];
-            }
-        } else {
-            const long long s = it - nt;
-            const int v = a.T.seg_row[s], j = a.T.seg_j[s];
-            const long long rs = a.T.rp[v], d = a.T.rp[v + 1] - rs;
-            const long long e0 = rs + (long long)j * GC_SEG;
-            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
-            if (threadIdx.x < GC_WAVE) {
-                ull p[3];
-                seg_sums(a.seg_aux, s - j, s, p);
-                if (threadIdx.x == 0) S.misc[0] = p[0];
-            }
-            // this thread's entries are CONTIGUOUS here ([16t, 16t+16)): ranks follow row order
-            const int j0 = threadIdx.x * GC_PER;
-            int nv = len - j0;
-            nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
-            int uu[GC_PER];
-            unsigned w[GC_PER];
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) uu[k] = k < nv ? a.col[e0 + j0 + k] : 0;
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) w[k] = k < nv ? a.hubmap[uu[k] >> 5] : 0u;
-            unsigned mk = 0;
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) mk |= ((k < nv && ((w[k] >> (uu[k] & 31)) & 1u)) ? 1u : 0u) << k;
-            ull tot;
-            const ull prefix = block_excl_scan((ull)__popc(mk), S.w, &tot);
-            const long long base = a.hin_rp[v] + (long long)S.misc[0] + (long long)prefix;
-            int o = 0;
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k)
-                if ((mk >> k) & 1u) {
-                    const unsigned bit = 1u << (uu[k] & 31);
-                    a.hin_col[base + o++] = a.hperm[a.hubpre[uu[k] >> 5] + __popc(w[k] & (bit - 1u))];
-                }
+__device__ __forceinline__ long long hb_rank(const ull* bits, const long long* wpre, long long e) {
+    const long long w = e >> 6;
+    const int b = (int)(e & 63);
+    return wpre[w] + (long long)__popcll(bits[w] & ((1ull << b) - 1ull));
+}
+
+// hin_rp[u] = rank(rp[u]) for u in [0, n] (hin_rp[n] = E); klow of every hub row
+__global__ void __launch_bounds__(GC_BLOCK) k_hin_rank(const long long* rp, long long n, const ull* bits,
+                                                      const long long* wpre, const int* nlow, const int* hid,
+                                                      long long* hin_rp, long long* klow) {
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (long long)gridDim.x * blockDim.x) {
+        const long long e = rp[v];
+        const long long r = hb_rank(bits, wpre, e);
+        hin_rp[v] = r;
+        if (v < n) {
+            const int x = hid[v];
+            if (x >= 0) klow[x] = hb_rank(bits, wpre, e + nlow[v]) - r;
         }
-        __syncthreads();
+    }
+}
+
+// hin_col[rank(e)] = hub index of col[e] for every hub entry e: a wave per 64 words, lane k
+// holding word w0 + k's bits and prefix, 8 words' entries in flight per step
+__global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(const int* col, long long nw, const ull* bits,
+                                                      const long long* wpre, const unsigned* hubmap,
+                                                      const unsigned* hubpre, const int* hperm, int* hin_col) {
+    const int lane = gc_lane();
+    const ull lt = gc_lanemask_lt();
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE;
+    const long long nwaves = (long long)gridDim.x * blockDim.x / GC_WAVE;
+    for (long long w0 = wave * GC_WAVE; w0 < nw; w0 += nwaves * GC_WAVE) {
+        const ull myb = w0 + lane < nw ? bits[w0 + lane] : 0ull;
+        const long long myp = w0 + lane < nw ? wpre[w0 + lane] : 0ll;
+#pragma unroll 1
+        for (int k0 = 0; k0 < GC_WAVE; k0 += 8) {
+            ull mk[8];
+            long long base[8];
+            int u[8];
+            bool on[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                mk[k] = __shfl(myb, k0 + k, GC_WAVE);
+                base[k] = __shfl(myp, k0 + k, GC_WAVE);
+                on[k] = (mk[k] >> lane) & 1ull;
+                u[k] = on[k] ? col[(w0 + k0 + k) * GC_WAVE + lane] : 0;
+            }
+            unsigned pre[8], hw[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                pre[k] = on[k] ? hubpre[u[k] >> 5] : 0u;
+                hw[k] = on[k] ? hubmap[u[k] >> 5] : 0u;
+            }
+            int x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                x[k] = on[k] ? hperm[pre[k] + __popc(hw[k] & ((1u << (u[k] & 31)) - 1u))] : 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (on[k]) hin_col[base[k] + __popcll(mk[k] & lt)] = x[k];
+        }
     }
 }
 
@@ -924,52 +862,59 @@ int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8) {
     return GC_OK;
 }
 
-// the count pass (hubmap / hubpre / hperm ready): hin_cnt (n + 1, zeroed here) and klow (H + 1)
-int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_cnt, long long* klow) {
+// the count pass (hubmap / hubpre / hperm / hid ready): the entry bits and their word
+// prefix (kept on g until the fill), hin_rp (n + 1: the exclusive prefix itself) and klow
+// (H + 1, zeroed here)
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow) {
     const hipStream_t s = g->stream;
-    int rc = gc_build_tiling(g);
-    if (rc) return rc;
-    GC_HIP(hipMemsetAsync(hin_cnt, 0, sizeof(long long) * (size_t)(g->n + 1), s));
+    const long long n = g->n, nnz = g->nnz;
+    const long long nw = (nnz + 63) / 64;
+    gc_hub_bits_free(g);
+    GC_HIP(gc_dmalloc((void**)&g->hb_bits, sizeof(ull) * (size_t)(nw + 1)));
+    GC_HIP(gc_dmalloc((void**)&g->hb_wpre, sizeof(long long) * (size_t)(nw + 1)));
+    long long* wcnt = nullptr;
+    GC_HIP(gc_dmalloc((void**)&wcnt, sizeof(long long) * (size_t)(nw + 1)));
+    GC_HIP(hipMemsetAsync(g->hb_bits + nw, 0, sizeof(ull), s));  // rank(nnz) may read word nw
+    GC_HIP(hipMemsetAsync(wcnt + nw, 0, sizeof(long long), s));
     GC_HIP(hipMemsetAsync(klow, 0, sizeof(long long) * (size_t)(H + 1), s));
-    HubArgs a;
-    a.T = tiles_of(g);
-    a.col = g->col;
-    a.nlow = g->nlow;
-    a.hid = g->hid;
-    a.hubmap = g->hubmap;
-    a.hubpre = g->hubpre;
-    a.hperm = g->hperm;
-    a.hin_cnt = hin_cnt;
-    a.klow = klow;
-    a.hin_rp = nullptr;
-    a.hin_col = nullptr;
-    a.seg_aux = g->seg_aux;
-    if (g->nnz > 0) hipLaunchKernelGGL(k_hin_count, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, s, a);
+    const int grid = (int)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 8192));
+    if (nw > 0)
+        hipLaunchKernelGGL(k_hbit, dim3(grid), dim3(GC_BLOCK), 0, s, (const int*)g->col, nnz, n,
+                           (const unsigned*)g->hubmap, g->hb_bits, wcnt, nw);
+    int rc = scan_ll(wcnt, g->hb_wpre, nw + 1, s);
+    gc_dfree(wcnt);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_hin_rank, dim3(small_grid(n + 1)), dim3(GC_BLOCK), 0, s, (const long long*)g->rp, n,
+                       (const ull*)g->hb_bits, (const long long*)g->hb_wpre, (const int*)g->nlow, (const int*)g->hid,
+                       hin_rp, klow);
     GC_HIP(hipGetLastError());
     return GC_OK;
 }
 
-// fill pass (hin_rp / hin_col allocated), then hlow rows as klow-prefixes (hlow_rp ready)
+// fill pass (hin_rp / hin_col allocated), then hlow rows as klow-prefixes (hlow_rp ready);
+// the entry bits are released
 int gc_hub_transpose_fill(gc_graph* g, long long H) {
     const hipStream_t s = g->stream;
-    HubArgs a;
-    a.T = tiles_of(g);
-    a.col = g->col;
-    a.nlow = g->nlow;
-    a.hid = g->hid;
-    a.hubmap = g->hubmap;
-    a.hubpre = g->hubpre;
-    a.hperm = g->hperm;
-    a.hin_cnt = nullptr;
-    a.klow = nullptr;
-    a.hin_rp = g->hin_rp;
-    a.hin_col = g->hin_col;
-    a.seg_aux = g->seg_aux;
-    if (g->nnz > 0) hipLaunchKernelGGL(k_hin_fill, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, s, a);
+    const long long nw = (g->nnz + 63) / 64;
+    if (!g->hb_bits || !g->hb_wpre) { gc_set_error("gc_hub_transpose_fill: no entry bits"); return GC_EINVAL; }
+    const int grid = (int)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 8192));
+    if (nw > 0)
+        hipLaunchKernelGGL(k_hin_fill, dim3(grid), dim3(GC_BLOCK), 0, s, (const int*)g->col, nw, (const ull*)g->hb_bits,
+                           (const long long*)g->hb_wpre, (const unsigned*)g->hubmap, (const unsigned*)g->hubpre,
+                           (const int*)g->hperm, g->hin_col);
     if (H > 0)
         hipLaunchKernelGGL(k_hlow_copy, dim3((int)std::min<long long>((H + 3) / 4, 8192)), dim3(GC_BLOCK), 0, s,
                            (const int*)g->hub_v, H, (const long long*)g->hin_rp, (const int*)g->hin_col,
                            (const long long*)g->hlow_rp, g->hlow_col);
     GC_HIP(hipGetLastError());
+    GC_HIP(hipStreamSynchronize(s));  // the bits go back to the cache idle
+    gc_hub_bits_free(g);
     return GC_OK;
+}
+
+void gc_hub_bits_free(gc_graph* g) {
+    if (g->hb_bits) gc_dfree(g->hb_bits);
+    if (g->hb_wpre) gc_dfree(g->hb_wpre);
+    g->hb_bits = nullptr;
+    g->hb_wpre = nullptr;
 }

@@ -21,7 +21,8 @@ case ${1:-} in
                  abl:rmat24:4:2:base=-,marks4=variants/marks4/libgcolor.so,claim4=variants/claim4/libgcolor.so,all4=variants/all4/libgcolor.so,hinhoist=variants/hinhoist/libgcolor.so,closeint=variants/close_interleaved/libgcolor.so,closecall=variants/close_call/libgcolor.so,tile8=variants/tile8/libgcolor.so) ;;
   # d: variant B's profile (PMC of this build), the tile size on the other workloads, the
   #    validation from the byte mirror, and the hybrid's switch point at P = 1
-  d) exec_steps=("profile:rmat24:--variant,B"
+  d) exec_steps=(file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING=
+                 "profile:rmat24:--variant,B"
                  abl:rmat26:3:1:base=-,tile8=variants/tile8/libgcolor.so,base2=-
                  abl:uniform10M:6:1:base=-,tile8=variants/tile8/libgcolor.so
                  abl:mesh512:3:1:base=-,tile8=variants/tile8/libgcolor.so
