@@ -91,7 +91,7 @@ struct gc_graph {
     uint64_t part_seed = 0;
     // edge-balanced tiling of the CSR (gc_prep.hip): whole-row tiles of <= GC_TW rows +
     // entries, rows longer than GC_TH split into GC_SEG-entry segments
-    unsigned char* kb = nullptr;  // min(deg, 255): the rank key's byte the partition gathers first
+    unsigned char* kb = nullptr;  // gc_deg_code(deg): the rank key's byte the partition gathers first
     int* tile_r0 = nullptr;       // [ntiles + 1] first row of each tile
     long long ntiles = 0;
     int* seg_row = nullptr;       // heavy segments: row, index within the row

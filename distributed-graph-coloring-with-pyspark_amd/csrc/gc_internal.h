@@ -388,6 +388,21 @@ __device__ __forceinline__ unsigned gc_c6_of(long long c) { return c >= 62 ? GC_
 __device__ __forceinline__ unsigned gc_k8_cand(unsigned k) { return k >> 2; }
 __device__ __forceinline__ unsigned gc_k8_state(unsigned k) { return k & 3u; }
 
+// The rank partition's first gather per entry (gc_prep.hip): a monotone byte code of the
+// degree -- exact below 32, then 8 equal-width buckets per octave (d in [2^k, 2^(k+1)) ->
+// 32 + 8 (k - 5) + floor(8 (d - 2^k) / 2^k), at most 239 for d < 2^31).  Different codes
+// order two degrees; equal codes >= 32 need the degrees themselves.  Round 3 used min(deg,
+// 255), so every entry between two vertices of degree >= 255 gathered the 4-byte degree too:
+// 52% of R-MAT-22's entries, against 7% with this code (numpy R-MAT, tools-free count).
+#define GC_DEG_CODE_EXACT 32u
+__host__ __device__ __forceinline__ unsigned gc_deg_code(long long d) {
+    if (d < (long long)GC_DEG_CODE_EXACT) return d < 0 ? 0u : (unsigned)d;
+    const int lz = 63 - __builtin_clzll((ull)d);  // floor(log2 d) >= 5
+    const ull rem = (ull)d - (1ull << lz);
+    const unsigned c = GC_DEG_CODE_EXACT + 8u * (unsigned)(lz - 5) + (unsigned)((rem * 8ull) >> lz);
+    return c < 255u ? c : 255u;
+}
+
 // rank order of coloring.py:64 (stable sort by deg of a file-ordered group): (deg, pos) asc
 __device__ __forceinline__ bool gc_rank_lt(int du, int u, int dv, int v) {
     return du < dv || (du == dv && u < v);

@@ -2840,14 +2840,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_own_front(GDev g, GLists L, 
 // ------------------------------------------------------------------------------------
 // graph helpers
 // ------------------------------------------------------------------------------------
-// deg, its byte key kb = min(deg, 255) (the rank partition gathers it first: gc_prep.hip),
+// deg, its byte key kb = gc_deg_code(deg) (the rank partition gathers it first: gc_prep.hip),
 // the max degree; *bad counts violations of the CSR offset contract
 __global__ void k_degrees(const long long* rp, int n, long long nnz, int* deg, unsigned char* kb, ull* maxdeg, ull* bad) {
     ull m = 0, b = 0;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (long long)gridDim.x * blockDim.x) {
         const long long d = rp[v + 1] - rp[v];
         deg[v] = (int)d;
-        kb[v] = (unsigned char)(d < 255 ? (d < 0 ? 0 : d) : 255);
+        kb[v] = (unsigned char)gc_deg_code(d);
         m = (d > 0 && (ull)d > m) ? (ull)d : m;
         b += d < 0;
         if (v == 0) b += rp[0] != 0;
