@@ -781,8 +781,10 @@ extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolore
     }
     GC_HIP(hipMemsetAsync(&g->ctl->uncolored, 0, sizeof(ull), g->stream));
     GC_HIP(hipMemsetAsync(&g->ctl->conflicts, 0, sizeof(ull), g->stream));
-    // GC_VALIDATE_C8=1 (staged): the resident colouring's neighbours gathered from its byte mirror
-    const bool c8 = !colors && getenv("GC_VALIDATE_C8") && atoi(getenv("GC_VALIDATE_C8")) > 0;
+    // the resident colouring (colors == null): its neighbours' colours gathered from the byte
+    // mirror c8 (n bytes instead of 4n of random-gather footprint: 67 MB against 268 MB on
+    // R-MAT-26; bit-exact, tests/test_gpu_parity.py); GC_VALIDATE_C8=0 gathers the int colours
+    const bool c8 = !colors && !(getenv("GC_VALIDATE_C8") && atoi(getenv("GC_VALIDATE_C8")) == 0);
     if ((rc = gc_validate_tiles(g, src, c8 ? g->c8 : nullptr))) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));

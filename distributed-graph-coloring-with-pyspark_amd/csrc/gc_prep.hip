@@ -30,10 +30,11 @@
 #include "gc_device.h"
 #include "gc_engine.h"
 
-// GC_TILE_PER (build knob, default 16): entries per thread.  The tile's LDS (~57 KB at 16)
-// allows two workgroups per CU; 8 halves it (A/B: tools/build_variant.sh tile8 -DGC_TILE_PER=8)
+// GC_TILE_PER (build knob, default 8 since round 4): entries per thread.  The tile's LDS
+// (~57 KB at 16) allowed two workgroups per CU; 8 halves it: R-MAT-24's step 171.2-173.5 ->
+// 165.5-167.1 ms in an alternating A/B of the two builds (profiles/r04/c; A/B variant tile16)
 #ifndef GC_TILE_PER
-#define GC_TILE_PER 16
+#define GC_TILE_PER 8
 #endif
 #define GC_PER GC_TILE_PER               // entries per thread: 256 x GC_PER = GC_TW + GC_TH = GC_SEG
 #define GC_TW (GC_BLOCK / 2 * GC_PER)    // merge-path keys (rows + entries) per tile (2048 at 16)
@@ -888,6 +889,10 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long*
                        (const ull*)g->hb_bits, (const long long*)g->hb_wpre, (const int*)g->nlow, (const int*)g->hid,
                        hin_rp, klow);
     GC_HIP(hipGetLastError());
+    // the caller reads hin_rp[n] with a plain hipMemcpy, which does not wait for this
+    // (non-blocking) stream: hin_rp must be final before returning (round 4's first GPU run
+    // of this pass read it early, sized hin_col from a stale E and the fill faulted)
+    GC_HIP(hipStreamSynchronize(s));
     return GC_OK;
 }
 

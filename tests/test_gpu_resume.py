@@ -9,6 +9,8 @@ profiles/r04/a, profiles/r04/b).
 * overflow_tree / under_ticket_close: a closing commit (arrival tickets on the next frontier's
   counter) whose waves overflow their LDS stage mid-launch -- round 3's k_commit aperture fault
   (DESIGN §5): the flush base masked (GC_COUNT_MASK) and bounded by the list capacity.
+* validate_c8: gc_validate of the resident colouring from the byte mirror c8 (the default since
+  round 4) against the int colours and the oracle's validator (coloring.py:149-162).
 """
 import os
 import sys
@@ -195,3 +197,40 @@ def test_hybrid_two_processes(tmp_path):
             assert res["colors"] == list(one.colors) and res["cround"] == list(one.colored_round), sw
             assert res["U"] == list(one.round_U) and res["acc"] == list(one.round_accepted), sw
         assert got["1000000000"]["switch"] == 0
+
+
+# --- validation of the resident colouring from the byte mirror (default since round 4) ---------
+def test_validate_c8_matches(monkeypatch):
+    """The resident colouring validated from c8 (the default since round 4; GC_VALIDATE_C8=0
+    gathers the int colours) counts what the int colours count: after a full
+    run, after a failed bounded run (uncoloured vertices), and after a resume from a state with
+    planted conflicts (colours < 254 and >= 254, the byte mirror's BIG case)."""
+    import torch
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(12, 16, seed=9) as dg:
+        rp, col = dg.export()
+        for k in (None, 3):
+            g = dg.color("A", num_colors=k)
+            monkeypatch.setenv("GC_VALIDATE_C8", "0")
+            ref = dg.validate()
+            monkeypatch.delenv("GC_VALIDATE_C8", raising=False)
+            assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
+        v = int(np.argmax(np.diff(rp)))  # the largest row: it has neighbours
+        u = int(col[rp[v]])
+        c = np.full(dg.n, -1, np.int32)
+        c[v], c[u] = 300, 300  # a conflict past the byte mirror
+        w = next(int(x) for x in col[rp[u]:rp[u + 1]] if int(x) not in (u, v))
+        x = next((int(y) for y in col[rp[w]:rp[w + 1]] if int(y) not in (u, v, w)), None)
+        c[w] = 5
+        if x is not None:
+            c[x] = 5  # a conflict below 254
+        front = np.array(sorted(y for y in set(int(y) for y in col[rp[v]:rp[v + 1]]) if c[y] < 0), np.int32)
+        ct, ft = torch.from_numpy(c).cuda(), torch.from_numpy(front if len(front) else np.zeros(1, np.int32)).cuda()
+        torch.cuda.synchronize()
+        g = dg.resume(ct.data_ptr(), ft.data_ptr(), len(front), 0)
+        monkeypatch.setenv("GC_VALIDATE_C8", "0")
+        ref = dg.validate()
+        monkeypatch.delenv("GC_VALIDATE_C8", raising=False)
+        assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
+        assert ref[1] > 0
+

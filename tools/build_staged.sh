@@ -7,13 +7,13 @@
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 declare -A FLAGS=(
-  [tile8]="-DGC_TILE_PER=8"                            # merge-path tiles of 8 rows per thread
+  [tile16]="-DGC_TILE_PER=16"                          # merge-path tiles of 16 entries per thread (round 3's default)
   [close_call]="-DGC_CLOSE_INLINE=0 -DGC_CLOSE_BATCH=0" # the round close as a call (rounds 1-2: scratch in k_commit)
   [close_interleaved]="-DGC_CLOSE_BATCH=0"             # the round close as rounds 1-3 ran it (store, load, store, ...)
   [checks]="-DGC_CHECKS=1"                             # range checks in k_commit (fault hunts)
 )
 NAMES=("$@")
-[ ${#NAMES[@]} -eq 0 ] && NAMES=(tile8 close_call close_interleaved checks)
+[ ${#NAMES[@]} -eq 0 ] && NAMES=(tile16 close_call close_interleaved checks)
 for n in "${NAMES[@]}"; do
   [ -n "${FLAGS[$n]+x}" ] || { echo "unknown variant $n" >&2; exit 2; }
   bash "$ROOT/tools/build_variant.sh" "$n" "${FLAGS[$n]}"

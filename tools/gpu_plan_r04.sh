@@ -30,6 +30,13 @@ case ${1:-} in
                  "bench:rmat24:--sharded,--multi,hybrid,--switch-below,1000000000,--steps,3,--warmup,1"
                  "bench:rmat24:--sharded,--multi,hybrid,--switch-below,262144,--steps,3,--warmup,1"
                  "bench:rmat24:--sharded,--multi,hybrid,--switch-below,16384,--steps,3,--warmup,1") ;;
-  *) echo "usage: $0 a|b|c|d" >&2; exit 2 ;;
+  # e: after d's fault (the host read hin_rp[n] before the stream finished: fixed by a stream
+  #    synchronisation in gc_hub_transpose_sym), the whole GPU suite first, then the prep-pass
+  #    timing, the tile-size and byte-mirror A/Bs, and the profile of this build
+  e) exec_steps=(tests smoke env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING=
+                 abl:rmat24:4:2:base=-,tile16=variants/tile16/libgcolor.so
+                 ab:rmat26:3:base,c8off=GC_VALIDATE_C8:0
+                 profile:rmat24) ;;
+  *) echo "usage: $0 a|b|c|d|e" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
