@@ -52,7 +52,10 @@ int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64_t n, int64
                     uint32_t flags, gc_graph** out);
 /* Same, from device pointers already resident in HBM: rp is copied, the rows are read in
    place and written rank-partitioned into the graph's own array (no copy of col).  The
-   caller's buffers need to stay valid only for the duration of the call.             */
+   caller's buffers need to stay valid only for the duration of the call.  Ordering: the
+   library works on its own non-blocking stream, so the call first waits for all work on
+   the device (hipDeviceSynchronize): buffers still being written by kernels on any stream
+   (e.g. torch's) are complete before their first read.                                */
 int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                            uint32_t flags, gc_graph** out);
 /* Device-side synthetic generators (no host round trip):
@@ -148,7 +151,8 @@ int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* c
    once, any order), cround_dev (DEVICE int32[n] or NULL) the round each was coloured in.
    Replaces coloring.py:73-132 from that round on; stats hold the rounds from round0 (their
    records, the failing round as an absolute index).  The multi-GPU hybrid hands the
-   replicated state of its sharded rounds to the one-GPU engine with it.                */
+   replicated state of its sharded rounds to the one-GPU engine with it.  Ordering: as
+   gc_graph_create_device, the device buffers are read after all work on the device.     */
 int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t* colors_dev, const int32_t* cround_dev,
                     const int32_t* front_dev, int64_t nfront, int64_t round0, int32_t* colors_out,
                     int32_t* colored_round_out, gc_stats* stats);

@@ -37,6 +37,13 @@ case ${1:-} in
                  abl:rmat24:4:2:base=-,tile16=variants/tile16/libgcolor.so
                  ab:rmat26:3:base,c8off=GC_VALIDATE_C8:0
                  profile:rmat24) ;;
-  *) echo "usage: $0 a|b|c|d|e" >&2; exit 2 ;;
+  # f: variant B's profile, the hybrid's switch point at P = 1, the tile size on the other workloads
+  f) exec_steps=("profile:rmat24:--variant,B"
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,1000000000,--steps,3,--warmup,1"
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,262144,--steps,3,--warmup,1"
+                 "bench:rmat24:--sharded,--multi,hybrid,--switch-below,16384,--steps,3,--warmup,1"
+                 abl:uniform10M:6:1:base=-,tile16=variants/tile16/libgcolor.so
+                 abl:mesh512:3:1:base=-,tile16=variants/tile16/libgcolor.so) ;;
+  *) echo "usage: $0 a|b|c|d|e|f" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
