@@ -105,6 +105,7 @@ struct gc_graph {
     int* hperm = nullptr;         // id-order index -> hub index (rank order)
     ull* hb_bits = nullptr;       // hub-transpose build only: bit per entry (col[e] is a hub)
     long long* hb_wpre = nullptr; //   and the exclusive prefix of the words' popcounts
+    uint2* hb_mp = nullptr;       //   and hubmap / hubpre interleaved per word
 };
 
 // caching allocator (gc_alloc.hip): every device / pinned-host buffer of the library

@@ -617,9 +617,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
 // Per entry: 4 B of col (both passes) + one hubmap gather (bits pass); per hub entry: 4 B
 // written + the hub-index gathers (hubpre / hubmap / hperm: 2 x n/8 + 4 H bytes, L2/MALL).
 
+// hubmap and hubpre interleaved per word (hb_mp, built for the transpose and freed after
+// it): one 8-byte gather gives an entry's hub bit and its word's id-order base -- both
+// passes are bound by their gather rate (~270 G/s on R-MAT-24), and the fill's per-hub-entry
+// lookup is then two gathers (this word, hperm) instead of three
+__global__ void k_hb_mp(const unsigned* hubmap, const unsigned* hubpre, long long words, uint2* mp) {
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (long long)gridDim.x * blockDim.x)
+        mp[w] = make_uint2(hubmap[w], hubpre[w]);
+}
+
 // bits of 64 consecutive words per wave and iteration; lane k keeps word w0 + k (coalesced
 // stores), 8 entry loads per lane in flight
-__global__ void __launch_bounds__(GC_BLOCK) k_hbit(const int* col, long long nnz, long long n, const unsigned* hubmap,
+__global__ void __launch_bounds__(GC_BLOCK) k_hbit(const int* col, long long nnz, long long n, const uint2* mp,
                                                   ull* bits, long long* wcnt, long long nw) {
     const int lane = gc_lane();
     const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE;
@@ -636,7 +645,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hbit(const int* col, long long nnz
                 u[k] = e < nnz ? col[e] : -1;
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) hw[k] = (u[k] >= 0 && (long long)u[k] < n) ? hubmap[u[k] >> 5] : 0u;
+            for (int k = 0; k < 8; ++k) hw[k] = (u[k] >= 0 && (long long)u[k] < n) ? mp[u[k] >> 5].x : 0u;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const ull m = __ballot(u[k] >= 0 && ((hw[k] >> (u[k] & 31)) & 1u));
@@ -675,8 +684,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_rank(const long long* rp, long
 // hin_col[rank(e)] = hub index of col[e] for every hub entry e: a wave per 64 words, lane k
 // holding word w0 + k's bits and prefix, 8 words' entries in flight per step
 __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(const int* col, long long nw, const ull* bits,
-                                                      const long long* wpre, const unsigned* hubmap,
-                                                      const unsigned* hubpre, const int* hperm, int* hin_col) {
+                                                      const long long* wpre, const uint2* mp, const int* hperm,
+                                                      int* hin_col) {
     const int lane = gc_lane();
     const ull lt = gc_lanemask_lt();
     const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE;
@@ -697,16 +706,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hin_fill(const int* col, long long
                 on[k] = (mk[k] >> lane) & 1ull;
                 u[k] = on[k] ? col[(w0 + k0 + k) * GC_WAVE + lane] : 0;
             }
-            unsigned pre[8], hw[8];
+            uint2 m[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                pre[k] = on[k] ? hubpre[u[k] >> 5] : 0u;
-                hw[k] = on[k] ? hubmap[u[k] >> 5] : 0u;
-            }
+            for (int k = 0; k < 8; ++k) m[k] = on[k] ? mp[u[k] >> 5] : make_uint2(0u, 0u);
             int x[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                x[k] = on[k] ? hperm[pre[k] + __popc(hw[k] & ((1u << (u[k] & 31)) - 1u))] : 0;
+                x[k] = on[k] ? hperm[m[k].y + __popc(m[k].x & ((1u << (u[k] & 31)) - 1u))] : 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if (on[k]) hin_col[base[k] + __popcll(mk[k] & lt)] = x[k];
@@ -871,6 +877,11 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long*
     const long long n = g->n, nnz = g->nnz;
     const long long nw = (nnz + 63) / 64;
     gc_hub_bits_free(g);
+    const long long words = (n + 31) / 32;
+    GC_HIP(gc_dmalloc((void**)&g->hb_mp, sizeof(uint2) * (size_t)std::max<long long>(words, 1)));
+    if (words > 0)
+        hipLaunchKernelGGL(k_hb_mp, dim3(small_grid(words)), dim3(GC_BLOCK), 0, s, (const unsigned*)g->hubmap,
+                           (const unsigned*)g->hubpre, words, g->hb_mp);
     GC_HIP(gc_dmalloc((void**)&g->hb_bits, sizeof(ull) * (size_t)(nw + 1)));
     GC_HIP(gc_dmalloc((void**)&g->hb_wpre, sizeof(long long) * (size_t)(nw + 1)));
     long long* wcnt = nullptr;
@@ -881,7 +892,7 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long*
     const int grid = (int)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 8192));
     if (nw > 0)
         hipLaunchKernelGGL(k_hbit, dim3(grid), dim3(GC_BLOCK), 0, s, (const int*)g->col, nnz, n,
-                           (const unsigned*)g->hubmap, g->hb_bits, wcnt, nw);
+                           (const uint2*)g->hb_mp, g->hb_bits, wcnt, nw);
     int rc = scan_ll(wcnt, g->hb_wpre, nw + 1, s);
     gc_dfree(wcnt);
     if (rc) return rc;
@@ -901,12 +912,11 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long*
 int gc_hub_transpose_fill(gc_graph* g, long long H) {
     const hipStream_t s = g->stream;
     const long long nw = (g->nnz + 63) / 64;
-    if (!g->hb_bits || !g->hb_wpre) { gc_set_error("gc_hub_transpose_fill: no entry bits"); return GC_EINVAL; }
+    if (!g->hb_bits || !g->hb_wpre || !g->hb_mp) { gc_set_error("gc_hub_transpose_fill: no entry bits"); return GC_EINVAL; }
     const int grid = (int)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 8192));
     if (nw > 0)
         hipLaunchKernelGGL(k_hin_fill, dim3(grid), dim3(GC_BLOCK), 0, s, (const int*)g->col, nw, (const ull*)g->hb_bits,
-                           (const long long*)g->hb_wpre, (const unsigned*)g->hubmap, (const unsigned*)g->hubpre,
-                           (const int*)g->hperm, g->hin_col);
+                           (const long long*)g->hb_wpre, (const uint2*)g->hb_mp, (const int*)g->hperm, g->hin_col);
     if (H > 0)
         hipLaunchKernelGGL(k_hlow_copy, dim3((int)std::min<long long>((H + 3) / 4, 8192)), dim3(GC_BLOCK), 0, s,
                            (const int*)g->hub_v, H, (const long long*)g->hin_rp, (const int*)g->hin_col,
@@ -920,6 +930,8 @@ int gc_hub_transpose_fill(gc_graph* g, long long H) {
 void gc_hub_bits_free(gc_graph* g) {
     if (g->hb_bits) gc_dfree(g->hb_bits);
     if (g->hb_wpre) gc_dfree(g->hb_wpre);
+    if (g->hb_mp) gc_dfree(g->hb_mp);
     g->hb_bits = nullptr;
     g->hb_wpre = nullptr;
+    g->hb_mp = nullptr;
 }
