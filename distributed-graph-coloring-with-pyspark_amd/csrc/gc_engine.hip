@@ -290,6 +290,11 @@ struct Run {
     int async_grid = 0;
     int async_par = 0;
     long long async_budget = 0;
+    // GC_ASYNC_BIG=0 (A/B knob, round 4): rounds whose frontier is big (the re-sort hint,
+    // >= n/256) run the full-grid sweeps and the one-workgroup tail instead of the
+    // asynchronous JP (the resident grid has a quarter of the full grid's waves)
+    const bool async_big = !(getenv("GC_ASYNC_BIG") && atoi(getenv("GC_ASYNC_BIG")) == 0);
+    bool async_now() const { return async_grid > 0 && (async_big || !resort_hint); }
     void init_async() {
         const char* e = getenv("GC_ASYNC");
         if (e && atoi(e) == 0) return;
@@ -382,7 +387,7 @@ struct Run {
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
         const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
-        if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
+        if (tail && async_now()) {  // the rest of the JP chain: one asynchronous launch
             kt.begin(GC_K_SWEEP);
             gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
             async_par ^= 1;
@@ -392,7 +397,7 @@ struct Run {
             gcl_sweep_loop(d, L, nsweeps, loop_grid, s);
             kt.end();
         }
-        if (tail && async_grid == 0) {
+        if (tail && !async_now()) {
             kt.begin(GC_K_SWEEP);
             gcl_sweep_tail(d, L, nsweeps, s);
             kt.end();
@@ -490,7 +495,7 @@ struct Run {
     bool skip_tail = false;  // set with S = 0 once 16 rounds ran without a second sweep
     int pick_sweeps(const DevCtl& h) {
         skip_tail = h.maxdepth <= 1 && h.round >= 16;
-        if (h.maxdepth <= 1 || async_grid > 0) return 0;  // k_sweep_async takes the whole chain
+        if (h.maxdepth <= 1 || async_now()) return 0;  // k_sweep_async takes the whole chain
         // the small-list tail runs in k_sweep_tail; with the loop kernel, the full grid only
         // takes the sweeps past its limits
         if (loop_grid > 0) return (int)std::min<long long>(64, h.lasthuge + 1);
@@ -589,8 +594,8 @@ struct Run {
                 const DevCtl& sn = g->hsnap[slot];
                 if (sn.halt != GC_RUN || sn.loop_err >= 2) break;
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
-                S = pick_sweeps(sn);
                 resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
+                S = pick_sweeps(sn);
                 c4_hint = pick_c4(sn, g->n);
                 batch = pick_batch(sn, g->n, batch);
                 slot ^= 1;
@@ -612,8 +617,8 @@ struct Run {
                 halt = h.halt;
             }
             proposed = h.proposed != 0;
-            S = pick_sweeps(h);
             resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
+            S = pick_sweeps(h);
             c4_hint = pick_c4(h, g->n);
             batch = pick_batch(h, g->n, 1);
             if (halt == GC_RUN) continue;
