@@ -329,6 +329,17 @@ struct Run {
     // k_propose_block has no work unless some vertex can be heavy or wide: skip its launch
     // (meshes: ~5 us of a ~80 us round)
     bool need_pblock() const { return g->maxdeg > d.heavy_t || g->maxdeg >= 64; }  // heavy_t is final once hubs are set
+    // GC_INLINE_PB=1 (A/B knob, round 4): small rounds propose their hubs and wide lights
+    // inside k_propose<1> (a wave each) and skip the k_propose_block launch.  Needs the hub
+    // bitmaps (heavy == hub) and lights narrow enough for k_propose's 2048-bit window; the
+    // bitmaps must cover every colour the enqueued rounds can reach (maxcolor grows by at most
+    // one a round: the last snapshot's maxcolor plus a margin of the rounds in flight).
+    const bool inline_pb = getenv("GC_INLINE_PB") && atoi(getenv("GC_INLINE_PB")) > 0;
+    long long maxc_hint = 0;  // the last snapshot's maxcolor
+    bool inline_now() const {
+        return inline_pb && !resort_hint && d.hbits_w && !d.hub_repl && d.heavy_t < 2048 &&
+               maxc_hint + 2 + 4ll * batch_max + 16 <= 32ll * d.hbits_w;
+    }
     // Fused commits (k_commit<1>) make the next round's proposals themselves, so a round
     // after one runs no k_propose: low-degree graphs (no heavy or wide proposer, no hubs),
     // small rounds (the big-round frontier rebuild and nibble mirror stay unfused).
@@ -462,10 +473,11 @@ struct Run {
             gcl_pack_c4(d, s);
             kt.end();
         }
+        const bool inl = inline_now();
         kt.begin(GC_K_PROPOSE);
-        gcl_propose(d, L, s, resort_hint ? 0 : 1);
+        gcl_propose(d, L, s, resort_hint ? 0 : 1, inl ? 1 : 0);
         kt.end();
-        if (need_pblock()) {  // heavy (deg > heavy_t) or wide (mex >= 64, so deg >= 64) proposers possible
+        if (need_pblock() && !inl) {  // heavy (deg > heavy_t) or wide (mex >= 64, so deg >= 64) proposers possible
             kt.begin(GC_K_PROPOSE);
             gcl_propose_block(d, L, s);
             kt.end();
@@ -595,6 +607,7 @@ struct Run {
                 if (sn.halt != GC_RUN || sn.loop_err >= 2) break;
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
                 resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
+                maxc_hint = sn.maxcolor;
                 S = pick_sweeps(sn);
                 c4_hint = pick_c4(sn, g->n);
                 batch = pick_batch(sn, g->n, batch);
@@ -618,6 +631,7 @@ struct Run {
             }
             proposed = h.proposed != 0;
             resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
+            maxc_hint = h.maxcolor;
             S = pick_sweeps(h);
             c4_hint = pick_c4(h, g->n);
             batch = pick_batch(h, g->n, 1);
@@ -642,6 +656,7 @@ struct Run {
             gc_set_error("unexpected device halt code %d", halt);
             return GC_EHIP;
         }
+        if (h.loop_err == GC_LERR_INL) { gc_set_error("k_propose: a hub bitmap does not cover the colours in use (round %lld)", h.round); return GC_EHIP; }
         if (h.loop_err == GC_LERR_LIST) { gc_set_error("a work-list append passed the list's capacity (round %lld)", h.round); return GC_EHIP; }
         if (h.loop_err == 2) { gc_set_error("k_sweep_async: undecided list count out of range"); return GC_EHIP; }
         if (h.loop_err == 4) { gc_set_error("gc_color_resume: a frontier entry is out of range"); return GC_EINVAL; }

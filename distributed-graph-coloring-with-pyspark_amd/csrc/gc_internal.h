@@ -243,6 +243,7 @@ __device__ __forceinline__ int gc_vpw(long long cnt, long long waves) {
 // would pass it writes nothing and sets DevCtl.loop_err = GC_LERR_LIST, which the host
 // reports as GC_EHIP: a wrong base becomes a reported error, never an aperture fault.
 #define GC_LERR_LIST 5
+#define GC_LERR_INL 6  // k_propose<1>: a hub bitmap no longer covers the colours in use
 struct GcStage {
     int* buf;
     int cnt;  // wave-uniform

@@ -256,10 +256,18 @@ __device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex) {
     g.k8[v] = gc_k8(c6, GC_JP_UND);
 }
 
+// INL = 1 (the one-GPU engine's small rounds, GC_INLINE_PB): the heavy proposers (hubs, whose
+// forbidden colours are pushed bitmaps covering every colour in use) and the wide lights
+// (mex >= 64, so mex <= deg <= heavy_t < GC_INL_BITS) are proposed here, the whole wave on
+// one of them at a time, instead of in a k_propose_block launch after this one.
+#define GC_INL_WORDS 32  // 2048-bit LDS window per wave for a wide light's mex
+#define GC_INL_BITS (64 * GC_INL_WORDS)
+template <int INL>
 __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
     __shared__ ull s_mask[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ ull s_wide[INL ? GC_WAVES_PER_BLOCK : 1][INL ? GC_INL_WORDS : 1];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
@@ -275,6 +283,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     const unsigned char* __restrict__ c8 = g.c8;
     const unsigned* __restrict__ c4 = g.c4;
     const bool use_c4 = c->use_c4 != 0;
+    long long hwords = INL ? (c->maxcolor + 2 + 31) / 32 : 0;  // the bitmap words in use (mex <= maxcolor + 1)
+    if (INL && hwords > g.hbits_w) {  // the host's margin was too small: report, propose nothing
+        if (threadIdx.x == 0 && blockIdx.x == 0)
+            __hip_atomic_store(&c->loop_err, GC_LERR_INL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
         const long long idx = ch * vpw + lane;
@@ -321,7 +335,69 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
                 lnv++;
             }
         }
-        gc_wave_append(iswide, v, L.wide, &c->wide_cnt);
+        if (!INL) {
+            gc_wave_append(iswide, v, L.wide, &c->wide_cnt);
+            continue;
+        }
+        // hubs: the first zero bit of the pushed bitmap (as k_propose_block's hub waves)
+        for (ull hm = __ballot(isheavy); hm; hm &= hm - 1) {
+            const int l = __ffsll((long long)hm) - 1;
+            const int hv = __shfl(v, l, GC_WAVE);
+            const int x = g.hid[hv];
+            const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
+            long long mex = -1;
+            for (int t0 = 0; t0 < hwords && mex < 0; t0 += GC_WAVE) {  // a zero bit lies in range
+                const int t = t0 + lane;
+                const unsigned wd = t < hwords ? hb[t] : 0xFFFFFFFFu;
+                const ull zm = __ballot(wd != 0xFFFFFFFFu);
+                if (zm) {
+                    const int zl = __ffsll((long long)zm) - 1;
+                    const unsigned zw = __shfl(wd, zl, GC_WAVE);
+                    mex = 32ll * (t0 + zl) + __builtin_ctz(~zw);
+                }
+            }
+            if (lane == 0) {
+                if (g.hub_w) {  // the hub JP's state: this round's conflict flag, cursors, mirror
+                    g.hkill[x] = 0u;
+                    g.hcur[x] = 0;
+                    g.hpc[x] = 0;
+                    if (g.hprep) g.hkcnt[x] = 0;
+                    g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);
+                }
+                gc_set_cand(g, hv, mex);
+                lmax = mex > lmax ? mex : lmax;
+                if (kbound >= 0 && mex >= kbound) lfail++;
+                lsum += (ull)g.deg[hv];
+                lnv++;
+            }
+        }
+        // wide lights: mex <= deg < GC_INL_BITS, one pass over the row into an LDS window
+        for (ull wm = __ballot(iswide); wm; wm &= wm - 1) {
+            const int l = __ffsll((long long)wm) - 1;
+            const int wv = __shfl(v, l, GC_WAVE);
+            const int wdg = __shfl(d, l, GC_WAVE);
+            const long long rs = s_start[w][l];
+            if (lane < GC_INL_WORDS) s_wide[w][lane] = 0ull;
+            gc_wave_sync();
+            for (int e = lane; e < wdg; e += GC_WAVE) {
+                const int cc = gc_colour(g, g.col[rs + e]);
+                if (cc >= 0 && cc < GC_INL_BITS) atomicOr(&s_wide[w][cc >> 6], 1ull << (cc & 63));
+            }
+            gc_wave_sync();
+            const ull wk = lane < GC_INL_WORDS ? s_wide[w][lane] : ~0ull;
+            const ull zm = __ballot(wk != ~0ull);  // nonzero: at most deg colours are forbidden
+            const int zk = __ffsll((long long)zm) - 1;
+            const ull zw = __shfl(wk, zk, GC_WAVE);
+            const int mex = 64 * zk + __builtin_ctzll(~zw);
+            if (lane == 0) {
+                gc_set_cand(g, wv, mex);
+                lmax = mex > lmax ? mex : lmax;
+                if (kbound >= 0 && mex >= kbound) lfail++;
+                lsum += (ull)wdg;
+                lnv++;
+            }
+            gc_wave_sync();
+        }
     }
     __syncthreads();
     gc_block_max(&c->maxmex, lmax, (long long*)scratch);
@@ -2930,8 +3006,9 @@ void gcl_stat_reduce(const GDev& g, hipStream_t s) {
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
     hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
 }
-void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small) {
-    hipLaunchKernelGGL(k_propose, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
+void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small, int inl) {
+    if (inl) hipLaunchKernelGGL(k_propose<1>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
+    else hipLaunchKernelGGL(k_propose<0>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
     hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);

@@ -95,7 +95,8 @@ int gcl_fsort_blocks(long long n);
 void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);
 void gcl_pack_c4(const GDev& g, hipStream_t s);
 void gcl_stat_reduce(const GDev& g, hipStream_t s);
-void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small = 0);  // small: the last frontier was < n/256
+// small: the last frontier was < n/256; inl: heavy and wide proposers here (no k_propose_block)
+void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small = 0, int inl = 0);
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s);
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);

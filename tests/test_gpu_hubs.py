@@ -49,17 +49,21 @@ SETTINGS = [
     {"GC_HUB_T": "3", "GC_ASYNC_BPC": "1"},                   # one workgroup per CU
     {"GC_HUB_T": "0", "GC_ASYNC": "0"},                       # round 2's full-grid sweeps + tail
     {"GC_HUB_T": "off", "GC_ASYNC": "0"},
+    {"GC_HUB_T": "0", "GC_INLINE_PB": "1"},                   # small rounds' hubs and wide lights in k_propose<1>
+    {"GC_HUB_T": "512", "GC_INLINE_PB": "1"},
+    {"GC_HUB_T": "1024", "GC_INLINE_PB": "1", "GC_ASYNC": "0"},
+    {"GC_HUB_T": "2", "GC_HUB_W": "2", "GC_INLINE_PB": "1"},  # a 64-colour bitmap: inline only while colours are few
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
        "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
        "T2loop", "offloop8", "T0async_abort", "T2async_abort", "offasync_abort", "T3async_bpc1",
-       "T0sync", "offsync"]
+       "T0sync", "offsync", "T0inl", "T512inl", "T1024inl_sync", "T2w2inl"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
     for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP",
-              "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC"):
+              "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC", "GC_INLINE_PB"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)
