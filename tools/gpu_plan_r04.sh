@@ -44,6 +44,12 @@ case ${1:-} in
                  "bench:rmat24:--sharded,--multi,hybrid,--switch-below,16384,--steps,3,--warmup,1"
                  abl:uniform10M:6:1:base=-,tile16=variants/tile16/libgcolor.so
                  abl:mesh512:3:1:base=-,tile16=variants/tile16/libgcolor.so) ;;
-  *) echo "usage: $0 a|b|c|d|e|f" >&2; exit 2 ;;
+  # g: the hub tests with k_propose's inlined hubs (GC_INLINE_PB), every GPU test on the build
+  #    with the interleaved hub transpose, the A/Bs of the two new knobs, variant B per round
+  g) exec_steps=(file:tests/test_gpu_hubs.py tests
+                 ab:rmat24:6:base,inl=GC_INLINE_PB:1,abig0=GC_ASYNC_BIG:0,both=GC_INLINE_PB:1+GC_ASYNC_BIG:0
+                 ab:rmat26:3:base,inl=GC_INLINE_PB:1,abig0=GC_ASYNC_BIG:0
+                 brounds:rmat24) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"

@@ -16,6 +16,7 @@
 #   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
 #   rounds:WL         per-round kernel cost by frontier size (tools/round_cost.py under
 #                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
+#   brounds:WL        variant B's per-round cost (tools/b_round_cost.py, likewise)
 #   ab:WL:REPS:CFGS   tools/ab_steps.py WL REPS CFG... (CFGS comma-separated, each NAME=VAR:val+VAR:val):
 #                     interleaved in-process A/B of environment knobs, colourings checked equal
 #   abl:WL:REPS:CYCLES:VARS  tools/ab_libs.sh: compile-time variants, a process each, alternated
@@ -87,6 +88,14 @@ for st in "$@"; do
         python tools/round_cost.py analyze "$tr" "$O/rounds_$rest/records.json" \
           > "$O/rounds_$rest/round_cost.txt" 2>> "$log" &&
         rm -f "$tr" && cat "$O/rounds_$rest/round_cost.txt" >> "$log" ;;
+    brounds)
+      mkdir -p "$O/brounds_$rest"
+      ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/brounds_$rest" -o run -- \
+          python3 "$ROOT/tools/b_round_cost.py" run "$rest" "$O/brounds_$rest/records.json" 2 ) > "$log" 2>&1 &&
+        tr=$(find "$O/brounds_$rest" -name '*kernel_trace.csv' -print -quit) && [ -n "$tr" ] &&
+        python tools/b_round_cost.py analyze "$tr" "$O/brounds_$rest/records.json" \
+          > "$O/brounds_$rest/b_round_cost.txt" 2>> "$log" &&
+        rm -f "$tr" && cat "$O/brounds_$rest/b_round_cost.txt" >> "$log" ;;
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
