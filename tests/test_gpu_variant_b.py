@@ -146,6 +146,53 @@ def test_variant_b_hub_bitmaps(monkeypatch, hub_t, hub_w):
         assert_same_run(dg.color("B", num_colors=int(o["max_color"])), oracle.c_color(rp, col, "B", k=int(o["max_color"])))
 
 
+TAIL_SETTINGS = [
+    {"GC_B_TAIL": "0"},                                                   # every pass a pair of full-grid launches
+    {},                                                                   # the default caps
+    {"GC_B_TAIL_L": "16", "GC_B_TAIL_H": "0", "GC_B_TAIL_E": "16"},       # the tail hands back and takes over often
+    {"GC_B_TAIL_L": "1000000", "GC_B_TAIL_H": "64", "GC_B_TAIL_E": "1000000"},  # whole folds after one full pass
+]
+
+
+@pytest.mark.parametrize("env", TAIL_SETTINGS, ids=["tail_off", "tail", "tail_small", "tail_all"])
+def test_variant_b_fold_tail(monkeypatch, env):
+    """The fold's deep end in k_b_tail's one workgroup (GC_B_TAIL): off, default, tiny caps
+    (passes alternate between the grid and the workgroup) and caps that take whole folds,
+    heavy admissions included -- every run equal to the oracle."""
+    for k in ("GC_B_TAIL", "GC_B_TAIL_L", "GC_B_TAIL_H", "GC_B_TAIL_E"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with _dg().rmat(13, 16, seed=5) as dg:
+        rp, col = dg.export()
+        o = oracle.c_color(rp, col, "B")
+        assert_same_run(dg.color("B"), o)
+        assert_same_run(dg.color("B", num_colors=int(o["max_color"]) // 2), oracle.c_color(rp, col, "B", k=int(o["max_color"]) // 2))
+    rp, col = _random_directed(3000, 9000, 7)
+    with _dg().from_csr(rp, col) as dg:
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+    n = 150 + 6000  # a 150-clique whose first vertex is a hub of 6000 leaves (heavy admissions, wide mex)
+    adj = [[] for _ in range(n)]
+    for i in range(150):
+        adj[i] += [j for j in range(150) if j != i]
+    for leaf in range(150, n):
+        adj[0].append(leaf)
+        adj[leaf].append(0)
+    from gcolor_amd.graphio import csr_from_adjacency
+    rp, col = csr_from_adjacency(adj)
+    with _dg().from_csr(rp, col) as dg:
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+    from gcolor_amd.engine import uniform_csr
+    rp, col = uniform_csr(50_000, 40, 3)
+    with _dg().from_csr(rp, col, symmetric=True) as dg:
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+    h = 2050  # K_{h,h}: every row is h equal-degree entries, past GC_B_HEAVY: heavy admissions only
+    rp = np.arange(2 * h + 1, dtype=np.int64) * h
+    col = np.concatenate([np.tile(np.arange(h, 2 * h, dtype=np.int32), h), np.tile(np.arange(h, dtype=np.int32), h)])
+    with _dg().from_csr(rp, col, symmetric=True) as dg:
+        assert_same_run(dg.color("B"), oracle.c_color(rp, col, "B"))
+
+
 def test_mesh_and_edgeless_variant_b():
     DG = _dg()
     with DG.mesh(16, 8, 4) as dg:
