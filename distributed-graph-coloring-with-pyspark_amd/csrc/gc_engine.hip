@@ -290,11 +290,9 @@ struct Run {
     int async_grid = 0;
     int async_par = 0;
     long long async_budget = 0;
-    // GC_ASYNC_BIG=0 (A/B knob, round 4): rounds whose frontier is big (the re-sort hint,
-    // >= n/256) run the full-grid sweeps and the one-workgroup tail instead of the
-    // asynchronous JP (the resident grid has a quarter of the full grid's waves)
-    const bool async_big = !(getenv("GC_ASYNC_BIG") && atoi(getenv("GC_ASYNC_BIG")) == 0);
-    bool async_now() const { return async_grid > 0 && (async_big || !resort_hint); }
+    // (round 4 measured the big rounds -- frontier >= n/256 -- on the full-grid sweeps and the
+    // one-workgroup tail instead: R-MAT-24 +6.1%, R-MAT-26 +5.0%, profiles/r04/g; the
+    // asynchronous JP stays on in every round)
     void init_async() {
         const char* e = getenv("GC_ASYNC");
         if (e && atoi(e) == 0) return;
@@ -329,13 +327,14 @@ struct Run {
     // k_propose_block has no work unless some vertex can be heavy or wide: skip its launch
     // (meshes: ~5 us of a ~80 us round)
     bool need_pblock() const { return g->maxdeg > d.heavy_t || g->maxdeg >= 64; }  // heavy_t is final once hubs are set
-    // GC_INLINE_PB=1 (A/B knob, round 4): small rounds propose their hubs and wide lights
-    // inside k_propose<1> (a wave each) and skip the k_propose_block launch.  Needs the hub
-    // bitmaps (heavy == hub) and lights narrow enough for k_propose's 2048-bit window; the
-    // bitmaps must cover every colour the enqueued rounds can reach (maxcolor grows by at most
-    // one a round: the last snapshot's maxcolor plus a margin of the rounds in flight).
-    const bool inline_pb = getenv("GC_INLINE_PB") && atoi(getenv("GC_INLINE_PB")) > 0;
-    long long maxc_hint = 0;  // the last snapshot's maxcolor
+    // Small rounds propose their hubs and wide lights inside k_propose<1> (a wave each) and
+    // skip the k_propose_block launch (round 4: R-MAT-24 158.7 -> 155.4 ms, R-MAT-26 429.4 ->
+    // 429.0, profiles/r04/g; GC_INLINE_PB=0 turns it off).  Needs the hub bitmaps (heavy ==
+    // hub) and lights narrow enough for k_propose's 2048-bit window; the bitmaps must cover
+    // every colour the enqueued rounds can reach (maxcolor grows by at most one a round: the
+    // last snapshot's maxcolor plus a margin of the rounds in flight).
+    const bool inline_pb = !(getenv("GC_INLINE_PB") && atoi(getenv("GC_INLINE_PB")) == 0);
+    long long maxc_hint = 1ll << 40;  // the last snapshot's maxcolor (none yet: no inlining; a resumed colouring's colours are unknown here)
     bool inline_now() const {
         return inline_pb && !resort_hint && d.hbits_w && !d.hub_repl && d.heavy_t < 2048 &&
                maxc_hint + 2 + 4ll * batch_max + 16 <= 32ll * d.hbits_w;
@@ -398,7 +397,7 @@ struct Run {
         // no tail kernel either; a round that needs more makes the commit ask for sweeps
         // (GC_H_SWEEPS), which come with the tail (nsweeps -1 tells k_commit it did not run)
         const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
-        if (tail && async_now()) {  // the rest of the JP chain: one asynchronous launch
+        if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
             kt.begin(GC_K_SWEEP);
             gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
             async_par ^= 1;
@@ -408,7 +407,7 @@ struct Run {
             gcl_sweep_loop(d, L, nsweeps, loop_grid, s);
             kt.end();
         }
-        if (tail && !async_now()) {
+        if (tail && async_grid == 0) {
             kt.begin(GC_K_SWEEP);
             gcl_sweep_tail(d, L, nsweeps, s);
             kt.end();
@@ -507,7 +506,7 @@ struct Run {
     bool skip_tail = false;  // set with S = 0 once 16 rounds ran without a second sweep
     int pick_sweeps(const DevCtl& h) {
         skip_tail = h.maxdepth <= 1 && h.round >= 16;
-        if (h.maxdepth <= 1 || async_now()) return 0;  // k_sweep_async takes the whole chain
+        if (h.maxdepth <= 1 || async_grid > 0) return 0;  // k_sweep_async takes the whole chain
         // the small-list tail runs in k_sweep_tail; with the loop kernel, the full grid only
         // takes the sweeps past its limits
         if (loop_grid > 0) return (int)std::min<long long>(64, h.lasthuge + 1);

@@ -95,7 +95,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_fail0(GDev g, GLists L) {
 #define GC_B_HEAVY 2048
 struct BLists {
     int* l[3][3];  // [kind][slot]
+    int* pend;     // nnz ints: each listed light vertex's still-pending entries, at rp[v] (see below)
 };
+// Pending entries (round 4).  A flag that reads 0 is final (a later arrival, a refused or
+// other-candidate vertex, an eviction before v), so after its first scan a light vertex only
+// ever needs the entries that were still pending: each scan writes them, compacted, to
+// pend[rp[v] ...] (in place after the first), and lcur[v] = -(count) - 1 says so.  An admitted
+// vertex's eviction scan likewise keeps its not-refused potential evictors there (its
+// admission entries are done with); lcur[v] = GC_B_EVCOL until its first eviction scan.
+// Heavy admissions (a workgroup each) keep the cursor form, lcur[v] >= 0: the first pending
+// entry of the row.  A pass's work is then the pending entries, not the rest of every row.
+#define GC_B_EVCOL 0x7FFFFFFF
+#define GC_B_PMARK 0x80000000u  // marks an entry read from pend[] (its degree was checked)
 __device__ __forceinline__ ull* b_cnt(DevCtl* c, int kind, int slot) { return &c->bcnt[kind * 3 + slot]; }
 // a list count at the start of a pass: a plain load in a full-grid launch (written by an
 // earlier launch), an agent-scope load in k_b_tail (written by its own atomics, maybe since
@@ -104,6 +115,31 @@ template <bool TAIL>
 __device__ __forceinline__ long long b_count(DevCtl* c, int kind, int slot) {
     ull* p = b_cnt(c, kind, slot);
     return TAIL ? (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (long long)*p;
+}
+
+// gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]
+template <typename Load, typename Apply>
+__device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl, int total, Load load, Apply apply) {
+    const int lane = gc_lane();
+    for (int base = 0; base < total; base += GC_SLOTS * GC_WAVE) {
+        int o[GC_SLOTS], x[GC_SLOTS], u[GC_SLOTS];
+        bool ok[GC_SLOTS];
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) {
+            const int e = base + k * GC_WAVE + lane;
+            o[k] = gc_owner(excl, e);
+            x[k] = e - __shfl(excl, o[k], GC_WAVE);
+            ok[k] = e < total;
+        }
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) u[k] = ok[k] ? s_src[o[k]][x[k]] : 0;
+        decltype(load(0)) gv[GC_SLOTS];
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k) gv[k] = ok[k] ? load(u[k]) : decltype(load(0)){};
+#pragma unroll
+        for (int k = 0; k < GC_SLOTS; ++k)
+            if (ok[k]) apply(o[k], u[k], gv[k], x[k]);
+    }
 }
 
 // Row layout (the (deg, pos) rank partition, gc_prep.hip): [lower degree | equal degree,
@@ -150,7 +186,9 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         else *b_cnt(c, threadIdx.x, zs) = 0ull;
     }
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ const int* s_src[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int* s_dst[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_np[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_min[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -170,9 +208,19 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0u;
         const int d = v >= 0 ? g.deg[v] : 0;
-        const int lo = v >= 0 ? g.nlow[v] : 0;
-        const int len = d - lo;
-        s_start[w][lane] = v >= 0 ? g.rp[v] + lo : 0;
+        const int lc = v >= 0 ? g.lcur[v] : GC_B_EVCOL;
+        const long long r0 = v >= 0 ? g.rp[v] : 0;
+        int len = 0;
+        if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's higher-rank part
+            const int lo = g.nlow[v];
+            len = d - lo;
+            s_src[w][lane] = g.col + r0 + lo;
+        } else if (v >= 0) {  // the kept potential evictors
+            len = -lc - 1;
+            s_src[w][lane] = B.pend + r0;
+        }
+        s_dst[w][lane] = B.pend + r0;
+        s_np[w][lane] = 0;
         s_min[w][lane] = GC_B_INF;
         s_v[w][lane] = v;
         s_d[w][lane] = d;
@@ -182,15 +230,24 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        gc_chunk_edges(
-            g.col, s_start[w], excl, total,
-            [&](int u) { return ((ull)(unsigned)g.deg[u] << 32) | (ull)k8[u]; },
-            [&](int o, int u, ull du) {
+        // a kept entry (marked) passed the static tests (later arrival, higher degree, same
+        // candidate): only its state can change
+        b_chunk_edges(
+            s_src[w], excl, total,
+            [&](int um) {
+                const int u = um & 0x7FFFFFFF;
+                return ((unsigned)um & GC_B_PMARK) ? (ull)k8[u] : ((ull)(unsigned)g.deg[u] << 32) | (ull)k8[u];
+            },
+            [&](int o, int um, ull du, int) {
+                const int u = um & 0x7FFFFFFF;
                 const unsigned ku = (unsigned)du & 0xFFu;
-                if (u <= s_v[w][o] || gc_k8_state(ku) == GC_JP_OUT) return;
-                if ((int)(du >> 32) <= s_d[w][o]) return;
-                if (!b_same(g, u, ku, s_c6[w][o], s_cv[w][o])) return;
+                if (gc_k8_state(ku) == GC_JP_OUT) return;
+                if (!((unsigned)um & GC_B_PMARK)) {
+                    if (u <= s_v[w][o] || (int)(du >> 32) <= s_d[w][o]) return;
+                    if (!b_same(g, u, ku, s_c6[w][o], s_cv[w][o])) return;
+                }
                 atomicMin(&s_min[w][o], u);
+                s_dst[w][o][atomicAdd(&s_np[w][o], 1)] = (int)((unsigned)u | GC_B_PMARK);
             });
         gc_wave_sync();
         bool pend = false;
@@ -198,6 +255,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
             const int e = s_min[w][lane];
             ev[v] = e;
             pend = e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN;
+            if (pend) g.lcur[v] = -s_np[w][lane] - 1;
         }
         gc_stage_push(st, pend, v, B.l[2][ws], b_cnt(c, 2, ws));
     }
@@ -236,6 +294,7 @@ __device__ __forceinline__ void b_adm_decide(GDev& g, BLists& B, DevCtl* c, int 
         *dst_kind = g.deg[v] - bc > GC_B_HEAVY ? 1 : 0;
     } else {
         g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
+        g.lcur[v] = GC_B_EVCOL;
         *dst_kind = 2;
     }
 }
@@ -304,9 +363,10 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
     const int rs = pass % 3, ws = (pass + 1) % 3;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ int s_estage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
-    __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ const int* s_src[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int* s_dst[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_flag[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_first[GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_np[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_v[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -323,13 +383,19 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
         const long long idx = ch * vpw + lane;
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0u;
-        const int d = v >= 0 ? g.deg[v] : 0;
-        const int bc = v >= 0 ? g.lcur[v] : 0;
-        const long long rs0 = v >= 0 ? g.rp[v] : 0;
-        const int len = d - bc;
-        s_start[w][lane] = rs0 + bc;
+        const int lc = v >= 0 ? g.lcur[v] : 0;
+        const long long r0 = v >= 0 ? g.rp[v] : 0;
+        int len = 0;
+        if (v >= 0 && lc >= 0) {  // first light scan: the row from the cursor
+            len = g.deg[v] - lc;
+            s_src[w][lane] = g.col + r0 + lc;
+        } else if (v >= 0) {  // the still-pending entries
+            len = -lc - 1;
+            s_src[w][lane] = B.pend + r0;
+        }
+        s_dst[w][lane] = B.pend + r0;
         s_flag[w][lane] = 0;
-        s_first[w][lane] = 0x7FFFFFFF;
+        s_np[w][lane] = 0;
         s_v[w][lane] = v;
         s_c6[w][lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
         s_cv[w][lane] = v >= 0 ? b_cand(g, v, kv) : -1;
@@ -337,16 +403,28 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
         const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
-        gc_chunk_edges_at(
-            g.col, s_start[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
-            [&](int o, int u, unsigned ku, int slot) {
+        b_chunk_edges(
+            s_src[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
+            [&](int o, int u, unsigned ku, int) {
                 const unsigned f = b_adm_flag(g, s_v[w][o], u, ku, s_c6[w][o], s_cv[w][o], ev);
                 if (f) atomicOr(&s_flag[w][o], f);
-                if (f == 2u) atomicMin(&s_first[w][o], slot);
+                if (f == 2u) s_dst[w][o][atomicAdd(&s_np[w][o], 1)] = u;
             });
         gc_wave_sync();
         int kind = -1;
-        if (v >= 0) b_adm_decide(g, B, c, ws, v, kv, s_flag[w][lane], s_first[w][lane], &kind);
+        if (v >= 0) {
+            const unsigned f = s_flag[w][lane];
+            if (f & 1u) {
+                g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_OUT);
+            } else if (f & 2u) {
+                g.lcur[v] = -s_np[w][lane] - 1;
+                kind = 0;
+            } else {
+                g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
+                g.lcur[v] = GC_B_EVCOL;
+                kind = 2;
+            }
+        }
         gc_wave_append(kind == 1, v, B.l[1][ws], b_cnt(c, 1, ws));
         gc_stage_push(st, kind == 0, v, B.l[0][ws], b_cnt(c, 0, ws));
         gc_stage_push(est, kind == 2, v, B.l[2][ws], b_cnt(c, 2, ws));
@@ -509,6 +587,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     int* const wl[9] = {g->undL[0], g->undL[1], g->undL[2], g->seeds[0], g->seeds[1], g->bigw,
                         g->undH[0], g->undH[1], g->undH[2]};
     for (int k = 0; k < 9; ++k) B.l[k / 3][k % 3] = wl[k];
+    if (!g->bpend && g->nnz > 0) GC_HIP(gc_dmalloc((void**)&g->bpend, sizeof(int) * (size_t)g->nnz));
+    B.pend = g->bpend;
     std::vector<RoundRec> recs;
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;

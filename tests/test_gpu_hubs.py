@@ -49,15 +49,15 @@ SETTINGS = [
     {"GC_HUB_T": "3", "GC_ASYNC_BPC": "1"},                   # one workgroup per CU
     {"GC_HUB_T": "0", "GC_ASYNC": "0"},                       # round 2's full-grid sweeps + tail
     {"GC_HUB_T": "off", "GC_ASYNC": "0"},
-    {"GC_HUB_T": "0", "GC_INLINE_PB": "1"},                   # small rounds' hubs and wide lights in k_propose<1>
-    {"GC_HUB_T": "512", "GC_INLINE_PB": "1"},
-    {"GC_HUB_T": "1024", "GC_INLINE_PB": "1", "GC_ASYNC": "0"},
-    {"GC_HUB_T": "2", "GC_HUB_W": "2", "GC_INLINE_PB": "1"},  # a 64-colour bitmap: inline only while colours are few
+    {"GC_HUB_T": "0", "GC_INLINE_PB": "0"},                   # every round's hubs and wide lights in k_propose_block
+    {"GC_HUB_T": "512", "GC_INLINE_PB": "0"},
+    {"GC_HUB_T": "1024", "GC_ASYNC": "0"},                    # k_propose<1> with the full-grid sweeps
+    {"GC_HUB_T": "2", "GC_HUB_W": "2"},                       # a 64-colour bitmap: inline only while colours are few
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
        "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
        "T2loop", "offloop8", "T0async_abort", "T2async_abort", "offasync_abort", "T3async_bpc1",
-       "T0sync", "offsync", "T0inl", "T512inl", "T1024inl_sync", "T2w2inl"]
+       "T0sync", "offsync", "T0noinl", "T512noinl", "T1024sync", "T2w2"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
