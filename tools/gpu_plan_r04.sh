@@ -50,6 +50,15 @@ case ${1:-} in
                  ab:rmat24:6:base,inl=GC_INLINE_PB:1,abig0=GC_ASYNC_BIG:0,both=GC_INLINE_PB:1+GC_ASYNC_BIG:0
                  ab:rmat26:3:base,inl=GC_INLINE_PB:1,abig0=GC_ASYNC_BIG:0
                  brounds:rmat24) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g" >&2; exit 2 ;;
+  # h: variant B's fold with compacted pending entries and the one-workgroup tail (its parity
+  #    tests first), its bench and per-round cost, the tail A/B; the inline hub proposals (now
+  #    on by default) through the hub and resume tests
+  h) exec_steps=(file:tests/test_gpu_variant_b.py file:tests/test_gpu_hubs.py file:tests/test_gpu_resume.py
+                 "bench:rmat24:--variant,B,--steps,5,--warmup,1"
+                 env:AB_VARIANT=B ab:rmat24:3:base,tail0=GC_B_TAIL:0,tailbig=GC_B_TAIL_L:16384+GC_B_TAIL_E:32768
+                 ab:uniform10M:4:base,tail0=GC_B_TAIL:0 env:AB_VARIANT=
+                 brounds:rmat24
+                 ab:rmat24:4:base,noinl=GC_INLINE_PB:0) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
