@@ -549,18 +549,19 @@ def main():
     ap.add_argument("--workload", default="rmat24", choices=sorted(WORKLOADS))
     ap.add_argument("--variant", default="A", choices=["A", "B"],
                     help="A = coloring.py semantics, B = coloring_optimized.py ('Optimizovano')")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak grows the graph with N, strong keeps the workload's graph")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="N > 1: weak grows the graph with N, strong keeps the workload's graph (default: strong "
+                         "for the modes that split one colouring -- hybrid, sharded -- weak for replicated / replicas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--multi", default="replicated", choices=["replicated", "replicas", "sharded", "hybrid"],
-                    help="N>1: replicated (default) -- every rank runs the one-GPU engine on the whole graph, no "
+    ap.add_argument("--multi", default="hybrid", choices=["replicated", "replicas", "sharded", "hybrid"],
+                    help="N>1: hybrid (default) -- one graph, sharded rounds while the frontier is large, then every "
+                         "rank resumes the one-GPU engine from the replicated state (gcolor_amd.shard.hybrid_color; "
+                         "DESIGN.md §7); replicated -- every rank runs the one-GPU engine on the whole graph, no "
                          "exchange, the job's time is the slowest rank's; replicas -- N independent colourings, one "
                          "base-size graph per rank (seed + rank), value = all ranks' edges / the slowest rank's time "
                          "(throughput of many graphs, not of one); sharded -- one graph cut into vertex-range "
-                         "shards with round seams over RCCL (gcolor_amd.shard; slower than one GPU, DESIGN.md §7); "
-                         "hybrid -- sharded rounds while the frontier is large, then every rank resumes the one-GPU "
-                         "engine from the replicated state (gcolor_amd.shard.hybrid_color)")
+                         "shards with round seams over RCCL in every round (gcolor_amd.shard; DESIGN.md §7)")
     ap.add_argument("--switch-below", type=int, default=0,
                     help="hybrid: frontier size below which the ranks switch to the one-GPU engine "
                          "(0: max(4096, n / 64))")
@@ -583,6 +584,8 @@ def main():
     ap.add_argument("--no-event-timing", action="store_true",
                     help="time the steps without per-launch HIP events (roofline fields then empty)")
     args = ap.parse_args()
+    if args.scaling is None:
+        args.scaling = "strong" if args.multi in ("hybrid", "sharded") else "weak"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
