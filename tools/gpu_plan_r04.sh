@@ -59,6 +59,13 @@ case ${1:-} in
                  ab:uniform10M:4:base,tail0=GC_B_TAIL:0 env:AB_VARIANT=
                  brounds:rmat24
                  ab:rmat24:4:base,noinl=GC_INLINE_PB:0) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h" >&2; exit 2 ;;
+  # i: variant B with the eviction watch and the fused pass (parity first), its A/Bs and per-round
+  #    cost; the N>1 default (hybrid, strong scaling) rehearsed as two ranks on this one GPU
+  i) exec_steps=(file:tests/test_gpu_variant_b.py
+                 env:AB_VARIANT=B ab:rmat24:3:base,unfused=GC_B_FUSED:0,tail=GC_B_TAIL:1
+                 ab:uniform10M:4:base,unfused=GC_B_FUSED:0 env:AB_VARIANT=
+                 brounds:rmat24
+                 "torchrun:2:--steps,2,--warmup,1,--no-north-star") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"

@@ -17,6 +17,7 @@
 #   rounds:WL         per-round kernel cost by frontier size (tools/round_cost.py under
 #                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
 #   brounds:WL        variant B's per-round cost (tools/b_round_cost.py, likewise)
+#   torchrun:N[:ARGS] bench.py --gpus N under torch.distributed.run, every rank on GPU 0, gloo
 #   ab:WL:REPS:CFGS   tools/ab_steps.py WL REPS CFG... (CFGS comma-separated, each NAME=VAR:val+VAR:val):
 #                     interleaved in-process A/B of environment knobs, colourings checked equal
 #   abl:WL:REPS:CYCLES:VARS  tools/ab_libs.sh: compile-time variants, a process each, alternated
@@ -96,6 +97,13 @@ for st in "$@"; do
         python tools/b_round_cost.py analyze "$tr" "$O/brounds_$rest/records.json" \
           > "$O/brounds_$rest/b_round_cost.txt" 2>> "$log" &&
         rm -f "$tr" && cat "$O/brounds_$rest/b_round_cost.txt" >> "$log" ;;
+    torchrun)
+      # the N-rank bench on this box's one GPU: every rank pinned to GPU 0 (GC_BENCH_DEVICE),
+      # the exchanges over gloo (two processes cannot share a GPU in one RCCL group)
+      np_=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      GC_BENCH_DEVICE=0 GC_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$np_" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$np_" ${a//,/ } \
+        --json-out "$O/bench_torchrun$np_.json" > "$log" 2>&1 ;;
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
