@@ -210,12 +210,20 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         const int d = v >= 0 ? g.deg[v] : 0;
         const int lc = v >= 0 ? g.lcur[v] : GC_B_EVCOL;
         const long long r0 = v >= 0 ? g.rp[v] : 0;
+        // Watch: after its first scan, ev(v) can only move when the evictor it names is
+        // refused -- while that one is undecided v stays listed unscanned, once it is admitted
+        // ev(v) is final; only a refusal asks for a rescan of the kept entries.
+        int watch = 0;  // 1: still pending, no scan; 2: final, no scan
+        if (v >= 0 && lc != GC_B_EVCOL) {
+            const unsigned st = gc_k8_state(k8[ev[v]]);
+            watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
+        }
         int len = 0;
         if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's higher-rank part
             const int lo = g.nlow[v];
             len = d - lo;
             s_src[w][lane] = g.col + r0 + lo;
-        } else if (v >= 0) {  // the kept potential evictors
+        } else if (v >= 0 && watch == 0) {  // the kept potential evictors
             len = -lc - 1;
             s_src[w][lane] = B.pend + r0;
         }
@@ -250,8 +258,8 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
                 s_dst[w][o][atomicAdd(&s_np[w][o], 1)] = (int)((unsigned)u | GC_B_PMARK);
             });
         gc_wave_sync();
-        bool pend = false;
-        if (v >= 0) {
+        bool pend = watch == 1;
+        if (v >= 0 && watch == 0) {
             const int e = s_min[w][lane];
             ev[v] = e;
             pend = e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN;
@@ -437,6 +445,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
     b_adm_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
+// One fold pass in ONE launch (round 4, GC_B_FUSED): every workgroup runs its slice of the
+// eviction pass, then its slice of the admission pass, with no grid barrier between them.
+// An admission may then read an eviction time this pass has not updated yet: it is the
+// previous pass's, a lower bound all the same (refusals only raise it), and an eviction is
+// only ever taken as final when the evictor named is admitted -- so staleness can delay a
+// decision by a pass, never change it.  Both halves read slot pass % 3 and append to slot
+// (pass + 1) % 3, as the two launches do.
+__global__ void __launch_bounds__(GC_BLOCK) k_b_pass(GDev g, BLists B, int* ev, int pass) {
+    b_ev_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
+    b_adm_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
+}
+
 // The rest of a round's fold in ONE workgroup (round 4, GC_B_TAIL): after the host's
 // full-grid passes, the fold's deep end is a chain of passes over a few hundred vertices
 // each -- two 2048-workgroup launches apiece.  Here they run back to back, a workgroup
@@ -556,10 +576,12 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const int grid_ev = getenv("GC_GRID_BE") && atoi(getenv("GC_GRID_BE")) > 0 ? atoi(getenv("GC_GRID_BE")) : GC_ROUND_GRID;
     const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
                          : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
-    // GC_B_TAIL=0: every fold pass a pair of full-grid launches (round 3); else the fold's deep
-    // end runs in k_b_tail's one workgroup while the lists are within GC_B_TAIL_L light
-    // admissions, GC_B_TAIL_H heavy admissions and GC_B_TAIL_E evictions
-    const bool tail_on = !(getenv("GC_B_TAIL") && atoi(getenv("GC_B_TAIL")) == 0);
+    // GC_B_TAIL=1: the fold's deep end runs in k_b_tail's one workgroup while the lists are
+    // within GC_B_TAIL_L light admissions, GC_B_TAIL_H heavy admissions and GC_B_TAIL_E
+    // evictions (round 4: off by default, R-MAT-24 656.5 -> 722.9 ms with it, profiles/r04/h)
+    const bool tail_on = getenv("GC_B_TAIL") && atoi(getenv("GC_B_TAIL")) > 0;
+    // GC_B_FUSED=0: a pass's eviction and admission halves as two launches (round 3)
+    const bool fused = !(getenv("GC_B_FUSED") && atoi(getenv("GC_B_FUSED")) == 0);
     const long long tail_l = getenv("GC_B_TAIL_L") ? atoll(getenv("GC_B_TAIL_L")) : 2048;
     const long long tail_h = getenv("GC_B_TAIL_H") ? atoll(getenv("GC_B_TAIL_H")) : 4;
     const long long tail_e = getenv("GC_B_TAIL_E") ? atoll(getenv("GC_B_TAIL_E")) : 4096;
@@ -617,6 +639,10 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         auto enqueue_passes = [&](long long k) {
             for (long long j = 0; j < k; ++j, ++passes, ++full) {
                 const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
+                if (fused) {
+                    hipLaunchKernelGGL(k_b_pass, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+                    continue;
+                }
                 hipLaunchKernelGGL(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
                 hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
