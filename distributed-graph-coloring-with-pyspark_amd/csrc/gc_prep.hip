@@ -179,6 +179,7 @@ struct TileLdsP {  // rank partition, hub fill
 struct TileLdsV {  // validation
     int off[GC_TW + 1];
     unsigned key[GC_TW];
+    int nl[GC_TW];
     int buf[GC_TW + GC_TH];
     ull w[GC_WAVES_PER_BLOCK];
     ull misc[4];
@@ -529,10 +530,17 @@ __device__ __forceinline__ bool same_colour8(const int* colors, int u, unsigned 
     const unsigned cv8 = gc_c8_of(cv);
     return cu8 == cv8 && (cv8 != GC_C8_BIG || colors[u] == cv);
 }
+// HALF (round 4; symmetric graphs): an entry (v, u), u != v, and its mirror (u, v) are one
+// conflict each or neither, and exactly one of them lies in a low part (the rank partition:
+// lower rank first; a strict order, so a self-loop is never low).  So the directed count is
+// 2 x the conflicts of the low parts + the self-loop entries (a self-loop always conflicts),
+// and only the low entries are gathered: half the gathers, col still read whole (the rows
+// are staged tile by tile).  Duplicates mirror too: each copy counts on both sides.
 
-template <int C8>
+template <int C8, int HALF>
 __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors,
-                                                             const unsigned char* c8, ull* unc_out, ull* conf_out) {
+                                                             const unsigned char* c8, const int* nlow, ull* unc_out,
+                                                             ull* conf_out) {
     __shared__ TileLdsV S;
     const long long nt = T.ntiles, ns = nseg_of(T);
     ull unc = 0, conf = 0;
@@ -546,49 +554,66 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
             for (int i = threadIdx.x; i < R; i += blockDim.x) {
                 const int cv = colors[r0 + i];
                 S.key[i] = (unsigned)cv;
+                if (HALF) S.nl[i] = nlow[r0 + i];
                 unc += cv == -1;
             }
             for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = col[eb + i];
             __syncthreads();
             int u[GC_PER], rk[GC_PER];
             const int nv = thread_entries(S, R, NE, u, rk);
+            bool on[GC_PER];  // entries whose colour is gathered
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                on[k] = k < nv;
+                if (HALF && on[k]) {
+                    const int j = threadIdx.x * GC_PER + k;  // thread_entries' entry j0 + k
+                    conf += u[k] == r0 + rk[k] ? 1 : 0;     // a self-loop
+                    on[k] = j - S.off[rk[k]] < S.nl[rk[k]];
+                }
+            }
             int cu[GC_PER];
 #pragma unroll
-            for (int k = 0; k < GC_PER; ++k) cu[k] = k < nv ? (C8 ? (int)c8[u[k]] : colors[u[k]]) : 0;
+            for (int k = 0; k < GC_PER; ++k) cu[k] = on[k] ? (C8 ? (int)c8[u[k]] : colors[u[k]]) : 0;
+            ull lc = 0;
             if (C8) {
 #pragma unroll
                 for (int k = 0; k < GC_PER; ++k)
-                    conf += (k < nv && same_colour8(colors, u[k], (unsigned)cu[k], (int)S.key[rk[k]])) ? 1 : 0;
+                    lc += (on[k] && same_colour8(colors, u[k], (unsigned)cu[k], (int)S.key[rk[k]])) ? 1 : 0;
             } else {
 #pragma unroll
-                for (int k = 0; k < GC_PER; ++k) conf += (k < nv && cu[k] == (int)S.key[rk[k]]) ? 1 : 0;
+                for (int k = 0; k < GC_PER; ++k) lc += (on[k] && cu[k] == (int)S.key[rk[k]]) ? 1 : 0;
             }
+            conf += HALF ? 2 * lc : lc;
         } else {
             const long long s = it - nt;
             const int v = T.seg_row[s], j = T.seg_j[s];
             const long long rs = T.rp[v], d = T.rp[v + 1] - rs;
             const long long e0 = rs + (long long)j * GC_SEG;
             const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            const int lowlen = HALF ? (int)std::max<long long>(0, std::min<long long>(len, nlow[v] - (long long)j * GC_SEG)) : len;
             const int cv = colors[v];
             int uu[GC_PER], cu[GC_PER];
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {  // coalesced: entry threadIdx + k * 256
                 const int i = threadIdx.x + k * GC_BLOCK;
                 uu[k] = i < len ? col[e0 + i] : 0;
+                if (HALF) conf += (i < len && uu[k] == v) ? 1 : 0;  // a self-loop
             }
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {
                 const int i = threadIdx.x + k * GC_BLOCK;
-                cu[k] = i < len ? (C8 ? (int)c8[uu[k]] : colors[uu[k]]) : 0;
+                cu[k] = i < lowlen ? (C8 ? (int)c8[uu[k]] : colors[uu[k]]) : 0;
             }
+            ull lc = 0;
             if (C8) {
 #pragma unroll
                 for (int k = 0; k < GC_PER; ++k)
-                    conf += (threadIdx.x + k * GC_BLOCK < len && same_colour8(colors, uu[k], (unsigned)cu[k], cv)) ? 1 : 0;
+                    lc += (threadIdx.x + k * GC_BLOCK < lowlen && same_colour8(colors, uu[k], (unsigned)cu[k], cv)) ? 1 : 0;
             } else {
 #pragma unroll
-                for (int k = 0; k < GC_PER; ++k) conf += (threadIdx.x + k * GC_BLOCK < len && cu[k] == cv) ? 1 : 0;
+                for (int k = 0; k < GC_PER; ++k) lc += (threadIdx.x + k * GC_BLOCK < lowlen && cu[k] == cv) ? 1 : 0;
             }
+            conf += HALF ? 2 * lc : lc;
         }
         __syncthreads();
     }
@@ -859,12 +884,22 @@ int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8) {
     if (g->n == 0) return GC_OK;
     int rc = gc_build_tiling(g);
     if (rc) return rc;
-    if (c8)
-        hipLaunchKernelGGL(k_validate_tiles<1>, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
-                           (const int*)g->col, colors, c8, &g->ctl->uncolored, &g->ctl->conflicts);
+    // symmetric graphs: the low parts only (k_validate_tiles' HALF; GC_VALIDATE_HALF=0 reads every entry)
+    const bool half = (g->flags & GC_GRAPH_SYMMETRIC) && g->nlow &&
+                      !(getenv("GC_VALIDATE_HALF") && atoi(getenv("GC_VALIDATE_HALF")) == 0);
+    const Tiles T = tiles_of(g);
+    const int grid = prep_grid(g);
+    ull* unc = &g->ctl->uncolored;
+    ull* conf = &g->ctl->conflicts;
+    const int* nl = g->nlow;
+    if (c8 && half)
+        hipLaunchKernelGGL((k_validate_tiles<1, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+    else if (c8)
+        hipLaunchKernelGGL((k_validate_tiles<1, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+    else if (half)
+        hipLaunchKernelGGL((k_validate_tiles<0, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
     else
-        hipLaunchKernelGGL(k_validate_tiles<0>, dim3(prep_grid(g)), dim3(GC_BLOCK), 0, g->stream, tiles_of(g),
-                           (const int*)g->col, colors, c8, &g->ctl->uncolored, &g->ctl->conflicts);
+        hipLaunchKernelGGL((k_validate_tiles<0, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
     GC_HIP(hipGetLastError());
     return GC_OK;
 }

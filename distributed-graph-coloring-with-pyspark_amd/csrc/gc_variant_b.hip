@@ -445,17 +445,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
     b_adm_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
-// One fold pass in ONE launch (round 4, GC_B_FUSED): every workgroup runs its slice of the
-// eviction pass, then its slice of the admission pass, with no grid barrier between them.
-// An admission may then read an eviction time this pass has not updated yet: it is the
-// previous pass's, a lower bound all the same (refusals only raise it), and an eviction is
-// only ever taken as final when the evictor named is admitted -- so staleness can delay a
-// decision by a pass, never change it.  Both halves read slot pass % 3 and append to slot
-// (pass + 1) % 3, as the two launches do.
-__global__ void __launch_bounds__(GC_BLOCK) k_b_pass(GDev g, BLists B, int* ev, int pass) {
-    b_ev_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
-    b_adm_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
-}
+// (Round 4 measured a pass's eviction and admission halves in ONE launch, no grid barrier
+// between them: R-MAT-24 656 -> 1000 ms, uniform 10M 20.7 -> 24.7 ms, profiles/r04/i; removed.)
 
 // The rest of a round's fold in ONE workgroup (round 4, GC_B_TAIL): after the host's
 // full-grid passes, the fold's deep end is a chain of passes over a few hundred vertices
@@ -580,8 +571,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // within GC_B_TAIL_L light admissions, GC_B_TAIL_H heavy admissions and GC_B_TAIL_E
     // evictions (round 4: off by default, R-MAT-24 656.5 -> 722.9 ms with it, profiles/r04/h)
     const bool tail_on = getenv("GC_B_TAIL") && atoi(getenv("GC_B_TAIL")) > 0;
-    // GC_B_FUSED=0: a pass's eviction and admission halves as two launches (round 3)
-    const bool fused = !(getenv("GC_B_FUSED") && atoi(getenv("GC_B_FUSED")) == 0);
     const long long tail_l = getenv("GC_B_TAIL_L") ? atoll(getenv("GC_B_TAIL_L")) : 2048;
     const long long tail_h = getenv("GC_B_TAIL_H") ? atoll(getenv("GC_B_TAIL_H")) : 4;
     const long long tail_e = getenv("GC_B_TAIL_E") ? atoll(getenv("GC_B_TAIL_E")) : 4096;
@@ -639,10 +628,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         auto enqueue_passes = [&](long long k) {
             for (long long j = 0; j < k; ++j, ++passes, ++full) {
                 const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
-                if (fused) {
-                    hipLaunchKernelGGL(k_b_pass, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
-                    continue;
-                }
                 hipLaunchKernelGGL(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
                 hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }

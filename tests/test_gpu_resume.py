@@ -234,3 +234,37 @@ def test_validate_c8_matches(monkeypatch):
         assert dg.validate() == ref == tuple(oracle.c_validate(rp, col, g.colors))
         assert ref[1] > 0
 
+
+
+@pytest.mark.parametrize("half", ["1", "0"], ids=["low_parts", "every_entry"])
+def test_validate_symmetric_half(monkeypatch, half):
+    """gc_validate of a symmetric graph reads only the low parts of the rank partition and counts
+    2 x their conflicts + the self-loop entries (round 4; GC_VALIDATE_HALF=0 reads every entry):
+    equal to the oracle's directed count (coloring.py:149-162) on a symmetric multigraph with
+    duplicates, self-loops and a row past the tile height (its segments), under arbitrary colour
+    arrays (uncoloured, colours < 254 and >= 254) and after real colourings."""
+    from gcolor_amd.engine import DeviceGraph
+    monkeypatch.setenv("GC_VALIDATE_HALF", half)
+    rng = np.random.default_rng(11)
+    n = 6000
+    a = rng.integers(0, n, 40000)
+    b = rng.integers(0, n, 40000)
+    a = np.concatenate([a, np.zeros(3000, np.int64), a[:500]])  # vertex 0 a row of > 3000 entries; duplicates
+    b = np.concatenate([b, rng.integers(1, n, 3000), b[:500]])
+    keep = a != b
+    src = np.concatenate([a[keep], b[keep], np.arange(0, n, 97)])  # self-loops: one entry each
+    dst = np.concatenate([b[keep], a[keep], np.arange(0, n, 97)])
+    order = np.lexsort((dst, src))
+    src, dst = src[order], dst[order]
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    rp = np.cumsum(rp)
+    col = dst.astype(np.int32)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("A")
+        assert tuple(dg.validate()) == tuple(oracle.c_validate(rp, col, g.colors))
+        g = dg.color("A", num_colors=2)  # failed: uncoloured vertices
+        assert tuple(dg.validate()) == tuple(oracle.c_validate(rp, col, g.colors))
+        for palette in (3, 400):
+            c = rng.integers(-1, palette, n).astype(np.int32)
+            assert tuple(dg.validate(c)) == tuple(oracle.c_validate(rp, col, c))

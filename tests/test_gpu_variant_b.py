@@ -147,22 +147,20 @@ def test_variant_b_hub_bitmaps(monkeypatch, hub_t, hub_w):
 
 
 TAIL_SETTINGS = [
-    {},                                                                   # one fused launch per pass
-    {"GC_B_FUSED": "0"},                                                  # eviction and admission launches
+    {},                                                                   # full-grid passes
     {"GC_B_TAIL": "1"},                                                   # the one-workgroup tail, default caps
     {"GC_B_TAIL": "1", "GC_B_TAIL_L": "16", "GC_B_TAIL_H": "0", "GC_B_TAIL_E": "16"},  # hands back, takes over often
-    {"GC_B_TAIL": "1", "GC_B_TAIL_L": "1000000", "GC_B_TAIL_H": "64", "GC_B_TAIL_E": "1000000",
-     "GC_B_FUSED": "0"},                                                  # whole folds after one full pass
+    {"GC_B_TAIL": "1", "GC_B_TAIL_L": "1000000", "GC_B_TAIL_H": "64", "GC_B_TAIL_E": "1000000"},  # whole folds
 ]
 
 
-@pytest.mark.parametrize("env", TAIL_SETTINGS, ids=["fused", "unfused", "tail", "tail_small", "tail_all"])
+@pytest.mark.parametrize("env", TAIL_SETTINGS, ids=["grid", "tail", "tail_small", "tail_all"])
 def test_variant_b_fold_tail(monkeypatch, env):
-    """The fold's passes: one fused launch each (the default), two launches each, and the deep
-    end in k_b_tail's one workgroup (GC_B_TAIL=1) with the default caps, tiny caps (passes
-    alternate between the grid and the workgroup) and caps that take whole folds, heavy
-    admissions included -- every run equal to the oracle."""
-    for k in ("GC_B_TAIL", "GC_B_TAIL_L", "GC_B_TAIL_H", "GC_B_TAIL_E", "GC_B_FUSED"):
+    """The fold's passes on the full grid (the default) and the deep end in k_b_tail's one
+    workgroup (GC_B_TAIL=1) with the default caps, tiny caps (passes alternate between the grid
+    and the workgroup) and caps that take whole folds after one full pass, heavy admissions
+    included -- every run equal to the oracle."""
+    for k in ("GC_B_TAIL", "GC_B_TAIL_L", "GC_B_TAIL_H", "GC_B_TAIL_E"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
