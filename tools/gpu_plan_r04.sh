@@ -66,6 +66,13 @@ case ${1:-} in
                  ab:uniform10M:4:base,unfused=GC_B_FUSED:0 env:AB_VARIANT=
                  brounds:rmat24
                  "torchrun:2:--steps,2,--warmup,1,--no-north-star") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i" >&2; exit 2 ;;
+  # j: validation from the low parts (symmetric graphs), its A/B on the step; variant B's tail
+  #    with small caps and the per-round cost of the two-launch passes with the eviction watch
+  j) exec_steps=(file:tests/test_gpu_resume.py file:tests/test_gpu_variant_b.py
+                 ab:rmat26:3:base,nohalf=GC_VALIDATE_HALF:0 ab:rmat24:5:base,nohalf=GC_VALIDATE_HALF:0
+                 env:AB_VARIANT=B
+                 ab:rmat24:3:base,tail256=GC_B_TAIL:1+GC_B_TAIL_L:256+GC_B_TAIL_H:0+GC_B_TAIL_E:512,tail64=GC_B_TAIL:1+GC_B_TAIL_L:64+GC_B_TAIL_H:0+GC_B_TAIL_E:128
+                 env:AB_VARIANT= brounds:rmat24) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
