@@ -117,7 +117,7 @@ __device__ __forceinline__ long long b_count(DevCtl* c, int kind, int slot) {
     return TAIL ? (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (long long)*p;
 }
 
-// gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]
+// gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]; load(o, u)
 template <typename Load, typename Apply>
 __device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl, int total, Load load, Apply apply) {
     const int lane = gc_lane();
@@ -133,9 +133,9 @@ __device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl,
         }
 #pragma unroll
         for (int k = 0; k < GC_SLOTS; ++k) u[k] = ok[k] ? s_src[o[k]][x[k]] : 0;
-        decltype(load(0)) gv[GC_SLOTS];
+        decltype(load(0, 0)) gv[GC_SLOTS];
 #pragma unroll
-        for (int k = 0; k < GC_SLOTS; ++k) gv[k] = ok[k] ? load(u[k]) : decltype(load(0)){};
+        for (int k = 0; k < GC_SLOTS; ++k) gv[k] = ok[k] ? load(o[k], u[k]) : decltype(load(0, 0)){};
 #pragma unroll
         for (int k = 0; k < GC_SLOTS; ++k)
             if (ok[k]) apply(o[k], u[k], gv[k], x[k]);
@@ -242,7 +242,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         // candidate): only its state can change
         b_chunk_edges(
             s_src[w], excl, total,
-            [&](int um) {
+            [&](int, int um) {
                 const int u = um & 0x7FFFFFFF;
                 return ((unsigned)um & GC_B_PMARK) ? (ull)k8[u] : ((ull)(unsigned)g.deg[u] << 32) | (ull)k8[u];
             },
@@ -412,7 +412,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
         gc_wave_sync();
         b_chunk_edges(
-            s_src[w], excl, total, [&](int u) { return (unsigned)k8[u]; },
+            s_src[w], excl, total, [&](int, int u) { return (unsigned)k8[u]; },
             [&](int o, int u, unsigned ku, int) {
                 const unsigned f = b_adm_flag(g, s_v[w][o], u, ku, s_c6[w][o], s_cv[w][o], ev);
                 if (f) atomicOr(&s_flag[w][o], f);
@@ -520,6 +520,294 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const i
 // (Round 3's asynchronous fold -- the round's passes in one launch on a resident grid,
 // GC_B_ASYNC=1 -- measured R-MAT-24 855.6 -> 1036.9 ms in round 4, profiles/r04/c: removed.)
 
+// ------------------------------------------------------------------------------------
+// Asynchronous fold (round 4, GC_B_ASYNC): after the host's first full-grid passes (the
+// bandwidth-bound first scans, which leave every light vertex's pending entries compacted),
+// the rest of the round's fold in ONE launch on a resident grid, with no host round trip and
+// no launch per pass.  Every wave owns a static slice of the round's items -- light
+// admissions and eviction times (edge-balanced wave chunks over their pending / kept
+// entries, as k_b_adm / k_b_ev) and heavy admissions (a wave each, a resumable scan that
+// stops at the first refusing or undecided entry) -- and passes over its unsettled items
+// until none is left; an admitted vertex becomes an eviction item of the same wave.  Every
+// decision is monotone (UND -> IN / OUT; eviction times only grow and are final once the
+// evictor named is admitted or there is none) and the earliest unsettled item in arrival
+// order can always settle, so the waves converge without waiting on each other.  States
+// and eviction times other waves read are stored and loaded agent-scope (sc1); a vertex's
+// cursor, pending entries and own byte are only ever touched by its own wave.  A wave past
+// the budget hands its unsettled items to the pass lists of the next slot and the host's
+// passes finish them.  (Round 3's asynchronous fold ran from the round's first pass,
+// rescanning whole rows: 21% slower than the passes, removed in round 4.)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ bool b_async_stop(DevCtl* c, ull t0, long long budget) {
+    int stop = 0;
+    if (gc_lane() == 0) {
+        stop = __hip_atomic_load(&c->async_abort[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!stop && (long long)(wall_clock64() - t0) > budget) {
+            stop = 1;
+            if (atomicCAS(&c->async_abort[0], 0, 1) == 0) atomicAdd(&c->async_aborts, 1ull);
+        }
+    }
+    return __shfl(stop, 0, GC_WAVE) != 0;
+}
+
+// a work item is v | kind << GC_BI_SHIFT (kind 0 admission, 2 eviction time): non-negative
+// for n < 2^29 (-1 marks an empty lane), so the host runs k_b_async only below that
+#define GC_BI_SHIFT 29
+#define GC_BI_MASK ((1 << GC_BI_SHIFT) - 1)
+
+// b_adm_flag with agent-scope loads of the states and eviction times other waves write
+__device__ __forceinline__ unsigned b_adm_flag_a(const GDev& g, int vo, int u, unsigned ku, unsigned c6, int cv,
+                                                 const int* ev) {
+    if (u >= vo) return 0u;
+    const unsigned st = gc_k8_state(ku);
+    if (st == GC_JP_OUT || !b_same(g, u, ku, c6, cv)) return 0u;
+    if (st != GC_JP_IN) return 2u;
+    const int e = gc_aldi(ev + u);
+    if (e > vo) return 1u;
+    if (e >= 0 && gc_k8_state(gc_ald8(g.k8 + e)) == GC_JP_IN) return 0u;
+    return 2u;
+}
+
+struct BAsyncLds {  // one wave's rows
+    const int* src[GC_WAVE];
+    int* dst[GC_WAVE];
+    unsigned flag[GC_WAVE];
+    int np[GC_WAVE];
+    int minv[GC_WAVE];
+    int v[GC_WAVE];
+    int d[GC_WAVE];
+    unsigned c6[GC_WAVE];
+    int cv[GC_WAVE];
+    int kind[GC_WAVE];
+};
+
+// one pass over the wave's light admission / eviction items l1[0, n1); the unsettled ones
+// are compacted to the front (an admitted vertex comes back as an eviction item); returns
+// their number
+__device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s) {
+    const int lane = gc_lane();
+    int nw = 0;
+    for (int c0 = 0; c0 < n1; c0 += GC_WAVE) {
+        const int it = c0 + lane < n1 ? l1[c0 + lane] : -1;
+        const int v = it >= 0 ? (it & GC_BI_MASK) : -1;
+        const int kind = it >= 0 ? (it >> GC_BI_SHIFT) : -1;
+        const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // its candidate (fixed for the round)
+        const int d = v >= 0 ? g.deg[v] : 0;
+        const int lc = v >= 0 ? g.lcur[v] : 0;
+        const long long r0 = v >= 0 ? g.rp[v] : 0;
+        int watch = 0;  // eviction items: 1 still pending, 2 final, no scan (b_ev_pass)
+        if (kind == 2 && lc != GC_B_EVCOL) {
+            const unsigned st = gc_k8_state(gc_ald8(g.k8 + ev[v]));
+            watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
+        }
+        int len = 0;
+        if (kind == 0) {
+            len = lc >= 0 ? d - lc : -lc - 1;
+            s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0;
+        } else if (kind == 2 && lc == GC_B_EVCOL) {
+            const int lo = g.nlow[v];
+            len = d - lo;
+            s.src[lane] = g.col + r0 + lo;
+        } else if (kind == 2 && watch == 0) {
+            len = -lc - 1;
+            s.src[lane] = B.pend + r0;
+        }
+        s.dst[lane] = B.pend + r0;
+        s.flag[lane] = 0;
+        s.np[lane] = 0;
+        s.minv[lane] = GC_B_INF;
+        s.v[lane] = v;
+        s.d[lane] = d;
+        s.c6[lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        s.cv[lane] = v >= 0 ? b_cand(g, v, kv) : -1;
+        s.kind[lane] = kind;
+        const int incl = gc_wave_incl_scan(len);
+        const int excl = incl - len;
+        const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        b_chunk_edges(
+            s.src, excl, total,
+            [&](int o, int um) {
+                const int u = um & 0x7FFFFFFF;
+                const ull k = (ull)gc_ald8(g.k8 + u);
+                return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
+            },
+            [&](int o, int um, ull du, int) {
+                const int u = um & 0x7FFFFFFF;
+                const unsigned ku = (unsigned)du & 0xFFu;
+                if (s.kind[o] == 0) {  // admission (k_b_adm)
+                    const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
+                    if (f) atomicOr(&s.flag[o], f);
+                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                } else {  // eviction time (k_b_ev)
+                    if (gc_k8_state(ku) == GC_JP_OUT) return;
+                    if (!((unsigned)um & GC_B_PMARK)) {
+                        if (u <= s.v[o] || (int)(du >> 32) <= s.d[o]) return;
+                        if (!b_same(g, u, ku, s.c6[o], s.cv[o])) return;
+                    }
+                    atomicMin(&s.minv[o], u);
+                    s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
+                }
+            });
+        gc_wave_sync();
+        int keep = -1;  // the item that stays (-1: settled)
+        if (kind == 0) {
+            const unsigned f = s.flag[lane];
+            if (f & 1u) {
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
+            } else if (f & 2u) {
+                g.lcur[v] = -s.np[lane] - 1;
+                keep = it;
+            } else {
+                g.lcur[v] = GC_B_EVCOL;
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_IN);
+                keep = v | (2 << GC_BI_SHIFT);  // admitted: its eviction time next
+            }
+        } else if (kind == 2) {
+            if (watch == 1) {
+                keep = it;
+            } else if (watch == 0) {
+                const int e = s.minv[lane];
+                gc_asti(ev + v, e);
+                if (e != GC_B_INF && gc_k8_state(gc_ald8(g.k8 + e)) != GC_JP_IN) {
+                    g.lcur[v] = -s.np[lane] - 1;
+                    keep = it;
+                }
+            }
+        }
+        const ull km = __ballot(keep >= 0);
+        if (keep >= 0) l1[nw + __popcll(km & gc_lanemask_lt())] = keep;
+        nw += __popcll(km);
+        gc_wave_sync();
+    }
+    return nw;
+}
+
+// one pass over the wave's heavy admissions l2[0, n2), one vertex at a time (the wave's
+// lanes over its row from the cursor, GC_HUB_UNR entries each in flight): a refusing entry
+// settles it OUT, the first undecided entry is its new cursor, the end of the row admits it
+// (appended to l1 as an eviction item at *n1).  Returns the heavy items left.
+__device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, int* ev) {
+    const int lane = gc_lane();
+    int nw = 0;
+    for (int i = 0; i < n2; ++i) {
+        const int v = l2[i];
+        const unsigned kv = g.k8[v];
+        const unsigned c6 = gc_k8_cand(kv);
+        const int cv = b_cand(g, v, kv);
+        const int d = g.deg[v];
+        const long long base = g.rp[v];
+        int pos = g.lcur[v];
+        bool refused = false;
+        int pend = -1;
+        while (pos < d && !refused && pend < 0) {
+            int u[GC_HUB_UNR];
+            unsigned f[GC_HUB_UNR];
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                const int e = pos + k * GC_WAVE + lane;
+                u[k] = e < d ? g.col[base + e] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k)
+                f[k] = u[k] >= 0 ? b_adm_flag_a(g, v, u[k], gc_ald8(g.k8 + u[k]), c6, cv, ev) : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_HUB_UNR; ++k) {
+                if (__ballot(f[k] == 1u)) refused = true;
+                const ull mb = __ballot(f[k] == 2u);
+                if (mb && pend < 0) pend = pos + k * GC_WAVE + __builtin_ctzll(mb);
+            }
+            pos += GC_HUB_UNR * GC_WAVE;
+        }
+        if (refused) {
+            if (lane == 0) gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
+        } else if (pend >= 0) {
+            if (lane == 0) {
+                g.lcur[v] = pend;
+                l2[nw] = v;
+            }
+            ++nw;
+        } else {
+            if (lane == 0) {
+                g.lcur[v] = GC_B_EVCOL;
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_IN);
+                l1[*n1] = v | (2 << GC_BI_SHIFT);
+            }
+            ++*n1;
+        }
+        gc_wave_sync();
+    }
+    return nw;
+}
+
+// pass `pass` of the round as one asynchronous launch: reads the three lists of slot
+// pass % 3, spills to slot (pass + 1) % 3, uses the arrays of slot (pass + 2) % 3 as the
+// waves' scratch and clears that slot's counts (as k_b_ev does)
+__global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev, int pass, long long budget) {
+    DevCtl* c = g.ctl;
+    const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
+    __shared__ BAsyncLds s_w[GC_WAVES_PER_BLOCK];
+    const int lane = gc_lane();
+    const int w = threadIdx.x / GC_WAVE;
+    const long long nA = (long long)*b_cnt(c, 0, rs), nH = (long long)*b_cnt(c, 1, rs), nE = (long long)*b_cnt(c, 2, rs);
+    const long long T = nA + nH + nE;
+    if (T > g.n) {  // never expected: report, touch nothing
+        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&c->loop_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 3) *b_cnt(c, threadIdx.x, zs) = 0ull;
+    const ull t0 = wall_clock64();
+    budget += 2 * T;
+    const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
+    const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+    const long long a = T * wid / W, b = T * (wid + 1) / W;
+    if (a >= b) return;
+    int* l1 = B.l[0][zs] + a;  // light admissions and eviction times
+    int* l2 = B.l[1][zs] + a;  // heavy admissions
+    int n1 = 0, n2 = 0;
+    for (long long i0 = a; i0 < b; i0 += GC_WAVE) {
+        const long long i = i0 + lane;
+        int v = -1, kind = -1;
+        if (i < b) {
+            if (i < nA) { v = B.l[0][rs][i]; kind = 0; }
+            else if (i < nA + nH) { v = B.l[1][rs][i - nA]; kind = 1; }
+            else { v = B.l[2][rs][i - nA - nH]; kind = 2; }
+        }
+        const ull m1 = __ballot(kind == 0 || kind == 2), m2 = __ballot(kind == 1);
+        if (kind == 0 || kind == 2) l1[n1 + __popcll(m1 & gc_lanemask_lt())] = v | (kind << GC_BI_SHIFT);
+        if (kind == 1) l2[n2 + __popcll(m2 & gc_lanemask_lt())] = v;
+        n1 += __popcll(m1);
+        n2 += __popcll(m2);
+    }
+    gc_wave_sync();
+    bool stop = false;
+    int idle = 0;
+    while (n1 + n2 > 0) {
+        const int before = n1 + n2;
+        n1 = b_async_chunk_pass(g, B, l1, n1, ev, s_w[w]);
+        if (n2) n2 = b_async_heavy_pass(g, l2, n2, l1, &n1, ev);
+        if (n1 + n2 == 0) break;
+        if ((stop = b_async_stop(c, t0, budget))) break;
+        if (n1 + n2 == before) {
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+        } else {
+            idle = 0;
+        }
+    }
+    if (!stop) return;
+    // hand the unsettled items to the host's passes (slot ws), by kind
+    for (int i0 = 0; i0 < n1; i0 += GC_WAVE) {
+        const int it = i0 + lane < n1 ? l1[i0 + lane] : -1;
+        const int kind = it >= 0 ? (it >> GC_BI_SHIFT) : -1;
+        gc_wave_append(kind == 0, it & GC_BI_MASK, B.l[0][ws], b_cnt(c, 0, ws));
+        gc_wave_append(kind == 2, it & GC_BI_MASK, B.l[2][ws], b_cnt(c, 2, ws));
+    }
+    for (int i0 = 0; i0 < n2; i0 += GC_WAVE) {
+        const int v = i0 + lane < n2 ? l2[i0 + lane] : -1;
+        gc_wave_append(v >= 0, v, B.l[1][ws], b_cnt(c, 1, ws));
+    }
+}
+
 struct RunB {
     gc_graph* g;
     GDev d;
@@ -571,6 +859,22 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // within GC_B_TAIL_L light admissions, GC_B_TAIL_H heavy admissions and GC_B_TAIL_E
     // evictions (round 4: off by default, R-MAT-24 656.5 -> 722.9 ms with it, profiles/r04/h)
     const bool tail_on = getenv("GC_B_TAIL") && atoi(getenv("GC_B_TAIL")) > 0;
+    // GC_B_ASYNC=1: after GC_B_ASYNC_K (default 1) full-grid passes, the rest of the round's
+    // fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2 workgroups);
+    // budget per launch GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item
+    int b_async_grid = 0;
+    long long b_async_budget = 0;
+    const long long b_async_k = getenv("GC_B_ASYNC_K") ? std::max(0ll, atoll(getenv("GC_B_ASYNC_K"))) : 1;
+    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0 && g->n < (1ll << GC_BI_SHIFT)) {  // items: 29-bit vertices
+        int cus = 0, rate_khz = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
+            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
+            rate_khz > 0) {
+            b_async_grid = 2 * cus;
+            const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
+            b_async_budget = std::max(0ll, us) * (long long)rate_khz / 1000;
+        }
+    }
     const long long tail_l = getenv("GC_B_TAIL_L") ? atoll(getenv("GC_B_TAIL_L")) : 2048;
     const long long tail_h = getenv("GC_B_TAIL_H") ? atoll(getenv("GC_B_TAIL_H")) : 4;
     const long long tail_e = getenv("GC_B_TAIL_E") ? atoll(getenv("GC_B_TAIL_E")) : 4096;
@@ -640,7 +944,15 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if (!r2 && tail_on) passes += h.b_tail_passes;
             return r2;
         };
-        enqueue_passes(tail_on ? std::max(1ll, std::min(prev_full, 24ll)) : std::max(2ll, std::min(prev_passes, 24ll)));
+        if (b_async_grid > 0) {  // the first passes on the full grid, then the rest as one asynchronous launch
+            enqueue_passes(b_async_k);
+            GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
+            hipLaunchKernelGGL(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3),
+                               b_async_budget);
+            ++passes;
+        } else {
+            enqueue_passes(tail_on ? std::max(1ll, std::min(prev_full, 24ll)) : std::max(2ll, std::min(prev_passes, 24ll)));
+        }
         if ((rc = synced())) return rc;
         if (r > 0) {
             recs.push_back(RoundRec{prevU, prevU, prev_maxmex, (long long)h.dcnt, 0, prev_passes});
@@ -652,6 +964,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             break;
         }
         if (h.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
+        if (h.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
         const long long maxmex = h.maxmex;
         if (h.kbound >= 0 && h.failcnt > 0) {  // state at the round start is returned
             recs.push_back(RoundRec{U, U, maxmex, 0, 0, 0});
