@@ -73,6 +73,12 @@ case ${1:-} in
                  env:AB_VARIANT=B
                  ab:rmat24:3:base,tail256=GC_B_TAIL:1+GC_B_TAIL_L:256+GC_B_TAIL_H:0+GC_B_TAIL_E:512,tail64=GC_B_TAIL:1+GC_B_TAIL_L:64+GC_B_TAIL_H:0+GC_B_TAIL_E:128
                  env:AB_VARIANT= brounds:rmat24) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j" >&2; exit 2 ;;
+  # k: variant B's asynchronous fold over the compacted entries: parity, A/Bs, per-round cost
+  k) exec_steps=(file:tests/test_gpu_variant_b.py
+                 env:AB_VARIANT=B
+                 ab:rmat24:3:base,async=GC_B_ASYNC:1,async0=GC_B_ASYNC:1+GC_B_ASYNC_K:0,async2=GC_B_ASYNC:1+GC_B_ASYNC_K:2
+                 ab:uniform10M:4:base,async=GC_B_ASYNC:1
+                 env:AB_VARIANT= env:GC_B_ASYNC=1 brounds:rmat24) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
