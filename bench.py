@@ -372,7 +372,7 @@ def north_star(torch, barrier, args):
            # is otherwise above the peak
            "algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
            "algorithmic_frac_capped": capped_alg(probe.kernels, S.n, S.nnz) / t / 1e9 / HBM_PEAK_GBS,
-           "classes_probe_step": class_table(probe.kernels, {}),
+           "classes_probe_step": class_table(probe.kernels, pmc_class_bytes("rmat26", "A")[0]),
            "pmc_frac": pmc_step_frac("rmat26", "A", t)}
     S.close()
     return out
@@ -393,6 +393,8 @@ def class_table(kern, pmc):
                 e["alg_over_peak"] = True  # credited bytes the path does not move (hub bitmaps)
         if k in pmc:
             e["pmc_GB"] = round(pmc[k] * v["launches"] / 1e9, 4)
+            if v["bytes"] > 0:  # physical / algorithmic: > 1 is traffic the §8d model does not need
+                e["pmc_over_alg"] = round(pmc[k] * v["launches"] / v["bytes"], 3)
             if v["ms"] > 0:
                 e["pmc_GBps"] = round(pmc[k] * v["launches"] / v["ms"] / 1e6, 1)
                 e["pmc_frac"] = round(e["pmc_GBps"] / HBM_PEAK_GBS, 4)
