@@ -818,13 +818,18 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const int grid_ev = getenv("GC_GRID_BE") && atoi(getenv("GC_GRID_BE")) > 0 ? atoi(getenv("GC_GRID_BE")) : GC_ROUND_GRID;
     const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
                          : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
-    // GC_B_ASYNC=1: after GC_B_ASYNC_K (default 1) full-grid passes, the rest of the round's
-    // fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2 workgroups);
-    // budget per launch GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item
+    // The round's fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2
+    // workgroups) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
+    // GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item.  On by default for graphs with
+    // hubs (round 4: R-MAT-24 658 -> 455 ms with K = 0, 497 with K = 1, 473 with K = 2;
+    // uniform 10M/16, no hub, 20.0 -> 21.4 ms: off there, as variant A's asynchronous JP;
+    // profiles/r04/k).  GC_B_ASYNC=0 off, =1 on for every graph.
     int b_async_grid = 0;
     long long b_async_budget = 0;
-    const long long b_async_k = getenv("GC_B_ASYNC_K") ? std::max(0ll, atoll(getenv("GC_B_ASYNC_K"))) : 1;
-    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0 && g->n < (1ll << GC_BI_SHIFT)) {  // items: 29-bit vertices
+    const long long b_async_k = getenv("GC_B_ASYNC_K") ? std::max(0ll, atoll(getenv("GC_B_ASYNC_K"))) : 0;
+    const int b_async_env = getenv("GC_B_ASYNC") ? atoi(getenv("GC_B_ASYNC")) : -1;
+    const bool b_async_on = b_async_env > 0 || (b_async_env < 0 && d.hbits_w > 0);
+    if (b_async_on && g->n < (1ll << GC_BI_SHIFT)) {  // items: 29-bit vertices
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&

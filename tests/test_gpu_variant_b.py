@@ -147,18 +147,20 @@ def test_variant_b_hub_bitmaps(monkeypatch, hub_t, hub_w):
 
 
 FOLD_SETTINGS = [
-    {},                                                                   # full-grid passes
-    {"GC_B_ASYNC": "1"},                                                  # one full pass, then k_b_async
-    {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "0"},                             # k_b_async from the first scans on
+    {"GC_B_ASYNC": "0"},                                                  # full-grid passes only
+    {},                                                                   # k_b_async where there are hubs
+    {"GC_B_ASYNC": "1"},                                                  # k_b_async on every graph
+    {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "1"},                             # one full pass first
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "3"},
     {"GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"},                       # gives up at once: hands back to passes
 ]
 
 
-@pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "async", "async_k0", "async_k3", "async_abort"])
+@pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort"])
 def test_variant_b_fold(monkeypatch, env):
-    """The fold's passes on the full grid and the asynchronous fold (GC_B_ASYNC=1) after 0, 1 or
-    3 full passes, and forced to hand back at once -- every run equal to the oracle."""
+    """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
+    default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
+    every run equal to the oracle."""
     for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
