@@ -159,7 +159,6 @@ struct DevCtl {
     int pad1;
     long long hub_start;    // hubs on: the sweep of this round that started the hubs' JP (the lights had converged)
     long long nx_maxmex;    // fused commit: next round's max candidate (k_close moves both into place)
-    long long b_tail_passes;  // variant B: fold passes the last k_b_tail ran
     ull bcnt[9];            // variant B work lists: kind (0 light admission, 1 heavy admission, 2 eviction) x 3 rotating slots
     ull xhub_cnt;           // shards with replicated hubs: frontier hubs this rank does not own (not counted in F)
     int lights_hold;        // shards: the hub JP waits for every rank's lights (cleared by gc_shard_release_hubs)

@@ -108,14 +108,8 @@ struct BLists {
 #define GC_B_EVCOL 0x7FFFFFFF
 #define GC_B_PMARK 0x80000000u  // marks an entry read from pend[] (its degree was checked)
 __device__ __forceinline__ ull* b_cnt(DevCtl* c, int kind, int slot) { return &c->bcnt[kind * 3 + slot]; }
-// a list count at the start of a pass: a plain load in a full-grid launch (written by an
-// earlier launch), an agent-scope load in k_b_tail (written by its own atomics, maybe since
-// this CU's L1 last held the line)
-template <bool TAIL>
-__device__ __forceinline__ long long b_count(DevCtl* c, int kind, int slot) {
-    ull* p = b_cnt(c, kind, slot);
-    return TAIL ? (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (long long)*p;
-}
+// a list count at the start of a pass (written by an earlier launch)
+__device__ __forceinline__ long long b_count(DevCtl* c, int kind, int slot) { return (long long)*b_cnt(c, kind, slot); }
 
 // gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]; load(o, u)
 template <typename Load, typename Apply>
@@ -175,16 +169,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B,
 
 // eviction pass over list slot i % 3: ev(u) = the smallest not-refused potential evictor
 // (v' > u listed by u, same candidate, deg(v') > deg(u)); final once that evictor is
-// admitted or there is none (INF), else u stays listed.  Workgroup bid of nblk (k_b_ev: the
-// grid; k_b_tail: its one workgroup).
-template <bool TAIL>
+// admitted or there is none (INF), else u stays listed.  Workgroup bid of nblk.
 __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nblk) {
     DevCtl* c = g.ctl;
     const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
-    if (bid == 0 && threadIdx.x < 3) {
-        if (TAIL) gc_st(b_cnt(c, threadIdx.x, zs), 0ull);
-        else *b_cnt(c, threadIdx.x, zs) = 0ull;
-    }
+    if (bid == 0 && threadIdx.x < 3) *b_cnt(c, threadIdx.x, zs) = 0ull;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ const int* s_src[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int* s_dst[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -197,7 +186,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int* __restrict__ list = B.l[2][rs];
-    const long long cnt = b_count<TAIL>(c, 2, rs);
+    const long long cnt = b_count(c, 2, rs);
     const unsigned char* __restrict__ k8 = g.k8;
     GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
     const int vpw = gc_vpw(cnt, (long long)nblk * GC_WAVES_PER_BLOCK);
@@ -271,7 +260,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, BLists B, int* ev, int pass) {
-    b_ev_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
+    b_ev_pass(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
 // admission flag of one entry u for v (vo): 1 = u admitted and still present at v's
@@ -309,11 +298,10 @@ __device__ __forceinline__ void b_adm_decide(GDev& g, BLists& B, DevCtl* c, int 
 
 // admission of the heavy list, slot i % 3: a workgroup per vertex (k_b_adm's workgroups,
 // before their light chunks)
-template <bool TAIL>
 __device__ void b_adm_heavy(GDev& g, BLists& B, const int* ev, int pass, int bid, int nblk) {
     DevCtl* c = g.ctl;
     const int rs = pass % 3, ws = (pass + 1) % 3;
-    const long long cnt = b_count<TAIL>(c, 1, rs);
+    const long long cnt = b_count(c, 1, rs);
     if (cnt == 0) return;
     __shared__ unsigned s_flag;
     __shared__ int s_first;
@@ -364,9 +352,8 @@ __device__ void b_adm_heavy(GDev& g, BLists& B, const int* ev, int pass, int bid
 
 // admission pass, slot i % 3: the heavy list (a workgroup per vertex), then the light list
 // (wave chunks)
-template <bool TAIL>
 __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid, int nblk) {
-    b_adm_heavy<TAIL>(g, B, ev, pass, bid, nblk);
+    b_adm_heavy(g, B, ev, pass, bid, nblk);
     DevCtl* c = g.ctl;
     const int rs = pass % 3, ws = (pass + 1) % 3;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
@@ -381,7 +368,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int* __restrict__ list = B.l[0][rs];
-    const long long cnt = b_count<TAIL>(c, 0, rs);
+    const long long cnt = b_count(c, 0, rs);
     const unsigned char* __restrict__ k8 = g.k8;
     GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err}, est{s_estage[w], 0, g.n, &g.ctl->loop_err};
     const int vpw = gc_vpw(cnt, (long long)nblk * GC_WAVES_PER_BLOCK);
@@ -442,40 +429,16 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int* ev, int pass) {
-    b_adm_pass<false>(g, B, ev, pass, blockIdx.x, gridDim.x);
+    b_adm_pass(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
 // (Round 4 measured a pass's eviction and admission halves in ONE launch, no grid barrier
 // between them: R-MAT-24 656 -> 1000 ms, uniform 10M 20.7 -> 24.7 ms, profiles/r04/i; removed.)
 
-// The rest of a round's fold in ONE workgroup (round 4, GC_B_TAIL): after the host's
-// full-grid passes, the fold's deep end is a chain of passes over a few hundred vertices
-// each -- two 2048-workgroup launches apiece.  Here they run back to back, a workgroup
-// barrier apart, while the lists stay within the caps (light admissions, heavy admissions,
-// evictions); a bigger list is left to full-grid passes (the host sees the counts).  The
-// passes run is stored in DevCtl.b_tail_passes (the host's pass count keeps the list slots).
-// Counters are read with agent-scope loads and cleared with agent-scope stores; list
-// entries, states, cursors and eviction times written before a barrier are visible to the
-// whole workgroup after it (one CU, one L1).
-__global__ void __launch_bounds__(GC_BLOCK) k_b_tail(GDev g, BLists B, int* ev, int pass0, long long capl,
-                                                     long long caph, long long cape, int maxp) {
-    DevCtl* c = g.ctl;
-    __shared__ long long s_n[3];
-    int k = 0;
-    for (; k < maxp; ++k) {
-        const int rs = (pass0 + k) % 3;
-        if (threadIdx.x < 3) s_n[threadIdx.x] = b_count<true>(c, threadIdx.x, rs);
-        __syncthreads();
-        const long long nl = s_n[0], nh = s_n[1], ne = s_n[2];
-        __syncthreads();  // every thread has read s_n
-        if (nl + nh + ne == 0 || nl > capl || nh > caph || ne > cape) break;
-        b_ev_pass<true>(g, B, ev, pass0 + k, 0, 1);
-        __syncthreads();
-        b_adm_pass<true>(g, B, ev, pass0 + k, 0, 1);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) gc_st(&c->b_tail_passes, (long long)k);
-}
+// (Round 4 also ran the fold's deep end in ONE workgroup, passes a workgroup barrier apart,
+// while the lists stayed small (k_b_tail): R-MAT-24 slower at every cap tried -- 2048 light /
+// 4 heavy / 4096 evictions 656 -> 723 ms, 256/0/512 658 -> 677, 64/0/128 658 -> 661,
+// profiles/r04/h, r04/j; removed.)
 
 
 // winners: admitted and never evicted, coloured (coloring_optimized.py:129-140); with hub
@@ -855,17 +818,18 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const int grid_ev = getenv("GC_GRID_BE") && atoi(getenv("GC_GRID_BE")) > 0 ? atoi(getenv("GC_GRID_BE")) : GC_ROUND_GRID;
     const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
                          : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
-    // GC_B_TAIL=1: the fold's deep end runs in k_b_tail's one workgroup while the lists are
-    // within GC_B_TAIL_L light admissions, GC_B_TAIL_H heavy admissions and GC_B_TAIL_E
-    // evictions (round 4: off by default, R-MAT-24 656.5 -> 722.9 ms with it, profiles/r04/h)
-    const bool tail_on = getenv("GC_B_TAIL") && atoi(getenv("GC_B_TAIL")) > 0;
-    // GC_B_ASYNC=1: after GC_B_ASYNC_K (default 1) full-grid passes, the rest of the round's
-    // fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2 workgroups);
-    // budget per launch GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item
+    // The round's fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2
+    // workgroups) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
+    // GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item.  On by default for graphs with
+    // hubs (round 4: R-MAT-24 658 -> 455 ms with K = 0, 497 with K = 1, 473 with K = 2;
+    // uniform 10M/16, no hub, 20.0 -> 21.4 ms: off there, as variant A's asynchronous JP;
+    // profiles/r04/k).  GC_B_ASYNC=0 off, =1 on for every graph.
     int b_async_grid = 0;
     long long b_async_budget = 0;
-    const long long b_async_k = getenv("GC_B_ASYNC_K") ? std::max(0ll, atoll(getenv("GC_B_ASYNC_K"))) : 1;
-    if (getenv("GC_B_ASYNC") && atoi(getenv("GC_B_ASYNC")) > 0 && g->n < (1ll << GC_BI_SHIFT)) {  // items: 29-bit vertices
+    const long long b_async_k = getenv("GC_B_ASYNC_K") ? std::max(0ll, atoll(getenv("GC_B_ASYNC_K"))) : 0;
+    const int b_async_env = getenv("GC_B_ASYNC") ? atoi(getenv("GC_B_ASYNC")) : -1;
+    const bool b_async_on = b_async_env > 0 || (b_async_env < 0 && d.hbits_w > 0);
+    if (b_async_on && g->n < (1ll << GC_BI_SHIFT)) {  // items: 29-bit vertices
         int cus = 0, rate_khz = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
@@ -875,9 +839,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             b_async_budget = std::max(0ll, us) * (long long)rate_khz / 1000;
         }
     }
-    const long long tail_l = getenv("GC_B_TAIL_L") ? atoll(getenv("GC_B_TAIL_L")) : 2048;
-    const long long tail_h = getenv("GC_B_TAIL_H") ? atoll(getenv("GC_B_TAIL_H")) : 4;
-    const long long tail_e = getenv("GC_B_TAIL_E") ? atoll(getenv("GC_B_TAIL_E")) : 4096;
     DevCtl& h = *g->hctl;
     memset(&h, 0, sizeof(DevCtl));
     h.kbound = opt->num_colors;
@@ -913,7 +874,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // round needed); the previous round's winner count comes back in the same snapshot
     // (k_b_reset keeps it).  A round that ends the colouring (no uncoloured vertex) or
     // fails (bounded attempt) has only run fold passes, which change no colour.
-    long long prev_passes = 2, prev_full = 1, prevU = 0, prev_maxmex = -1;
+    long long prev_passes = 2, prevU = 0, prev_maxmex = -1;
     for (long long r = 0;; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
         hipLaunchKernelGGL(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
@@ -928,22 +889,15 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         // the fold's passes over the work lists until no vertex is undecided and every
         // admitted vertex's eviction time is final
         hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
-        long long passes = 0, full = 0;
+        long long passes = 0;
         auto enqueue_passes = [&](long long k) {
-            for (long long j = 0; j < k; ++j, ++passes, ++full) {
+            for (long long j = 0; j < k; ++j, ++passes) {
                 const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
                 hipLaunchKernelGGL(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
                 hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
-            if (tail_on)  // the rest in one workgroup while the lists are small (its passes counted after the sync)
-                hipLaunchKernelGGL(k_b_tail, dim3(1), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3), tail_l, tail_h,
-                                   tail_e, 1 << 30);
         };
-        auto synced = [&]() {
-            int r2 = R.sync();
-            if (!r2 && tail_on) passes += h.b_tail_passes;
-            return r2;
-        };
+        auto synced = [&]() { return R.sync(); };
         if (b_async_grid > 0) {  // the first passes on the full grid, then the rest as one asynchronous launch
             enqueue_passes(b_async_k);
             GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
@@ -951,7 +905,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
                                b_async_budget);
             ++passes;
         } else {
-            enqueue_passes(tail_on ? std::max(1ll, std::min(prev_full, 24ll)) : std::max(2ll, std::min(prev_passes, 24ll)));
+            enqueue_passes(std::max(2ll, std::min(prev_passes, 24ll)));
         }
         if ((rc = synced())) return rc;
         if (r > 0) {
@@ -983,7 +937,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
         if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         prev_passes = passes;
-        prev_full = full;
         prevU = U;
         prev_maxmex = maxmex;
     }

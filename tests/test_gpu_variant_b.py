@@ -146,27 +146,22 @@ def test_variant_b_hub_bitmaps(monkeypatch, hub_t, hub_w):
         assert_same_run(dg.color("B", num_colors=int(o["max_color"])), oracle.c_color(rp, col, "B", k=int(o["max_color"])))
 
 
-TAIL_SETTINGS = [
-    {},                                                                   # full-grid passes
-    {"GC_B_TAIL": "1"},                                                   # the one-workgroup tail, default caps
-    {"GC_B_TAIL": "1", "GC_B_TAIL_L": "16", "GC_B_TAIL_H": "0", "GC_B_TAIL_E": "16"},  # hands back, takes over often
-    {"GC_B_TAIL": "1", "GC_B_TAIL_L": "1000000", "GC_B_TAIL_H": "64", "GC_B_TAIL_E": "1000000"},  # whole folds
-    {"GC_B_ASYNC": "1"},                                                  # one full pass, then k_b_async
-    {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "0"},                             # k_b_async from the first scans on
+FOLD_SETTINGS = [
+    {"GC_B_ASYNC": "0"},                                                  # full-grid passes only
+    {},                                                                   # k_b_async where there are hubs
+    {"GC_B_ASYNC": "1"},                                                  # k_b_async on every graph
+    {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "1"},                             # one full pass first
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "3"},
     {"GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"},                       # gives up at once: hands back to passes
 ]
 
 
-@pytest.mark.parametrize("env", TAIL_SETTINGS, ids=["grid", "tail", "tail_small", "tail_all", "async", "async_k0",
-                                                    "async_k3", "async_abort"])
-def test_variant_b_fold_tail(monkeypatch, env):
-    """The fold's passes on the full grid (the default), the deep end in k_b_tail's one
-    workgroup (GC_B_TAIL=1) with the default caps, tiny caps (passes alternate between the grid
-    and the workgroup) and caps that take whole folds after one full pass, heavy admissions
-    included, and the asynchronous fold (GC_B_ASYNC=1) after 0, 1 or 3 full passes and forced
-    to hand back at once -- every run equal to the oracle."""
-    for k in ("GC_B_TAIL", "GC_B_TAIL_L", "GC_B_TAIL_H", "GC_B_TAIL_E", "GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US"):
+@pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort"])
+def test_variant_b_fold(monkeypatch, env):
+    """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
+    default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
+    every run equal to the oracle."""
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
