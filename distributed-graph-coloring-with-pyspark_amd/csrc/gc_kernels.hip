@@ -3057,14 +3057,78 @@ void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t 
         hipLaunchKernelGGL(k_shard_hub_flags, dim3((int)std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, lo, hi);
 }
 void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
-// the winners gc_hub_push_wave left in `big`: a workgroup each walks its hub list
+// the winners gc_hub_push_wave left in `big`: their hub lists as one flat range over the
+// whole grid, GC_BLOCK winners at a time (every workgroup scans the tile's list lengths and
+// takes its stride of the tile's entries), 4 entries per thread in flight.  (Round 3 gave
+// each winner a workgroup: a hub's list of 10^4-10^5 hubs was then one workgroup's chain of
+// dependent load-load-atomic steps, ~100 us a round in variant B, profiles/r04/f.)
+#ifndef GC_PUSH_BIG_WG
+#define GC_PUSH_BIG_WG 0  // build knob for the A/B: 1 = round 3's workgroup per winner
+#endif
+#if GC_PUSH_BIG_WG
 __global__ void __launch_bounds__(GC_BLOCK) k_hub_push_big(GDev g, const int* big, const ull* cnt) {
     const long long nb = (long long)*cnt;
     for (long long i = blockIdx.x; i < nb; i += gridDim.x) {
         const int v = big[i];
-        gc_hub_mark_row(g, v, gc_colour(g, v), threadIdx.x, blockDim.x);  // committed: its colour is in c8
+        gc_hub_mark_row(g, v, gc_colour(g, v), threadIdx.x, blockDim.x);
     }
 }
+#else
+__global__ void __launch_bounds__(GC_BLOCK) k_hub_push_big(GDev g, const int* big, const ull* cnt) {
+    const long long nb = (long long)*cnt;
+    if (nb == 0) return;
+    __shared__ long long s_off[GC_BLOCK + 1];
+    __shared__ long long s_hs[GC_BLOCK];
+    __shared__ int s_cc[GC_BLOCK];
+    __shared__ long long s_wsum[GC_WAVES_PER_BLOCK];
+    const int t = threadIdx.x, lane = gc_lane(), w = t / GC_WAVE;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long j0 = 0; j0 < nb; j0 += GC_BLOCK) {
+        const int tn = (int)(nb - j0 < GC_BLOCK ? nb - j0 : GC_BLOCK);
+        long long len = 0;
+        if (t < tn) {
+            const int v = big[j0 + t];
+            s_hs[t] = g.hin_rp[v];
+            len = g.hin_rp[v + 1] - s_hs[t];
+            s_cc[t] = gc_colour(g, v);  // committed: its colour is in c8
+        }
+        long long x = len;  // workgroup inclusive scan of len
+#pragma unroll
+        for (int o = 1; o < GC_WAVE; o <<= 1) {
+            const long long y = __shfl_up(x, o, GC_WAVE);
+            if (lane >= o) x += y;
+        }
+        if (lane == GC_WAVE - 1) s_wsum[w] = x;
+        __syncthreads();
+        for (int k = 0; k < w; ++k) x += s_wsum[k];
+        s_off[t + 1] = x;
+        if (t == 0) s_off[0] = 0;
+        __syncthreads();
+        const long long total = s_off[tn];
+        for (long long f0 = (long long)blockIdx.x * blockDim.x * 4; f0 < total; f0 += stride * 4) {
+            int hx[4], hc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long f = f0 + (long long)q * blockDim.x + t;
+                hx[q] = -1;
+                hc[q] = 0;
+                if (f < total) {
+                    int k = 0;  // max k < tn with s_off[k] <= f
+#pragma unroll
+                    for (int step = GC_BLOCK / 2; step > 0; step >>= 1)
+                        if (k + step < tn && s_off[k + step] <= f) k += step;
+                    hx[q] = g.hin_col[s_hs[k] + (f - s_off[k])];
+                    hc[q] = s_cc[k];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (hx[q] >= 0) gc_hub_mark(g, hx[q], hc[q]);
+        }
+        __syncthreads();
+    }
+}
+#endif
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s) {
     hipLaunchKernelGGL(k_hub_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, big, cnt);
 }
