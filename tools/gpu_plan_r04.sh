@@ -79,12 +79,14 @@ case ${1:-} in
                  ab:rmat24:3:base,async=GC_B_ASYNC:1,async0=GC_B_ASYNC:1+GC_B_ASYNC_K:0,async2=GC_B_ASYNC:1+GC_B_ASYNC_K:2
                  ab:uniform10M:4:base,async=GC_B_ASYNC:1
                  env:AB_VARIANT= env:GC_B_ASYNC=1 brounds:rmat24) ;;
-  # l: variant B's asynchronous fold on by default (hub graphs, K = 0), the fold tail removed:
-  #    every GPU test, the A/Bs of the new defaults, variant B per round
+  # l: variant B's asynchronous fold on by default (hub graphs, K = 0), the fold tail removed,
+  #    long hub-list pushes flattened over the grid: every GPU test, the A/Bs of the new
+  #    defaults (the push against round 3's workgroup per winner), variant B per round
   l) exec_steps=(file:tests/test_gpu_variant_b.py tests smoke
                  env:AB_VARIANT=B
                  ab:rmat24:3:base,off=GC_B_ASYNC:0,k1=GC_B_ASYNC_K:1
                  ab:uniform10M:4:base,on=GC_B_ASYNC:1
+                 abl:rmat24:3:2:base=-,pushwg=build_variants/pushwg/libgcolor.so
                  env:AB_VARIANT= brounds:rmat24) ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
 esac
