@@ -86,7 +86,7 @@ case ${1:-} in
                  env:AB_VARIANT=B
                  ab:rmat24:3:base,off=GC_B_ASYNC:0,k1=GC_B_ASYNC_K:1
                  ab:uniform10M:4:base,on=GC_B_ASYNC:1
-                 abl:rmat24:3:2:base=-,pushwg=build_variants/pushwg/libgcolor.so
+                 abl:rmat24:3:2:base=-,pushwg=variants/pushwg/libgcolor.so
                  env:AB_VARIANT= brounds:rmat24) ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
 esac
