@@ -771,6 +771,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
     }
 }
 
+}  // namespace
+int gcl_b_async_blocks_per_cu() {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_b_async, GC_BLOCK, 0) != hipSuccess) return 0;
+    return b;
+}
+namespace {
+
 struct RunB {
     gc_graph* g;
     GDev d;
@@ -819,7 +827,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
                          : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
     // The round's fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2
-    // workgroups) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
+    // workgroups, GC_B_ASYNC_BPC) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
     // GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item.  On by default for graphs with
     // hubs (round 4: R-MAT-24 658 -> 455 ms with K = 0, 497 with K = 1, 473 with K = 2;
     // uniform 10M/16, no hub, 20.0 -> 21.4 ms: off there, as variant A's asynchronous JP;
@@ -834,7 +842,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
             rate_khz > 0) {
-            b_async_grid = 2 * cus;
+            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 2;
+            b_async_grid = std::min(bpc, std::max(1, gcl_b_async_blocks_per_cu())) * cus;  // resident: every wave's slice progresses
             const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
             b_async_budget = std::max(0ll, us) * (long long)rate_khz / 1000;
         }
