@@ -80,14 +80,18 @@ case ${1:-} in
                  ab:uniform10M:4:base,async=GC_B_ASYNC:1
                  env:AB_VARIANT= env:GC_B_ASYNC=1 brounds:rmat24) ;;
   # l: variant B's asynchronous fold on by default (hub graphs, K = 0), the fold tail removed,
-  #    long hub-list pushes flattened over the grid: every GPU test, the A/Bs of the new
-  #    defaults (the push against round 3's workgroup per winner), variant B per round
-  l) exec_steps=(file:tests/test_gpu_variant_b.py tests smoke
+  #    long hub-list pushes flattened over the grid, the hlow-sort and async-grid knobs: every
+  #    GPU test (the hub and variant B files first), smoke, then the A/Bs of the new defaults and
+  #    knobs (variant B: async off / 1 / 4 workgroups per CU, the push against round 3's
+  #    workgroup per winner; variant A: hlow rows unsorted) and variant B per round
+  l) exec_steps=(file:tests/test_gpu_hubs.py file:tests/test_gpu_variant_b.py tests smoke
                  env:AB_VARIANT=B
-                 ab:rmat24:3:base,off=GC_B_ASYNC:0,k1=GC_B_ASYNC_K:1
-                 ab:uniform10M:4:base,on=GC_B_ASYNC:1
+                 ab:rmat24:3:base,off=GC_B_ASYNC:0,bpc1=GC_B_ASYNC_BPC:1,bpc4=GC_B_ASYNC_BPC:4
                  abl:rmat24:3:2:base=-,pushwg=variants/pushwg/libgcolor.so
-                 env:AB_VARIANT= brounds:rmat24) ;;
+                 ab:uniform10M:4:base,on=GC_B_ASYNC:1
+                 env:AB_VARIANT=
+                 ab:rmat24:5:base,nosort=GC_HLOW_SORT:0 ab:rmat26:3:base,nosort=GC_HLOW_SORT:0
+                 brounds:rmat24) ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
