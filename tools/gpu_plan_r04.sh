@@ -91,7 +91,7 @@ case ${1:-} in
                  ab:uniform10M:4:base,on=GC_B_ASYNC:1
                  env:AB_VARIANT=
                  ab:rmat24:5:base,nosort=GC_HLOW_SORT:0 ab:rmat26:3:base,nosort=GC_HLOW_SORT:0
-                 brounds:rmat24) ;;
+                 brounds:rmat24 profile:rmat24 "profile:rmat24:--variant,B") ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
