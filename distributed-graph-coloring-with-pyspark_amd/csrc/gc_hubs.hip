@@ -329,11 +329,11 @@ int build(gc_graph* g, int T, int W) {
                            H, g->hlow_rp, g->hlow_col);
     }
     pc.mark("hin fill", s);
-    // GC_HLOW_SORT=0 (A/B knob, round 4): the hlow rows stay in row order.  The scan's result
-    // does not depend on the order (a flag-0 entry stays 0 for the round, a coloured one for
-    // good); rank order only makes its coloured prefix (hlen) long
-    const bool hsort = !(getenv("GC_HLOW_SORT") && atoi(getenv("GC_HLOW_SORT")) == 0);
-    if (EL > 0 && hsort) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
+    // (Round 4 measured the rows left in row order: the scan's result does not depend on the
+    // order, but rank order is what makes its coloured prefix (hlen) grow -- lower-rank hubs
+    // colour first -- and the resumable scans skip it: unsorted, R-MAT-24 153.9 ms -> 6.0 s,
+    // R-MAT-26 0.43 -> 25.9 s, profiles/r04/l.  The sort stays.)
+    if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
         // the keys are hub indices < H: only their low bit_width(H - 1) bits are sorted
         // (R-MAT-26: 20 of 32 bits, three 8-bit digit passes instead of four)
         const unsigned kbits = (unsigned)std::max(1, 64 - __builtin_clzll((unsigned long long)std::max(H - 1, 1ll)));

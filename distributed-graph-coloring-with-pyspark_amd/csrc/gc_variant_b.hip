@@ -826,8 +826,9 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     const int grid_ev = getenv("GC_GRID_BE") && atoi(getenv("GC_GRID_BE")) > 0 ? atoi(getenv("GC_GRID_BE")) : GC_ROUND_GRID;
     const int grid_adm = getenv("GC_GRID_BA") && atoi(getenv("GC_GRID_BA")) > 0 ? atoi(getenv("GC_GRID_BA"))
                          : (g->maxdeg > GC_B_HEAVY ? 2 * GC_ROUND_GRID : GC_ROUND_GRID);
-    // The round's fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 2
-    // workgroups, GC_B_ASYNC_BPC) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
+    // The round's fold as one asynchronous launch (k_b_async) on a resident grid (CUs x 4
+    // workgroups, GC_B_ASYNC_BPC, capped by the occupancy: R-MAT-24 420 ms at 2, 363 at 4, 557 at
+    // 1, profiles/r04/l) after GC_B_ASYNC_K (default 0) full-grid passes; budget per launch
     // GC_ASYNC_BUDGET_US (20 ms) plus 2 cycles per work item.  On by default for graphs with
     // hubs (round 4: R-MAT-24 658 -> 455 ms with K = 0, 497 with K = 1, 473 with K = 2;
     // uniform 10M/16, no hub, 20.0 -> 21.4 ms: off there, as variant A's asynchronous JP;
@@ -842,7 +843,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
             rate_khz > 0) {
-            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 2;
+            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 4;
             b_async_grid = std::min(bpc, std::max(1, gcl_b_async_blocks_per_cu())) * cus;  // resident: every wave's slice progresses
             const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
             b_async_budget = std::max(0ll, us) * (long long)rate_khz / 1000;

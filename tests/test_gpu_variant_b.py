@@ -153,15 +153,17 @@ FOLD_SETTINGS = [
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "1"},                             # one full pass first
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "3"},
     {"GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"},                       # gives up at once: hands back to passes
+    {"GC_B_ASYNC": "1", "GC_B_ASYNC_BPC": "1"},                           # one workgroup per CU
 ]
 
 
-@pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort"])
+@pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort",
+                                                    "async_bpc1"])
 def test_variant_b_fold(monkeypatch, env):
     """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
     default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
     every run equal to the oracle."""
-    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US"):
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)

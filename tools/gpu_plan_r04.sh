@@ -92,6 +92,13 @@ case ${1:-} in
                  env:AB_VARIANT=
                  ab:rmat24:5:base,nosort=GC_HLOW_SORT:0 ab:rmat26:3:base,nosort=GC_HLOW_SORT:0
                  brounds:rmat24 profile:rmat24 "profile:rmat24:--variant,B") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
+  # m: the round's final build (variant B's asynchronous fold at 4 workgroups per CU): the hub and
+  #    variant B tests, smoke, the profiles of THIS build (A and B on R-MAT-24, A on R-MAT-26:
+  #    profiles/pmc), the default bench line, then the async grid beyond 4 (for the record)
+  m) exec_steps=(file:tests/test_gpu_hubs.py file:tests/test_gpu_variant_b.py smoke
+                 profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26
+                 "bench:rmat24"
+                 env:AB_VARIANT=B ab:rmat24:3:base,bpc6=GC_B_ASYNC_BPC:6,bpc8=GC_B_ASYNC_BPC:8 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"

@@ -14,7 +14,8 @@ set -euo pipefail
 TAG=$1; WL=$2
 shift 2
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/$TAG/$WL
+SUF=$(echo "$*" | tr -c 'A-Za-z0-9\n' '_' | sed 's/^_*//; s/_*$//')
+OUT=$ROOT/gpurun_out/$TAG/$WL${SUF:+_$SUF}  # one directory per workload and argument set
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
