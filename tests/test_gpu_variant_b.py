@@ -244,3 +244,19 @@ def test_cli_variant_b_matches_reference(name, tmp_path):
     assert norm == cli_rec["stdout"]
     if "output_sha256" in cli_rec:
         assert hashlib.sha256(out_c.read_bytes()).hexdigest() == cli_rec["output_sha256"]
+
+
+@pytest.mark.parametrize("env", [{}, {"GC_B_ASYNC": "0"}], ids=["async", "passes"])
+def test_rmat20_variant_b_against_oracle(monkeypatch, env):
+    """R-MAT-20 (10^6 vertices, hubs of 10^4 entries, ~200 rounds): variant B's fold at a size
+    where the asynchronous fold spreads every round over thousands of waves, and the full-grid
+    passes -- every colour and per-round record equal to the C oracle's (variant 1)."""
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_B_ASYNC_BPC"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with _dg().rmat(20, 16, seed=1) as dg:
+        rp, col = dg.export()
+        g = dg.color("B")
+        assert_same_run(g, oracle.c_color(rp, col, "B"))
+        assert dg.validate() == (0, 0)

@@ -99,6 +99,10 @@ case ${1:-} in
                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26
                  "bench:rmat24"
                  env:AB_VARIANT=B ab:rmat24:3:base,bpc6=GC_B_ASYNC_BPC:6,bpc8=GC_B_ASYNC_BPC:8 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m" >&2; exit 2 ;;
+  # n: the final build again (no rebuild): variant B against the oracle at R-MAT-20 (asynchronous
+  #    fold and passes), variant A's per-round cost, variant B's K at 4 workgroups per CU
+  n) exec_steps=(file:tests/test_gpu_variant_b.py:rmat20 rounds:rmat24
+                 env:AB_VARIANT=B ab:rmat24:3:base,k1=GC_B_ASYNC_K:1 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
