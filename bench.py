@@ -71,12 +71,13 @@ WORKLOADS = {
 CLASS_KERNELS = {
     "init": ["k_init", "k_seed_prep"],
     "propose": ["k_propose", "k_propose_block"],
-    "resolve": ["k_resolve"],
+    # variant B's fold (k_b_init, its passes or the asynchronous fold) is its resolution class
+    "resolve": ["k_resolve", "k_b_init", "k_b_ev", "k_b_adm", "k_b_async"],
     "sweep": ["k_sweep", "k_sweep_tail", "k_sweep_async"],
-    "commit": ["k_commit", "k_commit_big", "k_pull"],
+    "commit": ["k_commit", "k_commit_big", "k_pull", "k_b_commit", "k_hub_push_big"],
     "reseed": ["k_unc_compact", "k_cc_hook", "k_cc_best", "k_cc_seeds"],
     "other": ["k_close", "k_pack_c4", "k_fsort_count", "k_fsort_scan", "k_fsort_write", "k_front_count",
-              "k_finalize", "k_stat_reduce"],
+              "k_finalize", "k_stat_reduce", "k_b_reset", "k_b_fail0"],
 }
 
 

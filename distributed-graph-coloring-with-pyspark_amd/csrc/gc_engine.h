@@ -164,3 +164,64 @@ static inline int gc_grid_for_waves(long long items, int cap = 2048) {
     if (blocks > cap) blocks = cap;
     return (int)blocks;
 }
+
+// Per-class HIP-event timing of a colouring's launches (gc_options.kernel_timing): begin(cls)
+// before a launch opens a run of that class (consecutive launches of one class share it),
+// collect() adds the runs' times to gc_stats.k_ms.  Used by the one-GPU engine and variant B.
+#include <stdio.h>
+#include <stdlib.h>
+struct KTimer {
+    gc_graph* g;
+    unsigned mask;  // kernel classes to time (bit GC_K_*)
+    gc_stats* st;
+    int run_cls = -1;  // class of the open run (-1: none)
+    std::vector<std::pair<int, size_t>> recs;  // (class, event index of start)
+    size_t used = 0;
+    hipEvent_t ev() {
+        if (used >= g->evpool.size()) {
+            hipEvent_t e;
+            hipEventCreate(&e);
+            g->evpool.push_back(e);
+        }
+        return g->evpool[used++];
+    }
+    // GC_DEBUG_SYNC: synchronise after every launch and name the kernel class of a fault
+    const bool dbg_sync = getenv("GC_DEBUG_SYNC") != nullptr;
+    int last_cls = -1;
+    long long nlaunch = 0;
+    void begin(int cls) {
+        last_cls = cls;
+        ++nlaunch;
+        if (st) st->k_launches[cls]++;
+        if (cls == run_cls) return;  // the open run goes on
+        close();
+        if (!((mask >> cls) & 1u)) return;
+        run_cls = cls;
+        recs.push_back({cls, used});
+        hipEventRecord(ev(), g->stream);
+    }
+    void end() {
+        if (!dbg_sync) return;
+        const hipError_t e = hipStreamSynchronize(g->stream);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[gc debug-sync] launch %lld (class %d) failed: %s\n", nlaunch, last_cls, hipGetErrorString(e));
+            fflush(stderr);
+            abort();
+        }
+    }
+    void close() {
+        if (run_cls < 0) return;
+        hipEventRecord(ev(), g->stream);
+        run_cls = -1;
+    }
+    void collect() {
+        close();
+        if (!mask || !st) return;
+        for (auto& r : recs) {
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, g->evpool[r.second], g->evpool[r.second + 1]);
+            st->k_ms[r.first] += ms;
+        }
+    }
+};
+

@@ -861,6 +861,10 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     GC_HIP(hipMemsetAsync(g->bstat, 0, sizeof(ull) * GC_STAT_SLOTS * 16, s));
     GC_HIP(hipEventRecord(g->ev0, s));
     // init + seed (coloring_optimized.py:70-80 == coloring.py:12-35)
+    // per-class launch timing (gc_options.kernel_timing), as the one-GPU engine: the fold
+    // (k_b_init and its passes or k_b_async) is the resolution class
+    KTimer kt{g, (unsigned)opt->kernel_timing, st};
+    kt.begin(GC_K_INIT);
     gcl_init(d, g->seeds[0], gc_grid_for_waves(g->n), s);
     gcl_seed_prep(d, g->seeds[0], g->seeds[1], s);
     gcl_commit(d, L, GC_CM_INIT, 0, s);
@@ -887,9 +891,11 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     long long prev_passes = 2, prevU = 0, prev_maxmex = -1;
     for (long long r = 0;; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
+        kt.begin(GC_K_OTHER);
         hipLaunchKernelGGL(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
         gcl_fsort(d, L, g->fsum, s);
         gcl_pack_c4(d, s);
+        kt.begin(GC_K_PROPOSE);
         gcl_propose(d, L, s);
         gcl_propose_block(d, L, s);
         if (h.kbound == 0) {
@@ -898,6 +904,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         }
         // the fold's passes over the work lists until no vertex is undecided and every
         // admitted vertex's eviction time is final
+        kt.begin(GC_K_RESOLVE);
         hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
         long long passes = 0;
         auto enqueue_passes = [&](long long k) {
@@ -941,22 +948,27 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             const int ws = (int)(passes % 3);  // written by the last pass
             if (h.bcnt[ws] + h.bcnt[3 + ws] + h.bcnt[6 + ws] == 0) break;
             if (passes > 2 * g->n + 64) { gc_set_error("variant B passes do not converge"); return GC_EROUNDS; }
+            kt.begin(GC_K_RESOLVE);
             enqueue_passes(batch);
             if ((rc = synced())) return rc;
         }
+        kt.begin(GC_K_COMMIT);
         hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
         if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         prev_passes = passes;
         prevU = U;
         prev_maxmex = maxmex;
     }
+    kt.begin(GC_K_OTHER);
     gcl_finalize(d, gc_grid_for_waves(g->n, 8192), s);
     gcl_stat_reduce(d, s);
+    kt.close();
     GC_HIP(hipEventRecord(g->ev1, s));
     if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
     if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
     if ((rc = R.sync())) return rc;
     if (st) {
+        kt.collect();
         float ms = 0.f;
         GC_HIP(hipEventElapsedTime(&ms, g->ev0, g->ev1));
         st->device_ms = ms;
