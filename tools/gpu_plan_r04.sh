@@ -103,6 +103,10 @@ case ${1:-} in
   #    fold and passes), variant A's per-round cost, variant B's K at 4 workgroups per CU
   n) exec_steps=(file:tests/test_gpu_variant_b.py:rmat20 rounds:rmat24
                  env:AB_VARIANT=B ab:rmat24:3:base,k1=GC_B_ASYNC_K:1 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n" >&2; exit 2 ;;
+  # o: the final build with variant B's per-class timing (KTimer shared with the one-GPU engine):
+  #    every GPU test, smoke, the profiles of THIS build, the variant B bench line (its roofline)
+  o) exec_steps=(file:tests/test_gpu_variant_b.py tests smoke
+                 profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
