@@ -107,6 +107,8 @@ case ${1:-} in
   #    every GPU test, smoke, the profiles of THIS build, the variant B bench line (its roofline)
   o) exec_steps=(file:tests/test_gpu_variant_b.py tests smoke
                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o" >&2; exit 2 ;;
+  # p: the final build's per-graph phases (GC_PREP_TIMING) on R-MAT-24 and R-MAT-26 (no rebuild)
+  p) exec_steps=(env:GC_PREP_TIMING=1 step:rmat24 step:rmat26 env:GC_PREP_TIMING=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
