@@ -109,6 +109,11 @@ case ${1:-} in
                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
   # p: the final build's per-graph phases (GC_PREP_TIMING) on R-MAT-24 and R-MAT-26 (no rebuild)
   p) exec_steps=(env:GC_PREP_TIMING=1 step:rmat24 step:rmat26 env:GC_PREP_TIMING=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p" >&2; exit 2 ;;
+  # q: the hub low rows sorted in LDS: the order check on both sort paths, every GPU test, the
+  #    A/B against rocPRIM's segmented sort, the phase times
+  q) exec_steps=(file:tests/test_gpu_hubs.py:hlow_rows_sorted tests smoke
+                 ab:rmat24:5:base,rocprim=GC_HLOW_LDS:0 ab:rmat26:3:base,rocprim=GC_HLOW_LDS:0
+                 env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
