@@ -138,64 +138,6 @@ __global__ void k_hlow_fill(const long long* rp, const int* col, const int* nlow
     }
 }
 
-// hlow rows sorted by hub index in LDS (round 4): a workgroup per row, bitonic over the row
-// padded to a power of two (rows of at most GC_HSORT_MAX entries; R-MAT-24's longest is
-// ~1.7k).  rocPRIM's segmented radix sort took 2.4 ms (R-MAT-24) / 12.3 ms (R-MAT-26) for
-// rows of ~550 entries; GC_HLOW_LDS=0 keeps it, and it is the path for longer rows.
-#define GC_HSORT_MAX 4096
-__global__ void k_hlow_maxlen(const long long* hlow_rp, long long H, unsigned long long* out) {
-    unsigned long long m = 0;
-    for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < H; x += (long long)gridDim.x * blockDim.x) {
-        const unsigned long long L = (unsigned long long)(hlow_rp[x + 1] - hlow_rp[x]);
-        m = L > m ? L : m;
-    }
-    for (int o = GC_WAVE / 2; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(m, o, GC_WAVE);
-        m = y > m ? y : m;
-    }
-    if (gc_lane() == 0 && m) atomicMax(out, m);
-}
-__global__ void __launch_bounds__(GC_BLOCK) k_hlow_sort_lds(const long long* hlow_rp, long long H, int* col) {
-    __shared__ int s[GC_HSORT_MAX];
-    for (long long x = blockIdx.x; x < H; x += gridDim.x) {
-        const long long b = hlow_rp[x];
-        const int L = (int)(hlow_rp[x + 1] - b);
-        if (L <= 1) continue;  // workgroup-uniform
-        int N = 2;
-        while (N < L) N <<= 1;
-        for (int i = threadIdx.x; i < N; i += blockDim.x) s[i] = i < L ? col[b + i] : 0x7FFFFFFF;
-        __syncthreads();
-        for (int k = 2; k <= N; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = threadIdx.x; i < N; i += blockDim.x) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const int a = s[i], c = s[ixj];
-                        if ((a > c) == ((i & k) == 0)) {
-                            s[i] = c;
-                            s[ixj] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int i = threadIdx.x; i < L; i += blockDim.x) col[b + i] = s[i];
-        __syncthreads();
-    }
-}
-// GC_HLOW_CHECK=1: count the hlow rows not in ascending order (a wrong order costs only time,
-// never a colour -- the tests use this to see the sort itself)
-__global__ void k_hlow_check(const long long* hlow_rp, long long H, const int* col, unsigned long long* bad) {
-    for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < H; x += (long long)gridDim.x * blockDim.x) {
-        for (long long e = hlow_rp[x] + 1; e < hlow_rp[x + 1]; ++e)
-            if (col[e - 1] > col[e]) {
-                atomicAdd(bad, 1ull);
-                break;
-            }
-    }
-}
-
 // static chunks of the hlow rows: ceil(len / GC_HCH) per hub, then chunk -> hub
 __global__ void k_hch_count(const long long* hlow_rp, long long H, long long* cnt) {
     const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -391,22 +333,7 @@ int build(gc_graph* g, int T, int W) {
     // order, but rank order is what makes its coloured prefix (hlen) grow -- lower-rank hubs
     // colour first -- and the resumable scans skip it: unsorted, R-MAT-24 153.9 ms -> 6.0 s,
     // R-MAT-26 0.43 -> 25.9 s, profiles/r04/l.  The sort stays.)
-    bool lds_sorted = false;
-    if (EL > 0 && !(getenv("GC_HLOW_LDS") && atoi(getenv("GC_HLOW_LDS")) == 0)) {  // rows short enough for LDS
-        unsigned long long* mx = (unsigned long long*)pos;  // pos: H + 1 >= 1 words of scratch here
-        GC_HIP(hipMemsetAsync(mx, 0, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(k_hlow_maxlen, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const long long*)g->hlow_rp, H, mx);
-        unsigned long long maxlen = 0;
-        GC_HIP(hipMemcpyAsync(&maxlen, mx, sizeof(maxlen), hipMemcpyDeviceToHost, s));
-        GC_HIP(hipStreamSynchronize(s));
-        if (maxlen <= GC_HSORT_MAX) {
-            hipLaunchKernelGGL(k_hlow_sort_lds, dim3((int)std::min<long long>(H, 16384)), dim3(GC_BLOCK), 0, s,
-                               (const long long*)g->hlow_rp, H, g->hlow_col);
-            GC_HIP(hipGetLastError());
-            lds_sorted = true;
-        }
-    }
-    if (EL > 0 && !lds_sorted) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
+    if (EL > 0) {  // every hlow row sorted by hub index == rank (gc_hub_scan_wave walks it in rank order)
         // the keys are hub indices < H: only their low bit_width(H - 1) bits are sorted
         // (R-MAT-26: 20 of 32 bits, three 8-bit digit passes instead of four)
         const unsigned kbits = (unsigned)std::max(1, 64 - __builtin_clzll((unsigned long long)std::max(H - 1, 1ll)));
@@ -421,20 +348,6 @@ int build(gc_graph* g, int T, int W) {
         gc_dfree(tmp);
         GC_HIP(e);
         std::swap(g->hlow_col, g->hpend[0]);  // the unsorted copy becomes working memory
-    }
-    if (EL > 0 && getenv("GC_HLOW_CHECK") && atoi(getenv("GC_HLOW_CHECK")) > 0) {
-        unsigned long long* bad = (unsigned long long*)pos;
-        GC_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(k_hlow_check, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const long long*)g->hlow_rp, H,
-                           (const int*)g->hlow_col, bad);
-        unsigned long long nbad = 0;
-        GC_HIP(hipMemcpyAsync(&nbad, bad, sizeof(nbad), hipMemcpyDeviceToHost, s));
-        GC_HIP(hipStreamSynchronize(s));
-        if (nbad) {
-            gc_dfree(pos);
-            gc_set_error("GC_HLOW_CHECK: %llu hub low rows not in rank order", nbad);
-            return GC_EHIP;
-        }
     }
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
     pc.mark("hlow sort", s);

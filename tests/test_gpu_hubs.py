@@ -150,21 +150,3 @@ def test_commit_big_tiles(monkeypatch, bigrow, hub_t):
     _check(rp, col, symmetric=True, bounded=False)
     rp, col = _random_directed(3000, 30000, 11)
     _check(rp, col)
-
-
-@pytest.mark.parametrize("lds", ["1", "0"], ids=["lds_sort", "rocprim_sort"])
-@pytest.mark.parametrize("hub_t", ["0", "64", "512"])
-def test_hlow_rows_sorted(monkeypatch, lds, hub_t):
-    """The hub low rows come out in rank order from the LDS bitonic sort (rows of at most
-    GC_HSORT_MAX entries) and from rocPRIM's segmented sort (GC_HLOW_LDS=0, and any graph with a
-    longer row): GC_HLOW_CHECK=1 fails the colouring on a row out of order -- an order the
-    colours alone cannot show (the scan's result does not depend on it, only its time)."""
-    monkeypatch.setenv("GC_HLOW_CHECK", "1")
-    monkeypatch.setenv("GC_HLOW_LDS", lds)
-    monkeypatch.setenv("GC_HUB_T", hub_t)
-    for k in ("GC_HUB_W", "GC_HUB_SCAN", "GC_ASYNC"):
-        monkeypatch.delenv(k, raising=False)
-    for scale in (12, 16):
-        with _dg().rmat(scale, 16, seed=scale) as dg:
-            rp, col = dg.export()
-            assert_same_run(dg.color("A"), oracle.c_color(rp, col, "A"))
