@@ -114,6 +114,10 @@ case ${1:-} in
   q) exec_steps=(file:tests/test_gpu_hubs.py:hlow_rows_sorted tests smoke
                  ab:rmat24:5:base,rocprim=GC_HLOW_LDS:0 ab:rmat26:3:base,rocprim=GC_HLOW_LDS:0
                  env:GC_PREP_TIMING=1 step:rmat26 env:GC_PREP_TIMING=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q" >&2; exit 2 ;;
+  # r: the hybrid's switch point on R-MAT-26 at P = 1 (no rebuild)
+  r) exec_steps=("bench:rmat26:--sharded,--multi,hybrid,--switch-below,1000000000,--steps,2,--warmup,1,--no-north-star"
+                 "bench:rmat26:--sharded,--multi,hybrid,--steps,2,--warmup,1,--no-north-star"
+                 "bench:rmat26:--sharded,--multi,hybrid,--switch-below,65536,--steps,2,--warmup,1,--no-north-star") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
