@@ -485,7 +485,7 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
     def step(want_colors):
         kw = dict(want_colors=want_colors, ahead=args.seam_ahead, inline_max=args.seam_inline_max)
         if hybrid:  # sharded rounds while the frontier is large, then every rank's own engine
-            return sh.hybrid_color(ops, comm, resume, switch_below, **kw)
+            return sh.hybrid_color(ops, comm, resume, switch_below, switch_after_peak=True, **kw)
         return sh.shard_color(ops, comm, **kw)
 
     for _ in range(max(args.warmup, 1)):
@@ -517,8 +517,9 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
                        "variant": "A (coloring.py)",
                        "parallelism": f"{world} vertex-range shards (balanced by deg+1), round seams over "
                                       f"{'RCCL' if comm.backend == 'nccl' else comm.backend}"
-                                      + (f"; hybrid: from the first round with a frontier below {switch_below} "
-                                         f"every rank finishes on its own one-GPU engine" if hybrid else ""),
+                                      + (f"; hybrid: from the first round with a frontier below {switch_below}, once "
+                                         f"the frontier has reached it (or after {sh.SWITCH_GRACE} rounds), every rank "
+                                         f"finishes on its own one-GPU engine" if hybrid else ""),
                        "multi": "hybrid" if hybrid else "sharded", "switch_round": res.switch_round,
                        "step": "the colouring of a resident, partitioned graph (creation and validation outside the "
                                "timed region, unlike the one-GPU / replicated step)",

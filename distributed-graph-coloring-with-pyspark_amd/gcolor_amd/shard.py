@@ -38,6 +38,9 @@ from . import _native as nat
 
 KIND_CAND, KIND_STATE, KIND_COLOUR = 0, 1, 2
 OK, FAILED, STALLED = 0, 1, 2
+# hybrid: rounds after which the switch no longer waits for the frontier to reach the
+# switch point (a graph whose frontier never gets that large)
+SWITCH_GRACE = 8
 
 
 def balanced_ranges(rp, parts):
@@ -388,7 +391,7 @@ def _hdr_values(words):
 
 def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=None, local_sweeps=1,
                 want_colors=True, inline=4096, deferred=True, hub_budget=3, fuse=True, ahead=4,
-                inline_max=1 << 16, switch_below=None, round0=0):
+                inline_max=1 << 16, switch_below=None, round0=0, switch_after_peak=False):
     """graph_coloring (coloring.py:73) over the ranks of ``comm``; every rank returns the
     same ShardResult (records with the single-GPU semantics of gc_color).
 
@@ -431,8 +434,11 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     ``switch_below``: stop at the top of the first round whose frontier (all ranks) is
     non-empty and smaller than that -- after the last round's finish has resolved and before
     any of this round's exchanges is applied by the host -- and return with ``switch_round``
-    set (``hybrid_color`` hands the state to the one-GPU engine there).  ``round0`` numbers
-    the rounds of a run started from a colouring in progress."""
+    set (``hybrid_color`` hands the state to the one-GPU engine there).  With
+    ``switch_after_peak`` only once some round's frontier reached ``switch_below`` (or after
+    SWITCH_GRACE rounds): a colouring's first frontiers are the seeds' neighbours, often small,
+    before the frontier peaks (R-MAT-26: the first round's is below n/64, rounds 1-3 far above).
+    ``round0`` numbers the rounds of a run started from a colouring in progress."""
     k = -1 if num_colors is None else int(num_colors)
     U, _ = ops.begin(k, track_rounds)
     res = ShardResult(status=OK, colors=None, colored_round=None)
@@ -497,6 +503,7 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
     last_fmax = None  # largest per-rank frontier of the last propose seam (does the next one fit inline?)
     last_seams = 1  # sweep seams the last round needed (how many a fused round runs ahead)
     r = int(round0)
+    fpeak = 0  # the largest frontier so far (switch_after_peak)
     while True:
         if U == 0 and pending is None:  # coloring.py:86-90
             rec(0, 0, -1, 0, 0)
@@ -559,7 +566,9 @@ def shard_color(ops, comm, num_colors=None, e1=True, track_rounds=False, dense=N
                 break
         F, maxmex, fails = int(hdr[:, 0].sum()), int(hdr[:, 1].max()), int(hdr[:, 2].sum())
         last_fmax = int(hdr[:, 0].max())
-        if switch_below is not None and 0 < F < int(switch_below):
+        fpeak = max(fpeak, F)
+        if switch_below is not None and 0 < F < int(switch_below) and (
+                not switch_after_peak or fpeak >= int(switch_below) or r - round0 >= SWITCH_GRACE):
             # the round's proposals and any sweeps run ahead touched no colour and no frontier
             res.switch_round = r
             break

@@ -277,3 +277,29 @@ def test_gloo_world_size_2(case, dense, inline, deferred_ops, switch_below, tmp_
         assert got["cround"] == list(o["colored_round"])
         assert got["U"] == list(o["round_U"]) and got["F"] == list(o["round_F"])
         assert got["acc"] == list(o["round_accepted"]) and got["seeds"] == list(o["round_seeds"])
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_hybrid_switch_after_peak(parts):
+    """switch_after_peak (the bench's hybrid): the switch waits until some round's frontier
+    reached the switch point -- a first frontier below it (the seeds' neighbours) no longer
+    ends the sharded rounds at round 0 -- or until SWITCH_GRACE rounds have run; records and
+    colours equal the oracle's either way."""
+    for seed in range(3):
+        rp, col = _random_directed(400, 2400, 50 + seed)
+        o = oracle.c_color(rp, col, "A")
+        F = [int(x) for x in o["round_F"]]
+        sw = max(F) // 2 + 1  # reached in some round, not in round 0 when the frontier grows first
+        want = next((i for i, f in enumerate(F)
+                     if 0 < f < sw and (max(F[:i + 1]) >= sw or i >= sh.SWITCH_GRACE)), None)
+        calls = []
+        res = run_threads(rp, col, parts, switch_below=sw, calls=calls, switch_after_peak=True)
+        for r in res:
+            assert_matches_oracle(r, o)
+        assert (calls[0][0] if calls else None) == want
+        calls = []  # a switch point no round reaches: after SWITCH_GRACE rounds
+        res = run_threads(rp, col, parts, switch_below=10**9, calls=calls, switch_after_peak=True)
+        for r in res:
+            assert_matches_oracle(r, o)
+        if len(F) > sh.SWITCH_GRACE and any(f > 0 for f in F[sh.SWITCH_GRACE:]):
+            assert calls[0][0] == next(i for i, f in enumerate(F) if i >= sh.SWITCH_GRACE and f > 0)
