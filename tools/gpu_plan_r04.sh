@@ -118,6 +118,12 @@ case ${1:-} in
   r) exec_steps=("bench:rmat26:--sharded,--multi,hybrid,--switch-below,1000000000,--steps,2,--warmup,1,--no-north-star"
                  "bench:rmat26:--sharded,--multi,hybrid,--steps,2,--warmup,1,--no-north-star"
                  "bench:rmat26:--sharded,--multi,hybrid,--switch-below,65536,--steps,2,--warmup,1,--no-north-star") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r" >&2; exit 2 ;;
+  # s: the hybrid's switch after the frontier peak (host change only): R-MAT-26 and R-MAT-24 at
+  #    P = 1, the shard tests, and the N = 2 default again as two ranks over gloo on this GPU
+  s) exec_steps=("bench:rmat26:--sharded,--multi,hybrid,--steps,2,--warmup,1,--no-north-star"
+                 "bench:rmat24:--sharded,--multi,hybrid,--steps,3,--warmup,1,--no-north-star"
+                 file:tests/test_gpu_resume.py:hybrid file:tests/test_shard_gpu.py
+                 "torchrun:2:--steps,2,--warmup,1,--no-north-star") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
