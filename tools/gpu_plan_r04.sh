@@ -124,6 +124,12 @@ case ${1:-} in
                  "bench:rmat24:--sharded,--multi,hybrid,--steps,3,--warmup,1,--no-north-star"
                  file:tests/test_gpu_resume.py:hybrid file:tests/test_shard_gpu.py
                  "torchrun:2:--steps,2,--warmup,1,--no-north-star") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s" >&2; exit 2 ;;
+  # t: the final build on the other configurations (C2 uniform 10M, C4 mesh 512^3, C5 R-MAT-28),
+  #    variant A and C2 variant B, for the record (no rebuild)
+  t) exec_steps=("bench:uniform10M:--no-north-star,--no-cpu-baseline,--no-end-to-end"
+                 "bench:mesh512:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,5"
+                 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
+                 "bench:uniform10M:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
