@@ -81,6 +81,12 @@ CLASS_KERNELS = {
 }
 
 
+def progress(msg):
+    """A phase line on stderr (stdout carries only the JSON line): a long workload (R-MAT-28)
+    otherwise writes nothing for minutes."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def build_graph(w):
     from gcolor_amd.engine import DeviceGraph, uniform_csr
     if w["kind"] == "uniform":
@@ -467,6 +473,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
     from gcolor_amd import shard as sh
     _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
     t0 = time.time()
+    if rank == 0:
+        progress(f"building {args.workload} ({world} ranks)")
     dg, rp, desc = sharded_graph(WORKLOADS[args.workload], world, args.scaling)
     gen_s = time.time() - t0
     m = dg.nnz // 2
@@ -490,6 +498,8 @@ def run_sharded(args, world, rank, local_rank, dist, torch):
 
     for _ in range(max(args.warmup, 1)):
         res = step(False)
+    if rank == 0:
+        progress("warmup done; timed steps")
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):  # colours stay in HBM, as in the 1-GPU step
@@ -629,7 +639,9 @@ def main():
     if V == "B" and (args.priority_seed is not None or args.speculative):
         raise SystemExit("--priority-seed / --speculative are variant A modes")
     t0 = time.time()
+    progress(f"building {args.workload}")
     dg0, host_csr = build_graph(w)
+    progress("graph built")
     gen_s = time.time() - t0
 
     def barrier():
@@ -653,7 +665,9 @@ def main():
     # partition -> colouring (hub index built inside) -> validation -> handle released, no
     # events.  Then the same K steps again with the dominant class's launch runs bracketed by
     # HIP events on the engine's own stream (the roofline's launch durations).
+    progress("warmup done; timed steps")
     t, kern, r, phases = S.steps(args.steps, None, roctx=True)
+    progress(f"timed steps done ({t * 1e3:.1f} ms per step)")
     t_self = t  # this rank's own step time: for replicated runs, the one-GPU time of the same work
     rounds, sweeps, reseeds, colours = r.rounds, r.jp_sweeps, r.reseeds, r.num_colors
     m_all = m  # edges coloured per step by the whole job
@@ -698,6 +712,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline and V == "A" and args.priority_seed is None and not args.speculative:
         final = S.final_colouring()  # outside the timed region
         try:
+            progress("CPU baseline")
             cpu = cpu_baseline(w, host_csr or final["csr"], final["colors"])
             # the colours must equal the restatement's (bit-exact semantics); a difference is
             # reported in the line (identical_to_gpu) rather than losing the measurement
@@ -713,6 +728,7 @@ def main():
     if world == 1 and not args.no_end_to_end:
         try:
             csr = host_csr or (final["csr"] if final else S.final_colouring()["csr"])
+            progress("end to end")
             e2e_s = S.end_to_end(*csr)
             e2e = {"ms": round(e2e_s * 1e3, 3), "edges_per_s": m / e2e_s,
                    "path": "CSR in pageable host memory -> gc_graph_create (H2D + rank partition) -> gc_color -> "
@@ -726,6 +742,7 @@ def main():
     if world == 1 and args.workload == "rmat24" and not args.no_north_star and V == "A" and not any(mode.values()):
         S.close()
         try:
+            progress("north star (R-MAT-26)")
             ns = north_star(torch, barrier, args)
         except Exception as e:  # noqa: BLE001 -- reported in the line, which still prints
             ns = {"error": f"{type(e).__name__}: {e}"}
