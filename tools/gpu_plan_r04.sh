@@ -130,6 +130,9 @@ case ${1:-} in
                  "bench:mesh512:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,5"
                  "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
                  "bench:uniform10M:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t" >&2; exit 2 ;;
+  # u: the default bench line with its phase lines (the round-end command), then C5 R-MAT-28
+  u) exec_steps=(bench:rmat24
+                 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,2,--warmup,1") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
