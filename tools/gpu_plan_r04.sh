@@ -133,6 +133,11 @@ case ${1:-} in
   # u: the default bench line with its phase lines (the round-end command), then C5 R-MAT-28
   u) exec_steps=(bench:rmat24
                  "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,2,--warmup,1") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u" >&2; exit 2 ;;
+  # v: the hub memory check from the actual hlow size: the full-size tests first (R-MAT-28 now
+  #    with hubs), every GPU test, smoke, C5's bench step, then the profiles of this build
+  v) exec_steps=(file:tests/test_gpu_fullsize.py tests smoke
+                 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
+                 profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
