@@ -138,6 +138,8 @@ case ${1:-} in
   v) exec_steps=(file:tests/test_gpu_fullsize.py tests smoke
                  "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v" >&2; exit 2 ;;
+  # w: C5's hybrid at P = 1 (R-MAT-28 as one shard, then the engine; no rebuild)
+  w) exec_steps=("bench:rmat28:--sharded,--multi,hybrid,--steps,2,--warmup,1,--no-north-star") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r04$1" "${exec_steps[@]}"
