@@ -12,11 +12,13 @@ nnz/2), whole job.  `recolour_ms` is the colouring alone on a persistent handle.
 Other workloads (--workload): uniform10M (C2), rmat26 (north star), mesh512 (C4 on one
 GPU), mesh256, uniform1M, rmat28 (C5, sharded runs).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU,
-ONE graph sharded over the ranks (gcolor_amd.shard).  --scaling weak (default) grows the
-graph with N (uniform n x N, R-MAT scale + log2 N, mesh z x N); --scaling strong keeps
-it fixed (C4: --workload mesh512, C5: --workload rmat28).  Barrier + synchronize around
-the K timed steps, max time over ranks; value = m / t_max.
+Multi-GPU (bench.py --gpus N starts N ranks itself under torch.distributed.run, or runs as
+one rank of an outside launcher): one process per GPU, ONE graph coloured by the ranks
+together (gcolor_amd.shard: the hybrid by default), timed on the one-GPU step's definition
+(create + colour + validate, MultiStep).  Default workload C5 (R-MAT-28, strong scaling);
+--scaling weak grows the graph with N (uniform n x N, R-MAT scale + log2 N, mesh z x N).
+Barrier + synchronize around the K timed steps, max time over ranks; value = m / t_max;
+single_gpu_ms / speedup_vs_single_gpu: the same graph's one-GPU step on rank 0's GPU.
 
 Extra objects on the JSON line:
   roofline      the kernel class that dominates the step BY TIME (every class, JP sweeps
@@ -372,7 +374,7 @@ def north_star(torch, barrier, args):
     balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
     out = {"workload": w["desc"], "n": S.n, "m_undirected": m, "steps": args.north_star_steps,
            "ms_per_step": t * 1e3, "edges_per_s": m / t, "colors_used": r.num_colors, "rounds": r.rounds,
-           "async_jp_aborts": r.async_aborts,
+           "async_jp_aborts": r.async_aborts, "hubs": r.hubs, "hubs_on": r.hubs > 0,
            "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
            # §8d bytes / t / peak: raw, and with no class credited more than the peak could move
            # in its (event-timed) time -- propose's §8d credit for hub rows the bitmaps replace
@@ -440,118 +442,195 @@ def replica_workload(w, world, rank):
     return w
 
 
-def sharded_graph(w, world, scaling):
-    from gcolor_amd.engine import DeviceGraph, uniform_csr
-    w = dict(w)
-    weak = scaling == "weak"
-    if w["kind"] == "uniform":
-        if weak:
-            w["n"] *= world
-        rp, col = uniform_csr(w["n"], w["d"], w["seed"])
-        dg = DeviceGraph.from_csr(rp, col, symmetric=True)
-        del col
-        desc = f"uniform (graph.py:30-43 process) n={w['n'] / 1e6:g}M, max-degree {w['d']}"
-    elif w["kind"] == "rmat":
-        if weak:
-            w["scale"] += int(round(math.log2(world)))
-        dg = DeviceGraph.rmat(w["scale"], w["ef"], seed=w["seed"])
-        rp, _ = dg.export(col=False)
-        desc = f"R-MAT scale {w['scale']}, edge factor {w['ef']}, seed {w['seed']}"
-    else:
-        x, y, z = w["dims"]
-        if weak:
-            z *= world
-        dg = DeviceGraph.mesh(x, y, z)
-        rp, _ = dg.export(col=False)
-        desc = f"3-D 7-point mesh {x}x{y}x{z} (z-slabs)"
-    return dg, rp, desc + (f" (= base x {world} GPUs)" if weak and world > 1 else "")
+def spawn_ranks(n):
+    """`bench.py --gpus N` (N > 1) without a launcher: run this same command as N ranks under
+    torch.distributed.run, one process per GPU, as a CHILD process -- this parent never touches
+    the GPU and is not replaced (no exec) -- and return the child's exit status.  Rank 0 prints
+    the JSON line; the ranks see WORLD_SIZE and do not spawn again."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    progress(f"--gpus {n}: starting {n} ranks (torch.distributed.run, 127.0.0.1:{port})")
+    return subprocess.call(cmd)
 
 
-def run_sharded(args, world, rank, local_rank, dist, torch):
-    """N > 1: ONE graph, vertex-range shards over the N ranks (gcolor_amd.shard)."""
+class MultiStep:
+    """The N-GPU step, on the ONE-GPU step's definition (SURVEY.md §8d's t): from the CSR
+    resident in every rank's HBM to a complete, validated colouring of ONE graph.
+      create    gc_graph_create_device (the rank partition of every row) + gc_shard_create (the
+                rank's vertex range, its in-neighbour rows, the replicated hub state; the hub
+                index is built inside)
+      colour    hybrid_color: the rounds sharded over the ranks while the frontier is large
+                (seams over RCCL), then every rank resumes the one-GPU engine from the replicated
+                state (gcolor_amd.shard); --multi sharded: every round sharded
+      validate  gc_validate_range over the rank's own vertex range + one all-reduce of the two
+                counts (validate_graph_coloring, coloring.py:149-162, split by rows)
+      destroy   both handles
+    The reference's counterpart is its partitioned execution (coloring.py:190-209: local[*],
+    parallelize, partitionBy) and the distributed count of coloring.py:149-162."""
+
+    def __init__(self, args, w, world, rank, comm, torch, dist):
+        from gcolor_amd import shard as sh
+        self.args, self.world, self.rank, self.comm, self.torch, self.dist = args, world, rank, comm, torch, dist
+        self.sh = sh
+        dg0, _ = build_graph(w)  # every rank generates the same graph (deterministic, on its own GPU)
+        self.n, self.nnz, self.max_degree, self.sym = dg0.n, dg0.nnz, dg0.max_degree, dg0.symmetric
+        rp, _ = dg0.export(col=False)
+        self.ranges = sh.balanced_ranges(rp, world)
+        self.lo, self.hi = self.ranges[rank]
+        del rp
+        self.d_rp, self.d_col = resident_csr(dg0, torch)
+        dg0.close()
+        self.hybrid = args.multi == "hybrid"
+        self.switch_below = args.switch_below if args.switch_below > 0 else max(4096, self.n // 64)
+
+    def colour(self, ops, dg, want_colors):
+        sh = self.sh
+        kw = dict(want_colors=want_colors, ahead=self.args.seam_ahead, inline_max=self.args.seam_inline_max)
+        if self.hybrid:
+            return sh.hybrid_color(ops, self.comm, sh.engine_resume(dg), self.switch_below, switch_after_peak=True, **kw)
+        return sh.shard_color(ops, self.comm, **kw)
+
+    def step(self, want_colors=False):
+        from gcolor_amd.engine import DeviceGraph
+        torch = self.torch
+        a = time.perf_counter()
+        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym)
+        ops = self.sh.HipShard(dg, self.lo, self.hi)
+        b = time.perf_counter()
+        res = self.colour(ops, dg, want_colors)
+        c = time.perf_counter()
+        if res.switch_round is not None:  # the resumed engine holds the colouring on every rank
+            unc, conf = dg.validate(None, lo=self.lo, hi=self.hi)
+        else:  # finished sharded: the shard's colours
+            cols = res.colors if res.colors is not None else ops.colors(False, True)[0]
+            unc, conf = dg.validate(cols, lo=self.lo, hi=self.hi)
+        cnt = torch.tensor([unc, conf], dtype=torch.int64, device="cuda" if self.comm.backend == "nccl" else "cpu")
+        self.dist.all_reduce(cnt)
+        unc, conf = (int(x) for x in cnt.tolist())
+        d = time.perf_counter()
+        ops.close()
+        dg.close()
+        e = time.perf_counter()
+        assert unc == 0 and (conf == 0 or not self.sym), f"invalid colouring: {unc} uncoloured, {conf} conflicts"
+        return res, {"create": b - a, "colour": c - b, "validate": d - c, "destroy": e - d}
+
+    def single_gpu(self, reps=2):
+        """The same graph's ONE-GPU step (the N = 1 line's definition) on this rank's GPU: the
+        best of `reps` step times, the colours (a first, untimed run) and one event-timed probe
+        (its kernel classes, for the roofline)."""
+        from gcolor_amd.engine import DeviceGraph
+        times, colours, probe = [], None, None
+        for i in range(reps + 2):  # 0: colours to host; 1..reps: timed; last: event-timed probe
+            timing = i == reps + 1
+            a = time.perf_counter()
+            with DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz,
+                                         symmetric=self.sym) as dg:
+                r = dg.color("A", want_rounds=False, want_colors=(i == 0), kernel_timing=timing)
+                unc, conf = dg.validate()
+            dt = time.perf_counter() - a
+            assert unc == 0 and conf == 0, f"invalid one-GPU colouring: {unc} uncoloured, {conf} conflicts"
+            if i == 0:
+                colours = r.colors
+            elif timing:
+                probe = r
+            else:
+                times.append(dt)
+        return min(times), colours, probe
+
+    def close(self):
+        self.d_rp = self.d_col = None
+        self.torch.cuda.empty_cache()
+
+
+def run_multi(args, world, rank, local_rank, dist, torch):
+    """N > 1 (or --sharded at N = 1): ONE graph coloured by the N ranks together, timed on the
+    N = 1 step's definition (MultiStep).  value = m / t_max, whole job."""
     from gcolor_amd import _native
     from gcolor_amd import shard as sh
     _native.check("gc_set_device", _native.load().gc_set_device(local_rank))
+    w = scaled_workload(WORKLOADS[args.workload], world, args.scaling)
     t0 = time.time()
     if rank == 0:
         progress(f"building {args.workload} ({world} ranks)")
-    dg, rp, desc = sharded_graph(WORKLOADS[args.workload], world, args.scaling)
-    gen_s = time.time() - t0
-    m = dg.nnz // 2
-    lo, hi = sh.balanced_ranges(rp, world)[rank]
-    ops = sh.HipShard(dg, lo, hi)
     comm = sh.TorchTransport()
+    S = MultiStep(args, w, world, rank, comm, torch, dist)
+    gen_s = time.time() - t0
+    m = S.nnz // 2
 
     def barrier():
         torch.cuda.synchronize()
         dist.barrier()
 
-    hybrid = args.multi == "hybrid"
-    switch_below = args.switch_below if args.switch_below > 0 else max(4096, dg.n // 64)
-    resume = sh.engine_resume(dg) if hybrid else None
-
-    def step(want_colors):
-        kw = dict(want_colors=want_colors, ahead=args.seam_ahead, inline_max=args.seam_inline_max)
-        if hybrid:  # sharded rounds while the frontier is large, then every rank's own engine
-            return sh.hybrid_color(ops, comm, resume, switch_below, switch_after_peak=True, **kw)
-        return sh.shard_color(ops, comm, **kw)
-
     for _ in range(max(args.warmup, 1)):
-        res = step(False)
+        res, _ = S.step(False)
     if rank == 0:
         progress("warmup done; timed steps")
     barrier()
     t0 = time.perf_counter()
+    ph = {}
     for _ in range(args.steps):  # colours stay in HBM, as in the 1-GPU step
-        res = step(False)
+        res, p = S.step(False)
+        for k, v in p.items():
+            ph[k] = ph.get(k, 0.0) + v / args.steps
     barrier()
     t = (time.perf_counter() - t0) / args.steps
-    tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+    tt = torch.tensor([t], dtype=torch.float64, device="cuda" if comm.backend == "nccl" else "cpu")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t = float(tt.item())
-    res = step(True)  # once more with the colours to host, outside the timed region
     if rank == 0:
-        unc, conf = dg.validate(res.colors)
-        assert unc == 0 and conf == 0, f"invalid colouring: {unc} uncoloured, {conf} conflicts"
-        one = dg.color("A", want_rounds=False, want_colors=True)  # reference run (outside timing)
-        assert np.array_equal(one.colors, res.colors), "sharded colouring differs from the 1-GPU engine"
-        t1 = min(dg.color("A", want_rounds=False, want_colors=False).device_ms for _ in range(2))  # the same graph on ONE GPU
-        balg = one.balg_bytes + 20.0 * dg.n + 8.0 * dg.nnz
-        achieved = balg / world / t / 1e9
+        progress(f"timed steps done ({t * 1e3:.1f} ms per step); the one-GPU step of the same graph")
+    res, _ = S.step(True)  # once more with the colours to host, outside the timed region
+    line = None
+    if rank == 0:
+        t1, one_colours, probe = S.single_gpu()  # the same graph, the N = 1 step, on rank 0's GPU
+        assert np.array_equal(one_colours, res.colors), "multi-GPU colouring differs from the one-GPU engine"
+        cap = capped_alg(probe.kernels, S.n, S.nnz)
+        achieved = cap / world / t / 1e9
         line = {
             "metric": METRIC, "value": m / t, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": t * 1e3, "higher_is_better": True,
             "scaling": args.scaling if world > 1 else None,
             "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": desc, "n": dg.n, "m_undirected": m, "nnz": dg.nnz, "max_degree": dg.max_degree,
+            "config": {"workload": w["desc"], "n": S.n, "m_undirected": m, "nnz": S.nnz, "max_degree": S.max_degree,
                        "variant": "A (coloring.py)",
                        "parallelism": f"{world} vertex-range shards (balanced by deg+1), round seams over "
                                       f"{'RCCL' if comm.backend == 'nccl' else comm.backend}"
-                                      + (f"; hybrid: from the first round with a frontier below {switch_below}, once "
+                                      + (f"; hybrid: from the first round with a frontier below {S.switch_below}, once "
                                          f"the frontier has reached it (or after {sh.SWITCH_GRACE} rounds), every rank "
-                                         f"finishes on its own one-GPU engine" if hybrid else ""),
-                       "multi": "hybrid" if hybrid else "sharded", "switch_round": res.switch_round,
-                       "step": "the colouring of a resident, partitioned graph (creation and validation outside the "
-                               "timed region, unlike the one-GPU / replicated step)",
+                                         f"finishes on its own one-GPU engine" if S.hybrid else ""),
+                       "multi": "hybrid" if S.hybrid else "sharded", "switch_round": res.switch_round,
+                       "step": "the one-GPU step's definition: resident CSR (HBM, every rank) -> gc_graph_create_device "
+                               "(rank partition) + gc_shard_create (hub index inside) -> colouring over the ranks -> "
+                               "gc_validate_range of each rank's vertex range + all-reduce -> destroy",
                        "rounds": res.rounds, "exchanges_per_step": res.exchanges,
                        "dense_exchanges_per_step": res.dense_exchanges, "jp_extra_sweeps": res.jp_sweeps,
                        "reseeds": res.reseeds, "graph_build_s": round(gen_s, 2),
-                       "seam_ahead": args.seam_ahead, "seam_inline_max": args.seam_inline_max, "sweep_seams_run_ahead": res.ahead_seams,
-                       "fused_misses": res.fused_misses,
-                       # the same graph coloured by the single-GPU engine on rank 0's GPU (best of 2)
-                       "single_gpu_ms": round(t1, 2), "speedup_vs_single_gpu": round(t1 / (t * 1e3), 3)},
+                       "seam_ahead": args.seam_ahead, "seam_inline_max": args.seam_inline_max,
+                       "sweep_seams_run_ahead": res.ahead_seams, "fused_misses": res.fused_misses,
+                       "hubs": probe.hubs, "hubs_on": probe.hubs > 0,
+                       # the same graph, the N = 1 step (create + colour + validate), rank 0's GPU, best of 2
+                       "single_gpu_ms": round(t1 * 1e3, 2), "speedup_vs_single_gpu": round(t1 / t, 3)},
+            "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
             "colors_used": res.max_color + 1,
-            "roofline": {"bound": "hbm", "kernel": "whole colouring per GPU (sharded), §8d algorithmic bytes",
+            "roofline": {"bound": "hbm", "kernel": "whole colouring per GPU, §8d algorithmic bytes of the one-GPU "
+                                                   "colouring (no class credited above the peak) / N / t",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None},
             "cpu_baseline": None,
         }
+    barrier()  # every rank waits for rank 0's one-GPU reference
+    S.close()
+    if line is not None:
         s = json.dumps(line)
         print(s, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(s + "\n")
-    ops.close()
     dist.destroy_process_group()
 
 
@@ -560,7 +639,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="rmat24", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: rmat24 (C3) on one GPU; rmat28 (C5, the north star's scaling graph) for the "
+                         "modes that split one colouring over N > 1 GPUs (hybrid, sharded)")
     ap.add_argument("--variant", default="A", choices=["A", "B"],
                     help="A = coloring.py semantics, B = coloring_optimized.py ('Optimizovano')")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
@@ -600,8 +681,14 @@ def main():
     args = ap.parse_args()
     if args.scaling is None:
         args.scaling = "strong" if args.multi in ("hybrid", "sharded") else "weak"
+    if args.workload is None:
+        args.workload = "rmat28" if args.gpus > 1 and args.multi in ("hybrid", "sharded") else "rmat24"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:  # no launcher: start the N ranks ourselves
+        sys.exit(spawn_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -624,7 +711,7 @@ def main():
         else:
             dist.init_process_group(backend)
         if args.sharded or args.multi in ("sharded", "hybrid"):
-            return run_sharded(args, world, rank, local_rank, dist, torch)
+            return run_multi(args, world, rank, local_rank, dist, torch)
     else:
         torch.cuda.set_device(0)
 
@@ -780,6 +867,9 @@ def main():
                            "partition) -> gc_color (hub index built inside) -> gc_validate -> destroy",
                    "rounds": rounds, "jp_extra_sweeps": sweeps, "reseeds": reseeds,
                    "async_jp_aborts": r.async_aborts,
+                   # the hub engine (pushed forbidden-colour bitmaps, hub JP): a graph with hubs whose
+                   # index did not fit runs row scans instead (gc_color warns on stderr)
+                   "hubs": r.hubs, "hubs_on": r.hubs > 0,
                    "graph_build_s": round(gen_s, 2),
                    "event_timed_class": None if args.no_event_timing else dom_class},
         "end_to_end_ms": e2e and e2e.get("ms"),

@@ -13,6 +13,10 @@
 // stream synchronisation), so a parked block is idle by construction.
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -34,12 +38,32 @@ struct Cache {
     size_t idle_bytes = 0;
 };
 
+// GC_ALLOC_TRACE=1: every hipMalloc / hipFree this allocator makes (cache misses, and frees
+// past the idle cap) of 16 MB or more, with its host time, on stderr
+bool trace_on() {
+    static const bool on = getenv("GC_ALLOC_TRACE") != nullptr;
+    return on;
+}
+
+struct TraceClock {
+    const char* what;
+    size_t bytes;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    TraceClock(const char* w, size_t b) : what(w), bytes(b) {}
+    ~TraceClock() {
+        if (!trace_on() || bytes < ((size_t)16 << 20)) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[gc alloc] %-9s %10.1f MB %9.3f ms\n", what, (double)bytes / 1048576.0, ms);
+    }
+};
+
 Cache& cache() {
     static Cache* c = new Cache();  // never destroyed: frees at process exit would race the runtime's teardown
     return *c;
 }
 
 void release_locked(Cache& c) {
+    TraceClock tc("release", c.idle_bytes);
     int dev0 = 0;
     hipGetDevice(&dev0);
     for (auto& kv : c.idle) {
@@ -72,7 +96,11 @@ hipError_t alloc(void** p, size_t bytes, bool host) {
             return hipSuccess;
         }
     }
-    hipError_t e = host ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+    hipError_t e;
+    {
+        TraceClock tc(host ? "hostalloc" : "malloc", bytes);
+        e = host ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+    }
     if (e != hipSuccess) {  // the cache may hold what is missing: give it back and retry once
         (void)hipGetLastError();
         std::lock_guard<std::mutex> lk(c.mu);
@@ -90,8 +118,21 @@ hipError_t alloc(void** p, size_t bytes, bool host) {
 hipError_t gc_dmalloc(void** p, size_t bytes) { return alloc(p, bytes, false); }
 hipError_t gc_hmalloc(void** p, size_t bytes) { return alloc(p, bytes, true); }
 
-// parked bytes beyond this are freed at once (one graph's buffers fit many times over)
-static const size_t kIdleCap = (size_t)64 << 30;
+// Parked bytes beyond this are freed at once: half the device's memory, at least 64 GB.
+// Round 4's fixed 64 GB was below one R-MAT-28 handle's buffers (~110 GB: the partitioned
+// CSR, the hub transpose and its hlow copies, the work lists), so every step's destroy freed
+// ~40 GB with hipFree -- which returns at once -- and the next large hipMalloc waited ~3 s
+// for that release (GC_ALLOC_TRACE=1, profiles/r05/a: "malloc 1024 MB 3123 ms"), one step in
+// two or three: R-MAT-28's bench step 2.93 s against 1.77 s without the stall.
+static size_t idle_cap() {
+    static size_t cap = 0;
+    if (!cap) {
+        size_t freeb = 0, total = 0;
+        const size_t floor = (size_t)64 << 30;
+        cap = (hipMemGetInfo(&freeb, &total) == hipSuccess && total / 2 > floor) ? total / 2 : floor;
+    }
+    return cap;
+}
 
 hipError_t gc_dfree(void* p) {
     if (!p) return hipSuccess;
@@ -101,7 +142,10 @@ hipError_t gc_dfree(void* p) {
     if (it == c.live.end()) return hipFree(p);  // not ours (never expected)
     const Block b = it->second;
     c.live.erase(it);
-    if (c.idle_bytes + b.bytes > kIdleCap) return b.host ? hipHostFree(p) : hipFree(p);
+    if (c.idle_bytes + b.bytes > idle_cap()) {
+        TraceClock tc("free", b.bytes);
+        return b.host ? hipHostFree(p) : hipFree(p);
+    }
     c.idle.insert({{b.host ? -1 : b.device, b.bytes}, p});
     c.idle_bytes += b.bytes;
     return hipSuccess;

@@ -124,7 +124,7 @@ int gc_build_tiling(gc_graph* g);
 // 1: key = prio_hash(seed, v).  *bad (device) counts entries outside [0, n).
 int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad);
 // -> ctl->uncolored, ctl->conflicts; c8 (optional): the byte mirror of `colors` (the resident colouring)
-int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8 = nullptr);
+int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8, long long lo, long long hi);
 // symmetric graphs: hub transpose (hin_rp / hin_col: the hubs listed in each row) and the
 // lower-rank hubs of every hub row (hlow counts -> klow[x]); hubmap / hid / hub_v ready
 int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow);
@@ -140,6 +140,28 @@ void gc_set_error(const char* fmt, ...);
             gc_set_error("%s failed at %s:%d: %s", #call, __FILE__, __LINE__, hipGetErrorString(e_)); \
             return GC_EHIP;                                                                   \
         }                                                                                     \
+    } while (0)
+
+// Host reads of device data produced on a stream (counts, offsets, exports): the copy is
+// enqueued on THAT stream and waited for with its status checked.  A plain hipMemcpy does not
+// wait for the library's non-blocking streams (round 4's k_hin_fill fault: hin_col was sized
+// from a stale count), and a failure of an earlier kernel is reported here, at the read that
+// depends on it, instead of at a later unrelated call.
+template <typename T>
+inline int gc_read_dev(hipStream_t s, T* host, const T* dev, size_t count = 1) {
+    if (count == 0) return GC_OK;
+    hipError_t e = hipMemcpyAsync(host, dev, sizeof(T) * count, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        gc_set_error("device-to-host read of %zu bytes: %s", sizeof(T) * count, hipGetErrorString(e));
+        return GC_EHIP;
+    }
+    return GC_OK;
+}
+#define GC_READ(s, host, dev, count)                             \
+    do {                                                         \
+        const int rr_ = gc_read_dev((s), (host), (dev), (count)); \
+        if (rr_) return rr_;                                     \
     } while (0)
 
 int gc_alloc_graph_common(gc_graph* g, const int* src);  // deg, maxdeg, rank partition of src, transpose (gc_graph.hip)
@@ -175,6 +197,8 @@ struct KTimer {
     unsigned mask;  // kernel classes to time (bit GC_K_*)
     gc_stats* st;
     int run_cls = -1;  // class of the open run (-1: none)
+    int cnt_cls = -1;  // class the launches since cnt_start are counted for (timed or not)
+    long long cnt_start = 0;
     std::vector<std::pair<int, size_t>> recs;  // (class, event index of start)
     size_t used = 0;
     hipEvent_t ev() {
@@ -189,10 +213,19 @@ struct KTimer {
     const bool dbg_sync = getenv("GC_DEBUG_SYNC") != nullptr;
     int last_cls = -1;
     long long nlaunch = 0;
+    // the kernels launched (GC_LAUNCH) since the class was begun go to its k_launches
+    void count() {
+        if (cnt_cls >= 0 && st) st->k_launches[cnt_cls] += gc_tl_launches - cnt_start;
+        cnt_cls = -1;
+    }
     void begin(int cls) {
         last_cls = cls;
         ++nlaunch;
-        if (st) st->k_launches[cls]++;
+        if (cls != cnt_cls) {
+            count();
+            cnt_cls = cls;
+            cnt_start = gc_tl_launches;
+        }
         if (cls == run_cls) return;  // the open run goes on
         close();
         if (!((mask >> cls) & 1u)) return;
@@ -216,6 +249,7 @@ struct KTimer {
     }
     void collect() {
         close();
+        count();
         if (!mask || !st) return;
         for (auto& r : recs) {
             float ms = 0.f;

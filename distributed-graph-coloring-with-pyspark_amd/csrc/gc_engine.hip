@@ -9,6 +9,7 @@
 // rare events the device cannot finish alone: an E1 re-seed (zero proposers, uncoloured
 // vertices left), a round whose Jones-Plassmann depth exceeded the S sweeps enqueued
 // (more sweeps, then the commit again), a full round-record buffer.
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -43,10 +44,19 @@ extern "C" int gc_set_device(int32_t device) {
     return GC_OK;
 }
 
+thread_local long long gc_tl_launches = 0;
+
 GDev gc_view(const gc_graph* g) {
     GDev d;
     d.n = (int)g->n;
     d.nnz = g->nnz;
+    // GC_TEST_LIST_CAP (tests only): a smaller capacity for the staged list appends, so that a
+    // colouring hits the overflow path (reported GC_EHIP, pipeline halted) on a small graph
+    d.list_cap = g->n;
+    if (const char* e = getenv("GC_TEST_LIST_CAP")) {
+        const long long c = atoll(e);
+        if (c >= 0 && c < d.list_cap) d.list_cap = c;
+    }
     d.rp = g->rp;
     d.col = g->col;
     d.deg = g->deg;
@@ -631,6 +641,7 @@ struct Run {
             st->max_color = h.maxcolor;
             st->jp_sweeps = h.sweep_total;
             st->async_aborts = (int64_t)h.async_aborts;
+            st->hubs = d.hbits_w ? (int64_t)g->nhub : 0;
             st->fail_round = h.halt == GC_H_FAILED ? h.fail_round : -1;
             st->fail_count = h.halt == GC_H_FAILED ? h.fail_count : 0;
             for (const RoundRec& r : recs) st->reseeds += r.seeds;
@@ -654,6 +665,20 @@ struct Run {
 
 }  // namespace
 
+// GC_PREP_TIMING=1: host-side phase times of a colouring's set-up on stderr (each phase ends
+// in a stream synchronisation; gc_hubs.hip prints the hub index's own phases)
+struct ColourClock {
+    bool on = getenv("GC_PREP_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what, hipStream_t s) {
+        if (!on) return;
+        hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[gc color] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out, gc_stats* stats,
                       const ResumeArgs* rs) {
     if (!g || !opt) { gc_set_error("gc_color: null argument"); return GC_EINVAL; }
@@ -662,8 +687,10 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
         return GC_EINVAL;
     }
     GC_HIP(hipSetDevice(g->device));
+    ColourClock cc;
     int rc = gc_alloc_run_state(g);
     if (rc) return rc;
+    cc.mark("run state", g->stream);
     if (stats) {
         // keep caller's round buffers, clear outputs
         gc_stats keep = *stats;
@@ -686,6 +713,7 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     }
     // the rows are partitioned for the rank of this colouring (re-partitioned when it changes)
     if ((rc = gc_set_priority(g, opt->priority, opt->seed))) return rc;
+    cc.mark("priority", g->stream);
     if (opt->variant == GC_VARIANT_B) return gc_color_variant_b(g, opt, colors_out, cround_out, stats);
     if (opt->speculative) return gc_color_speculative(g, opt, colors_out, cround_out, stats);
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
@@ -693,6 +721,7 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     // hubs: forbidden-colour bitmaps for their proposals; the hub JP (hubs rank above every
     // light vertex) only under (deg, pos) -- seeded ranks resolve hubs by row scans
     if ((rc = gc_hubs_prepare(g, run.d))) return rc;
+    cc.mark("hubs", g->stream);
     if (opt->priority != GC_PRIORITY_REF) {
         run.d.hub_w = 0;
         run.d.tail_hmax = GC_TAIL_HMAX;
@@ -711,7 +740,10 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     }
     run.d.accs = g->accs;
     GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
-    return run.go(colors_out, cround_out, rs);  // stats->rounds may exceed round_cap: the caller re-asks
+    cc.mark("set-up", g->stream);
+    rc = run.go(colors_out, cround_out, rs);  // stats->rounds may exceed round_cap: the caller re-asks
+    cc.mark("rounds", g->stream);
+    return rc;
 }
 
 extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,
@@ -736,6 +768,16 @@ extern "C" int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t
 
 extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts) {
     if (!g) { gc_set_error("gc_validate: null graph"); return GC_EINVAL; }
+    return gc_validate_range(g, colors, 0, g->n, uncolored, conflicts);
+}
+
+extern "C" int gc_validate_range(gc_graph* g, const int32_t* colors, int64_t lo, int64_t hi, int64_t* uncolored,
+                                 int64_t* conflicts) {
+    if (!g) { gc_set_error("gc_validate: null graph"); return GC_EINVAL; }
+    if (lo < 0 || hi > g->n || lo > hi) {
+        gc_set_error("gc_validate_range: [%lld, %lld) is not within [0, %lld)", (long long)lo, (long long)hi, g->n);
+        return GC_EINVAL;
+    }
     GC_HIP(hipSetDevice(g->device));
     int rc = gc_alloc_run_state(g);
     if (rc) return rc;
@@ -751,7 +793,7 @@ extern "C" int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolore
     // mirror c8 (n bytes instead of 4n of random-gather footprint: 67 MB against 268 MB on
     // R-MAT-26; bit-exact, tests/test_gpu_parity.py); GC_VALIDATE_C8=0 gathers the int colours
     const bool c8 = !colors && !(getenv("GC_VALIDATE_C8") && atoi(getenv("GC_VALIDATE_C8")) == 0);
-    if ((rc = gc_validate_tiles(g, src, c8 ? g->c8 : nullptr))) return rc;
+    if ((rc = gc_validate_tiles(g, src, c8 ? g->c8 : nullptr, lo, hi))) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, g->stream));
     GC_HIP(hipStreamSynchronize(g->stream));
     if (uncolored) *uncolored = (int64_t)g->hctl->uncolored;

@@ -157,9 +157,10 @@ static int exclusive_scan_ll(const long long* in, long long* out, long long coun
     void* tmp = nullptr;
     GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
-    hipStreamSynchronize(s);
+    const hipError_t se = hipStreamSynchronize(s);
     gc_dfree(tmp);
     GC_HIP(e);
+    GC_HIP(se);
     return GC_OK;
 }
 
@@ -271,8 +272,8 @@ int gc_alloc_graph_common(gc_graph* g, const int* src) {
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi) {
     hipStream_t s = g->stream;
     long long e0 = 0, e1 = 0;
-    GC_HIP(hipMemcpy(&e0, g->rp + lo, sizeof(long long), hipMemcpyDeviceToHost));
-    GC_HIP(hipMemcpy(&e1, g->rp + hi, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_READ(s, &e0, g->rp + lo, 1);
+    GC_READ(s, &e1, g->rp + hi, 1);
     long long* cnt = nullptr;
     GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(g->n + 1)));
     GC_HIP(gc_dmalloc((void**)&g->trp, sizeof(long long) * (size_t)(g->n + 1)));
@@ -306,7 +307,7 @@ int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi) {
     gc_dfree(cnt);
     if (rc) return rc;
     long long e = 0;
-    GC_HIP(hipMemcpy(&e, g->trp + g->n, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_READ(s, &e, (const long long*)g->trp + g->n, 1);
     GC_HIP(gc_dmalloc((void**)&g->tcol, sizeof(int) * (size_t)std::max<long long>(e, 1)));
     if (g->n > 0)
         hipLaunchKernelGGL(k_filter_fill, dim3(grid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->n, lo, hi, g->trp, g->tcol);
@@ -524,8 +525,8 @@ extern "C" int gc_graph_device(const gc_graph* g, int32_t* device) {
 extern "C" int gc_graph_export(const gc_graph* g, int64_t* row_ptr, int32_t* col) {
     if (!g) { gc_set_error("null graph"); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    if (row_ptr) GC_HIP(hipMemcpy(row_ptr, g->rp, sizeof(long long) * (size_t)(g->n + 1), hipMemcpyDeviceToHost));
-    if (col && g->nnz) GC_HIP(hipMemcpy(col, g->col, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToHost));
+    if (row_ptr) GC_READ(g->stream, (long long*)row_ptr, (const long long*)g->rp, (size_t)(g->n + 1));
+    if (col && g->nnz) GC_READ(g->stream, (int*)col, (const int*)g->col, (size_t)g->nnz);
     return GC_OK;
 }
 
@@ -543,6 +544,6 @@ extern "C" int gc_graph_export_device(const gc_graph* g, int64_t* d_row_ptr, int
 extern "C" int gc_graph_lower_counts(const gc_graph* g, int32_t* nlow_out) {
     if (!g || !nlow_out) { gc_set_error("null argument"); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
-    if (g->n) GC_HIP(hipMemcpy(nlow_out, g->nlow, sizeof(int) * (size_t)g->n, hipMemcpyDeviceToHost));
+    if (g->n) GC_READ(g->stream, (int*)nlow_out, (const int*)g->nlow, (size_t)g->n);
     return GC_OK;
 }

@@ -156,9 +156,10 @@ int scan_ll(const long long* in, long long* out, long long count, hipStream_t s)
     void* tmp = nullptr;
     GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
-    hipStreamSynchronize(s);
+    const hipError_t se = hipStreamSynchronize(s);  // (a fault of an earlier kernel on s shows here)
     gc_dfree(tmp);
     GC_HIP(e);
+    GC_HIP(se);
     return GC_OK;
 }
 
@@ -168,9 +169,10 @@ int scan_u32(const unsigned* in, unsigned* out, long long count, hipStream_t s) 
     void* tmp = nullptr;
     GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0u, (size_t)count, rocprim::plus<unsigned>(), s);
-    hipStreamSynchronize(s);
+    const hipError_t se = hipStreamSynchronize(s);
     gc_dfree(tmp);
     GC_HIP(e);
+    GC_HIP(se);
     return GC_OK;
 }
 
@@ -217,7 +219,7 @@ int build(gc_graph* g, int T, int W) {
     int rc = scan_u32(wcnt, g->hubpre, words + 1, s);
     gc_dfree(wcnt);
     unsigned Hu = 0;
-    if (!rc && hipMemcpy(&Hu, g->hubpre + words, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) rc = GC_EHIP;
+    if (!rc) rc = gc_read_dev(s, &Hu, (const unsigned*)g->hubpre + words);
     const long long H = Hu;
     long long* pos = nullptr;
     if (rc || H == 0) {
@@ -231,6 +233,8 @@ int build(gc_graph* g, int T, int W) {
     freeb += gc_cache_idle_bytes();
     const double need = 4.0 * (double)n + 8.0 * (double)(n + 1) + (28.0 + 4.0 * W) * (double)H;
     if (need > 0.5 * (double)freeb) {  // no room: row scans as before
+        fprintf(stderr, "[gcolor] warning: hub index skipped (%lld hubs): its ids and bitmaps need %.1f GB, %.1f GB "
+                        "free; hubs are resolved by row scans (slower)\n", H, need / 1e9, (double)freeb / 1e9);
         g->hub_t = T;
         g->nhub = 0;
         return GC_OK;
@@ -256,11 +260,12 @@ int build(gc_graph* g, int T, int W) {
         if (e == hipSuccess)
             hipLaunchKernelGGL(k_hub_reindex, dim3(grid_of(H)), dim3(GC_BLOCK), 0, s, (const ull*)k1, H, g->hid, g->hub_v,
                                (const unsigned*)g->hubmap, (const unsigned*)g->hubpre, g->hperm);
-        hipStreamSynchronize(s);
+        const hipError_t se = hipStreamSynchronize(s);
         gc_dfree(tmp);
         gc_dfree(k0);
         gc_dfree(k1);
         GC_HIP(e);
+        GC_HIP(se);
     }
     pc.mark("rank sort", s);
     const int hgrid = (int)std::max<long long>(1, std::min<long long>((H + 3) / 4, 8192));
@@ -280,14 +285,14 @@ int build(gc_graph* g, int T, int W) {
         hipLaunchKernelGGL(k_hub_count, dim3(hgrid), dim3(GC_BLOCK), 0, s, g->rp, g->col, g->hub_v, H, (ull*)pos);
         if ((rc = scan_ll(pos, g->hin_rp, n + 1, s))) { gc_dfree(pos); return rc; }
     }
-    GC_HIP(hipMemcpy(&E, g->hin_rp + n, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_READ(s, &E, (const long long*)g->hin_rp + n, 1);
     GC_HIP(gc_dmalloc((void**)&g->hlow_rp, sizeof(long long) * (size_t)(H + 1)));
     if (sym) {  // the hlow rows' offsets now: their total sizes the memory check below
         rc = scan_ll(klow, g->hlow_rp, H + 1, s);
         gc_dfree(klow);
         klow = nullptr;
         if (rc) { gc_dfree(pos); return rc; }
-        GC_HIP(hipMemcpy(&EL, g->hlow_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
+        GC_READ(s, &EL, (const long long*)g->hlow_rp + H, 1);
     }
     pc.mark("hin count", s);
     hipMemGetInfo(&freeb, &totalb);
@@ -298,6 +303,9 @@ int build(gc_graph* g, int T, int W) {
     // 49 s a step with row scans (profiles/r04/u).
     const double need2 = 4.0 * (double)E + 20.0 * (double)(sym ? EL : E) + (28.0 + 4.0 * W) * (double)H;
     if (need2 > 0.6 * (double)freeb) {
+        fprintf(stderr, "[gcolor] warning: hub index skipped (%lld hubs, %lld hub entries): its transpose needs "
+                        "%.1f GB, %.1f GB free; hubs are resolved by row scans (slower)\n", H, E, need2 / 1e9,
+                (double)freeb / 1e9);
         gc_dfree(pos);
         gc_dfree(klow);
         gc_hub_bits_free(g);
@@ -321,7 +329,7 @@ int build(gc_graph* g, int T, int W) {
                            H, pos);
         if ((rc = scan_ll(pos, g->hlow_rp, H + 1, s))) { gc_dfree(pos); return rc; }
     }
-    GC_HIP(hipMemcpy(&EL, g->hlow_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_READ(s, &EL, (const long long*)g->hlow_rp + H, 1);
     GC_HIP(gc_dmalloc((void**)&g->hlow_col, sizeof(int) * (size_t)std::max<long long>(EL, 1)));
     GC_HIP(gc_dmalloc((void**)&g->hpend[0], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
     GC_HIP(gc_dmalloc((void**)&g->hpend[1], sizeof(int) * (size_t)std::max<long long>(EL, 1)));
@@ -351,9 +359,10 @@ int build(gc_graph* g, int T, int W) {
         GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
         const hipError_t e = rocprim::segmented_radix_sort_keys(tmp, bytes, g->hlow_col, g->hpend[0], (unsigned)EL,
                                                                 (unsigned)H, g->hlow_rp, g->hlow_rp + 1, 0, kbits, s);
-        hipStreamSynchronize(s);
+        const hipError_t se = hipStreamSynchronize(s);
         gc_dfree(tmp);
         GC_HIP(e);
+        GC_HIP(se);
         std::swap(g->hlow_col, g->hpend[0]);  // the unsorted copy becomes working memory
     }
     GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(H + 1), s));
@@ -361,7 +370,7 @@ int build(gc_graph* g, int T, int W) {
     hipLaunchKernelGGL(k_hch_count, dim3(grid_of(H + 1)), dim3(GC_BLOCK), 0, s, g->hlow_rp, H, pos);
     GC_HIP(gc_dmalloc((void**)&g->hch_rp, sizeof(long long) * (size_t)(H + 1)));
     if ((rc = scan_ll(pos, g->hch_rp, H + 1, s))) { gc_dfree(pos); return rc; }
-    GC_HIP(hipMemcpy(&g->nhch, g->hch_rp + H, sizeof(long long), hipMemcpyDeviceToHost));
+    GC_READ(s, &g->nhch, (const long long*)g->hch_rp + H, 1);
     GC_HIP(gc_dmalloc((void**)&g->hch_own, sizeof(int) * (size_t)std::max<long long>(g->nhch, 1)));
     GC_HIP(gc_dmalloc((void**)&g->hkcnt, sizeof(int) * (size_t)H));
     GC_HIP(gc_dmalloc((void**)&g->hk, sizeof(unsigned) * (size_t)H));

@@ -240,8 +240,10 @@ __device__ __forceinline__ int gc_vpw(long long cnt, long long waves) {
 // Per-wave append staging in LDS: one global atomic per GC_STAGE_CAP entries instead of
 // one per wave-instruction (a single counter saturates at ~88 returning atomics/us).
 // Every list a stage flushes into holds `cap` entries (int32[n]); a flush whose base + count
-// would pass it writes nothing and sets DevCtl.loop_err = GC_LERR_LIST, which the host
-// reports as GC_EHIP: a wrong base becomes a reported error, never an aperture fault.
+// would pass it writes nothing, sets DevCtl.loop_err = GC_LERR_LIST, which the host reports
+// as GC_EHIP, and halts the pipeline (DevCtl.halt = GC_H_STALLED): the list's counter is left
+// past its capacity, and every later kernel returns at once instead of reading the list up to
+// that count.  A wrong base becomes a reported error, never an aperture fault.
 #define GC_LERR_LIST 5
 #define GC_LERR_INL 6  // k_propose<1>: a hub bitmap no longer covers the colours in use
 struct GcStage {
@@ -249,6 +251,7 @@ struct GcStage {
     int cnt;  // wave-uniform
     long long cap;  // entries of the destination list
     int* err;       // DevCtl.loop_err
+    int* halt;      // DevCtl.halt
 };
 
 // A commit that closes its own round (k_commit with tclose) counts arrivals in the high bits
@@ -261,7 +264,10 @@ struct GcStage {
 // the bound of one wave's flush (base and count wave-uniform): false = overflow, reported
 __device__ __forceinline__ bool gc_stage_fits(const GcStage& s, ull base) {
     if (base + (ull)s.cnt <= (ull)s.cap) return true;
-    if (gc_lane() == 0) __hip_atomic_store(s.err, GC_LERR_LIST, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gc_lane() == 0) {
+        __hip_atomic_store(s.err, GC_LERR_LIST, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(s.halt, GC_H_STALLED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return false;
 }
 

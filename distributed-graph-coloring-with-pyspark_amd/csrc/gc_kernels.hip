@@ -945,10 +945,10 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
     const unsigned char* __restrict__ k8 = g.k8;
     // undecided appends staged in LDS: one atomic per 512 entries, not one per wave-chunk
     // (a single counter takes ~88 returning atomics/us; 86k chunks cost ~1 ms)
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     // heavy vertices first.  Hubs off: a workgroup each, undecided ones staged by wave 0
     __shared__ int s_hstage[GC_STAGE_CAP];
-    GcStage hst{s_hstage, 0, g.n, &g.ctl->loop_err};
+    GcStage hst{s_hstage, 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     long long* const hdout = g.hub_repl ? nullptr : dout;  // replicated hubs (shards) are never sent
     if (g.hub_w) {  // hubs on: a wave per hub (gc_hub_jp_wave), undecided staged per wave
         // a wave's hubs are i = wid + j * waves; lane l loads the state of hub j0 + l, so a
@@ -1927,7 +1927,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     ull* next_cnt = &c->fcnt[nxt];
     const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);  // next list: k_front_*
     const bool mark = big && !gc_pull_on(c);                              // else k_pull claims
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     long long lmaxc = -1;
     ull lacc = 0, lsum = 0;
 #if GC_CHECKS
@@ -2199,7 +2199,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
     const bool big = mode == GC_CM_ROUND && allow_big && gc_big_on(g, c);
     const bool mark = big && !gc_pull_on(c);
     const bool walk_t = mark || !big;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long j0 = 0; j0 < nb; j0 += GC_BLOCK) {
         const int tn = (int)(nb - j0 < GC_BLOCK ? nb - j0 : GC_BLOCK);
@@ -2443,7 +2443,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_list_commit(GDev g, GLists L
     ull* next_cnt = &c->fcnt[nxt];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     long long lmaxc = -1;
     ull lacc = 0;
     const long long cnt = (long long)c->rwin_cnt;
@@ -2510,7 +2510,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_scan_commit(GDev g, GLists L
     ull* next_cnt = &c->fcnt[nxt];
     const int round = (int)(c->round + 1);
     const bool want_cround = c->want_cround != 0;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     long long lmaxc = -1;
     ull lacc = 0;
     const long long n = g.n;
@@ -2652,7 +2652,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_shard_hub_claim(GDev g, GLists L, 
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
     const int slot = slot_next ? (c->cur ^ 1) : c->cur;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const long long H = g.nhub_repl;
     const long long steps = (H + GC_WAVE - 1) / GC_WAVE;
     for (long long sidx = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; sidx < steps;
@@ -2716,7 +2716,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_unc_compact(GDev g, int* list, ull
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v - lane < g.n; v += stride) {
         const bool u = v < g.n && g.c8[v] == GC_C8_NONE;
@@ -2941,25 +2941,25 @@ __global__ void k_degrees(const long long* rp, int n, long long nnz, int* deg, u
 // host-callable launch wrappers
 // ------------------------------------------------------------------------------------
 void gcl_init(const GDev& g, int* seed_light, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, seed_light);
+    GC_LAUNCH(k_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, seed_light);
 }
 void gcl_seed_prep(const GDev& g, int* sl, int* sh, hipStream_t s) {
-    hipLaunchKernelGGL(k_seed_prep, dim3(1), dim3(64), 0, s, g, sl, sh);
+    GC_LAUNCH(k_seed_prep, dim3(1), dim3(64), 0, s, g, sl, sh);
 }
 int gcl_fsort_blocks(long long n) { return (int)(((n + 31) / 32 + GC_BLOCK - 1) / GC_BLOCK); }
 void gcl_fsort(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s) {
     const int nb = gcl_fsort_blocks(g.n);
     if (nb <= 0) return;
-    hipLaunchKernelGGL(k_fsort_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
-    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 0);
-    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 0);
+    GC_LAUNCH(k_fsort_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
+    GC_LAUNCH(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 0);
+    GC_LAUNCH(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 0);
 }
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s) {
     const int nb = gcl_fsort_blocks(g.n);
     if (nb <= 0) return;
-    hipLaunchKernelGGL(k_front_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
-    hipLaunchKernelGGL(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 1);
-    hipLaunchKernelGGL(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 1);
+    GC_LAUNCH(k_front_count, dim3(nb), dim3(GC_BLOCK), 0, s, g, bsum);
+    GC_LAUNCH(k_fsort_scan, dim3(1), dim3(1024), 0, s, g, bsum, nb, 1);
+    GC_LAUNCH(k_fsort_write, dim3(nb), dim3(GC_BLOCK), 0, s, g, (const unsigned*)bsum, L, 1);
 }
 // Grids of the gather-heavy round kernels (workgroups; they grid-stride over device
 // counts).  Their waves spend ~80% of their cycles waiting on gathers (SQ_WAIT_ANY), so
@@ -3000,63 +3000,63 @@ __global__ void k_stat_reduce(GDev g) {
     }
 }
 void gcl_stat_reduce(const GDev& g, hipStream_t s) {
-    hipLaunchKernelGGL(k_stat_reduce, dim3(1), dim3(64), 0, s, g);
+    GC_LAUNCH(k_stat_reduce, dim3(1), dim3(64), 0, s, g);
 }
 
 void gcl_pack_c4(const GDev& g, hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
+    GC_LAUNCH(k_pack_c4, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g);
 }
 void gcl_propose(const GDev& g, const GLists& L, hipStream_t s, int small, int inl) {
-    if (inl) hipLaunchKernelGGL(k_propose<1>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
-    else hipLaunchKernelGGL(k_propose<0>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
+    if (inl) GC_LAUNCH(k_propose<1>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
+    else GC_LAUNCH(k_propose<0>, dim3(small ? kGridPS : kGridP), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_propose_block(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
+    GC_LAUNCH(k_propose_block, dim3(kGridPB), dim3(GC_BLOCK), (size_t)GC_MEX_WORDS * 4, s, g, L);
 }
 void gcl_resolve(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_resolve, dim3(g.heavy_wg ? kGridRH : kGridR), dim3(GC_BLOCK), 0, s, g, L);
+    GC_LAUNCH(k_resolve, dim3(g.heavy_wg ? kGridRH : kGridR), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep, dim3(g.heavy_wg ? kGridSH : kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
+    GC_LAUNCH(k_sweep, dim3(g.heavy_wg ? kGridSH : kGridS), dim3(GC_BLOCK), 0, s, g, L, i);
 }
 void gcl_delta_cand(const GDev& g, const GLists& L, hipStream_t s) {
-    hipLaunchKernelGGL(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
+    GC_LAUNCH(k_delta_cand, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L);
 }
 void gcl_apply(const GDev& g, int kind, const long long* recv, long long count, long long lo, long long hi, int round,
                int* rwin, hipStream_t s, long long hdr_stride) {
     if (count <= 0) return;
-    hipLaunchKernelGGL(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round, rwin,
+    GC_LAUNCH(k_apply, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, kind, recv, count, lo, hi, round, rwin,
                        hdr_stride);
 }
 __global__ void k_shard_clear_halt(GDev g, int code) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && g.ctl->halt == code) g.ctl->halt = GC_RUN;
 }
 void gcl_shard_clear_halt(const GDev& g, int code, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_clear_halt, dim3(1), dim3(64), 0, s, g, code);
+    GC_LAUNCH(k_shard_clear_halt, dim3(1), dim3(64), 0, s, g, code);
 }
 void gcl_shard_list_commit(const GDev& g, const GLists& L, const int* rwin, int* big, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_list_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, rwin, big);
+    GC_LAUNCH(k_shard_list_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, rwin, big);
 }
 void gcl_shard_scan_commit(const GDev& g, const GLists& L, long long lo, long long hi, int* big, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_scan_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, big);
+    GC_LAUNCH(k_shard_scan_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, big);
 }
 void gcl_shard_pack(const GDev& g, int kind, int slot, const long long* delta, long long* send, long long cap,
                     hipStream_t s) {
     const int grid = (int)std::max<long long>(1, std::min<long long>((cap + GC_BLOCK - 1) / GC_BLOCK, 64));
-    hipLaunchKernelGGL(k_shard_pack, dim3(grid), dim3(GC_BLOCK), 0, s, g, kind, slot, delta, send, cap);
+    GC_LAUNCH(k_shard_pack, dim3(grid), dim3(GC_BLOCK), 0, s, g, kind, slot, delta, send, cap);
 }
 void gcl_shard_reset(const GDev& g, long long round, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
+    GC_LAUNCH(k_shard_reset, dim3(1), dim3(64), 0, s, g, round);
 }
 void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStream_t s) {
     if (g.hub_repl && g.nhub_repl > 0)
-        hipLaunchKernelGGL(k_shard_hub_claim, dim3((int)std::min<long long>((g.nhub_repl + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, L, slot_next);
+        GC_LAUNCH(k_shard_hub_claim, dim3((int)std::min<long long>((g.nhub_repl + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, L, slot_next);
 }
 void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s) {
     if (g.hub_repl && g.hub_w && g.n > 0)
-        hipLaunchKernelGGL(k_shard_hub_flags, dim3((int)std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, lo, hi);
+        GC_LAUNCH(k_shard_hub_flags, dim3((int)std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 2048)), dim3(GC_BLOCK), 0, s, g, lo, hi);
 }
-void gcl_shard_flip(const GDev& g, hipStream_t s) { hipLaunchKernelGGL(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
+void gcl_shard_flip(const GDev& g, hipStream_t s) { GC_LAUNCH(k_shard_flip, dim3(1), dim3(64), 0, s, g); }
 // the winners gc_hub_push_wave left in `big`: their hub lists as one flat range over the
 // whole grid, GC_BLOCK winners at a time (every workgroup scans the tile's list lengths and
 // takes its stride of the tile's entries), 4 entries per thread in flight.  (Round 3 gave
@@ -3130,41 +3130,41 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hub_push_big(GDev g, const int* bi
 }
 #endif
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s) {
-    hipLaunchKernelGGL(k_hub_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, big, cnt);
+    GC_LAUNCH(k_hub_push_big, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, big, cnt);
 }
 void gcl_close(const GDev& g, const GLists& L, int mode, hipStream_t s, int allow_big, int fused, DevCtl* snap) {
-    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big, fused, snap);
+    GC_LAUNCH(k_close, dim3(1), dim3(64), 0, s, g, L, mode, allow_big, fused, snap);
 }
 void gcl_resume(const GDev& g, const GLists& L, const int* colors, const int* cround, const int* front, long long nf,
                 int* big, ull* big_cnt, hipStream_t s) {
     const int grid = (int)std::max<long long>(1, std::min<long long>((g.n + GC_BLOCK - 1) / GC_BLOCK, 8192));
-    hipLaunchKernelGGL(k_resume_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, cround);
+    GC_LAUNCH(k_resume_init, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, cround);
     if (nf > 0)
-        hipLaunchKernelGGL(k_resume_front, dim3((int)std::max<long long>(1, std::min<long long>((nf + GC_BLOCK - 1) / GC_BLOCK, 8192))),
+        GC_LAUNCH(k_resume_front, dim3((int)std::max<long long>(1, std::min<long long>((nf + GC_BLOCK - 1) / GC_BLOCK, 8192))),
                            dim3(GC_BLOCK), 0, s, g, L, front, nf);
     if (g.hbits_w) {
-        hipLaunchKernelGGL(k_resume_hbits, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, big, big_cnt);
+        GC_LAUNCH(k_resume_hbits, dim3(grid), dim3(GC_BLOCK), 0, s, g, colors, big, big_cnt);
         gcl_hub_push_big(g, big, big_cnt, s);
     }
-    hipLaunchKernelGGL(k_resume_close, dim3(1), dim3(64), 0, s, g, L);
+    GC_LAUNCH(k_resume_close, dim3(1), dim3(64), 0, s, g, L);
 }
 void gcl_shard_own_front(const GDev& g, const GLists& L, long long lo, long long hi, int* out, ull* out_cnt,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_own_front, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, out, out_cnt);
+    GC_LAUNCH(k_shard_own_front, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, out, out_cnt);
 }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
+    GC_LAUNCH(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
 }
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep_loop, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S);
+    GC_LAUNCH(k_sweep_loop, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S);
 }
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
-    if (g.tail_nw == 16) hipLaunchKernelGGL(k_sweep_tail<16>, dim3(1), dim3(16 * GC_WAVE), 0, s, g, L, S);
-    else if (g.tail_nw == 8) hipLaunchKernelGGL(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
-    else hipLaunchKernelGGL(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
+    if (g.tail_nw == 16) GC_LAUNCH(k_sweep_tail<16>, dim3(1), dim3(16 * GC_WAVE), 0, s, g, L, S);
+    else if (g.tail_nw == 8) GC_LAUNCH(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
+    else GC_LAUNCH(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
 }
 void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
+    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
 }
 int gcl_sweep_async_blocks_per_cu() {
     int b = 0;
@@ -3172,33 +3172,33 @@ int gcl_sweep_async_blocks_per_cu() {
     return b;
 }
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
-    hipLaunchKernelGGL(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
+    GC_LAUNCH(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);
 }
 void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream_t s, int allow_big, int fused,
                 DevCtl* snap, int tclose) {
     const int gc = kGridC;
     if (fused) {  // no heavy vertex, so nothing is deferred to k_commit_big
-        hipLaunchKernelGGL(k_commit<1>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
+        GC_LAUNCH(k_commit<1>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
         return;
     }
-    hipLaunchKernelGGL(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
+    GC_LAUNCH(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        hipLaunchKernelGGL(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
+        GC_LAUNCH(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
+    GC_LAUNCH(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
 }
 void gcl_cc_hook(const GDev& g, const int* list, const ull* cnt, int* parent, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_hook, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent);
+    GC_LAUNCH(k_cc_hook, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent);
 }
 void gcl_cc_best(const GDev& g, const int* list, const ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_best, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
+    GC_LAUNCH(k_cc_best, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);
 }
 void gcl_cc_seeds(const GDev& g, const int* list, const ull* cnt, int* parent, const ull* best, int* sl, int* sh,
                   int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best, sl, sh);
+    GC_LAUNCH(k_cc_seeds, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best, sl, sh);
 }
 void gcl_degrees(const long long* rp, int n, long long nnz, int* deg, unsigned char* kb, ull* maxdeg, ull* bad, int grid,
                  hipStream_t s) {
-    hipLaunchKernelGGL(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, nnz, deg, kb, maxdeg, bad);
+    GC_LAUNCH(k_degrees, dim3(grid), dim3(GC_BLOCK), 0, s, rp, n, nnz, deg, kb, maxdeg, bad);
 }

@@ -4,9 +4,21 @@
 #include "gc_internal.h"
 
 // Graph + run state, passed by value to every kernel.
+// Host-side count of the round kernels this thread has launched (every launch in
+// gc_kernels.hip, gc_variant_b.hip and gc_priority.hip goes through GC_LAUNCH): KTimer
+// attributes the launches between two class switches to the class, so a bracket that
+// enqueues two kernels (gcl_commit: k_commit + k_commit_big) counts two.
+extern thread_local long long gc_tl_launches;
+#define GC_LAUNCH(...)                    \
+    do {                                  \
+        ++gc_tl_launches;                 \
+        hipLaunchKernelGGL(__VA_ARGS__);  \
+    } while (0)
+
 struct GDev {
     int n;
     long long nnz;
+    long long list_cap;  // entries a staged append may place in a work list (n; GC_TEST_LIST_CAP lowers it in tests)
     const long long* rp;
     const int* col;
     const int* deg;

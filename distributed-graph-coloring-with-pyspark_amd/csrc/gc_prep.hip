@@ -537,15 +537,23 @@ __device__ __forceinline__ bool same_colour8(const int* colors, int u, unsigned 
 // and only the low entries are gathered: half the gathers, col still read whole (the rows
 // are staged tile by tile).  Duplicates mirror too: each copy counts on both sides.
 
+// Rows [V.lo, V.hi) only (gc_validate_range): the tiles [t0, t1) and segments [s0, s1) that
+// hold them; rows of a boundary tile outside the range are skipped.
+struct VRange {
+    long long t0, t1, s0, s1;
+    int lo, hi;
+};
+
 template <int C8, int HALF>
-__global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int* col, const int* colors,
+__global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, VRange V, const int* col, const int* colors,
                                                              const unsigned char* c8, const int* nlow, ull* unc_out,
                                                              ull* conf_out) {
     __shared__ TileLdsV S;
-    const long long nt = T.ntiles, ns = nseg_of(T);
+    const long long nt = V.t1 - V.t0, ns = V.s1 - V.s0;
     ull unc = 0, conf = 0;
-    for (long long it = blockIdx.x; it < nt + ns; it += gridDim.x) {
-        if (it < nt) {
+    for (long long q = blockIdx.x; q < nt + ns; q += gridDim.x) {
+        if (q < nt) {
+            const long long it = V.t0 + q;
             int r0, NE;
             long long eb;
             bool hl;
@@ -555,7 +563,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
                 const int cv = colors[r0 + i];
                 S.key[i] = (unsigned)cv;
                 if (HALF) S.nl[i] = nlow[r0 + i];
-                unc += cv == -1;
+                unc += cv == -1 && r0 + i >= V.lo && r0 + i < V.hi;
             }
             for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = col[eb + i];
             __syncthreads();
@@ -564,7 +572,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
             bool on[GC_PER];  // entries whose colour is gathered
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {
-                on[k] = k < nv;
+                on[k] = k < nv && r0 + rk[k] >= V.lo && r0 + rk[k] < V.hi;
                 if (HALF && on[k]) {
                     const int j = threadIdx.x * GC_PER + k;  // thread_entries' entry j0 + k
                     conf += u[k] == r0 + rk[k] ? 1 : 0;     // a self-loop
@@ -585,8 +593,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_validate_tiles(Tiles T, const int*
             }
             conf += HALF ? 2 * lc : lc;
         } else {
-            const long long s = it - nt;
+            const long long s = V.s0 + (q - nt);
             const int v = T.seg_row[s], j = T.seg_j[s];
+            if (v < V.lo || v >= V.hi) continue;  // (uniform per workgroup: no barrier skipped)
             const long long rs = T.rp[v], d = T.rp[v + 1] - rs;
             const long long e0 = rs + (long long)j * GC_SEG;
             const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
@@ -761,9 +770,10 @@ int scan_ll(const long long* in, long long* out, long long count, hipStream_t s)
     void* tmp = nullptr;
     GC_HIP(gc_dmalloc(&tmp, bytes ? bytes : 1));
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, 0ll, (size_t)count, rocprim::plus<long long>(), s);
-    hipStreamSynchronize(s);  // the temporary goes back to the cache idle
+    const hipError_t se = hipStreamSynchronize(s);  // the temporary goes back to the cache idle
     gc_dfree(tmp);
     GC_HIP(e);
+    GC_HIP(se);
     return GC_OK;
 }
 
@@ -880,10 +890,31 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
     return GC_OK;
 }
 
-int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8) {
-    if (g->n == 0) return GC_OK;
+int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8, long long lo, long long hi) {
+    if (g->n == 0 || lo >= hi) return GC_OK;
     int rc = gc_build_tiling(g);
     if (rc) return rc;
+    // the tiles holding rows [lo, hi): tile t holds the rows with rp[r] + r in [t GC_TW, (t+1) GC_TW)
+    VRange V;
+    V.lo = (int)lo;
+    V.hi = (int)hi;
+    if (lo == 0 && hi == g->n) {
+        V.t0 = 0;
+        V.t1 = g->ntiles;
+    } else {
+        long long rl = 0, rh = 0;
+        GC_HIP(hipMemcpyAsync(&rl, g->rp + lo, sizeof(long long), hipMemcpyDeviceToHost, g->stream));
+        GC_HIP(hipMemcpyAsync(&rh, g->rp + hi - 1, sizeof(long long), hipMemcpyDeviceToHost, g->stream));
+        GC_HIP(hipStreamSynchronize(g->stream));
+        V.t0 = std::min<long long>((rl + lo) / GC_TW, g->ntiles);
+        V.t1 = std::min<long long>((rh + hi - 1) / GC_TW + 1, g->ntiles);
+    }
+    long long sb[2] = {0, 0};
+    GC_HIP(hipMemcpyAsync(&sb[0], g->seg_base + V.t0, sizeof(long long), hipMemcpyDeviceToHost, g->stream));
+    GC_HIP(hipMemcpyAsync(&sb[1], g->seg_base + V.t1, sizeof(long long), hipMemcpyDeviceToHost, g->stream));
+    GC_HIP(hipStreamSynchronize(g->stream));
+    V.s0 = sb[0];
+    V.s1 = sb[1];
     // symmetric graphs: the low parts only (k_validate_tiles' HALF; GC_VALIDATE_HALF=0 reads every entry)
     const bool half = (g->flags & GC_GRAPH_SYMMETRIC) && g->nlow &&
                       !(getenv("GC_VALIDATE_HALF") && atoi(getenv("GC_VALIDATE_HALF")) == 0);
@@ -893,13 +924,13 @@ int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8) {
     ull* conf = &g->ctl->conflicts;
     const int* nl = g->nlow;
     if (c8 && half)
-        hipLaunchKernelGGL((k_validate_tiles<1, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+        hipLaunchKernelGGL((k_validate_tiles<1, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, V, (const int*)g->col, colors, c8, nl, unc, conf);
     else if (c8)
-        hipLaunchKernelGGL((k_validate_tiles<1, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+        hipLaunchKernelGGL((k_validate_tiles<1, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, V, (const int*)g->col, colors, c8, nl, unc, conf);
     else if (half)
-        hipLaunchKernelGGL((k_validate_tiles<0, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+        hipLaunchKernelGGL((k_validate_tiles<0, 1>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, V, (const int*)g->col, colors, c8, nl, unc, conf);
     else
-        hipLaunchKernelGGL((k_validate_tiles<0, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, (const int*)g->col, colors, c8, nl, unc, conf);
+        hipLaunchKernelGGL((k_validate_tiles<0, 0>), dim3(grid), dim3(GC_BLOCK), 0, g->stream, T, V, (const int*)g->col, colors, c8, nl, unc, conf);
     GC_HIP(hipGetLastError());
     return GC_OK;
 }

@@ -251,7 +251,7 @@ int gc_color_speculative(gc_graph* g, const gc_options* opt, int32_t* colors_out
     const long long max_rounds = 4ll * g->n + 16;
     for (long long r = 0;; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
-        hipLaunchKernelGGL(k_spec_reset, dim3(1), dim3(64), 0, s, d, r);
+        GC_LAUNCH(k_spec_reset, dim3(1), dim3(64), 0, s, d, r);
         gcl_fsort(d, L, g->fsum, s);
         if ((rc = sync_ctl(g))) return rc;
         const long long U = (long long)h.fcnt[0];
@@ -271,8 +271,8 @@ int gc_color_speculative(gc_graph* g, const gc_options* opt, int32_t* colors_out
             fail_count = (long long)h.failcnt;
             break;
         }
-        hipLaunchKernelGGL(k_spec_resolve, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
-        hipLaunchKernelGGL(k_spec_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, g->ulist);
+        GC_LAUNCH(k_spec_resolve, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
+        GC_LAUNCH(k_spec_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, g->ulist);
         if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         if ((rc = sync_ctl(g))) return rc;
         recs.push_back(RoundRec{U, U, maxmex, (long long)h.accepted, 0, 1});

@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B,
     DevCtl* c = g.ctl;
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
     const long long steps = (cnt + GC_WAVE - 1) / GC_WAVE;
@@ -188,7 +188,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
     const int* __restrict__ list = B.l[2][rs];
     const long long cnt = b_count(c, 2, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const int vpw = gc_vpw(cnt, (long long)nblk * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)bid * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -370,7 +370,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
     const int* __restrict__ list = B.l[0][rs];
     const long long cnt = b_count(c, 0, rs);
     const unsigned char* __restrict__ k8 = g.k8;
-    GcStage st{s_stage[w], 0, g.n, &g.ctl->loop_err}, est{s_estage[w], 0, g.n, &g.ctl->loop_err};
+    GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt}, est{s_estage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
     const int vpw = gc_vpw(cnt, (long long)nblk * GC_WAVES_PER_BLOCK);
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)bid * GC_WAVES_PER_BLOCK + w; ch < nch;
@@ -892,7 +892,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     for (long long r = 0;; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
         kt.begin(GC_K_OTHER);
-        hipLaunchKernelGGL(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
+        GC_LAUNCH(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
         gcl_fsort(d, L, g->fsum, s);
         gcl_pack_c4(d, s);
         kt.begin(GC_K_PROPOSE);
@@ -900,25 +900,30 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         gcl_propose_block(d, L, s);
         if (h.kbound == 0) {
             if ((rc = R.zero(&g->ctl->failcnt))) return rc;
-            hipLaunchKernelGGL(k_b_fail0, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
+            GC_LAUNCH(k_b_fail0, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
         }
         // the fold's passes over the work lists until no vertex is undecided and every
         // admitted vertex's eviction time is final
         kt.begin(GC_K_RESOLVE);
-        hipLaunchKernelGGL(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
+        GC_LAUNCH(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
         long long passes = 0;
         auto enqueue_passes = [&](long long k) {
             for (long long j = 0; j < k; ++j, ++passes) {
                 const int pi = (int)(passes % 3);  // slot arithmetic only needs the pass mod 3
-                hipLaunchKernelGGL(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
-                hipLaunchKernelGGL(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
+                GC_LAUNCH(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+                GC_LAUNCH(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
             }
         };
-        auto synced = [&]() { return R.sync(); };
+        // an open timing run never spans a host wait (the resolve class took every
+        // round's synchronisation and host decision time)
+        auto synced = [&]() {
+            kt.close();
+            return R.sync();
+        };
         if (b_async_grid > 0) {  // the first passes on the full grid, then the rest as one asynchronous launch
             enqueue_passes(b_async_k);
             GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
-            hipLaunchKernelGGL(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3),
+            GC_LAUNCH(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3),
                                b_async_budget);
             ++passes;
         } else {
@@ -929,13 +934,13 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             recs.push_back(RoundRec{prevU, prevU, prev_maxmex, (long long)h.dcnt, 0, prev_passes});
             sweeps_total += prev_passes;
         }
+        if (h.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
+        if (h.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
         const long long U = (long long)h.fcnt[0];
         if (U == 0) {  // coloring_optimized.py: no uncoloured vertex left
             recs.push_back(RoundRec{0, 0, -1, 0, 0, 0});
             break;
         }
-        if (h.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
-        if (h.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
         const long long maxmex = h.maxmex;
         if (h.kbound >= 0 && h.failcnt > 0) {  // state at the round start is returned
             recs.push_back(RoundRec{U, U, maxmex, 0, 0, 0});
@@ -953,7 +958,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if ((rc = synced())) return rc;
         }
         kt.begin(GC_K_COMMIT);
-        hipLaunchKernelGGL(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
+        GC_LAUNCH(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
         if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         prev_passes = passes;
         prevU = U;
@@ -976,6 +981,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         st->max_color = h.maxcolor;
         st->jp_sweeps = sweeps_total;
         st->async_aborts = (int64_t)h.async_aborts;
+        st->hubs = R.d.hbits_w ? (int64_t)g->nhub : 0;
         st->fail_round = fail_round;
         st->fail_count = fail_count;
         for (long long i = 0; i < (long long)recs.size() && i < st->round_cap; ++i) {

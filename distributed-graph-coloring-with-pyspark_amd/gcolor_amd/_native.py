@@ -27,7 +27,7 @@ KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "va
 
 # Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
 EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
-           "gc_graph_destroy", "gc_graph_info", "gc_graph_device", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate",
+           "gc_graph_destroy", "gc_graph_info", "gc_graph_device", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate", "gc_validate_range",
            "gc_gen_uniform", "gc_last_error", "gc_release_cache", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
            "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors", "gc_shard_set_stream",
@@ -65,7 +65,7 @@ class GcStats(ctypes.Structure):
                 ("k_bytes", ctypes.c_double * GC_NKERNELS),
                 ("round_cap", ctypes.c_int64), ("round_U", _I64P), ("round_F", _I64P),
                 ("round_maxmex", _I64P), ("round_accepted", _I64P), ("round_seeds", _I64P),
-                ("async_aborts", ctypes.c_int64)]
+                ("async_aborts", ctypes.c_int64), ("hubs", ctypes.c_int64)]
 
 
 class GcolorError(RuntimeError):
@@ -107,6 +107,7 @@ def load():
         "gc_color_resume": ([P, ctypes.POINTER(GcOptions), P, P, P, I64, I64, P, P, ctypes.POINTER(GcStats)],
                             ctypes.c_int),
         "gc_validate": ([P, P, _I64P, _I64P], ctypes.c_int),
+        "gc_validate_range": ([P, P, I64, I64, _I64P, _I64P], ctypes.c_int),
         "gc_gen_uniform": ([I64, I32, U64, P, P, I64, _I64P], ctypes.c_int),
         "gc_last_error": ([], ctypes.c_char_p),
         "gc_release_cache": ([], ctypes.c_int),

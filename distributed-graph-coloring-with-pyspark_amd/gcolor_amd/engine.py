@@ -51,6 +51,7 @@ class ColorResult:
     device_ms: float
     kernels: dict = field(default_factory=dict)
     async_aborts: int = 0  # asynchronous JP launches that handed their rest to host sweeps (0 expected)
+    hubs: int = 0  # vertices with pushed hub state (0: no hub, or the hub index did not fit)
 
     @property
     def ok(self):
@@ -231,16 +232,31 @@ class DeviceGraph:
                            round_seeds=rb["seeds"][:r].copy() if want_rounds else None,
                            fail_round=st.fail_round, fail_count=st.fail_count, reseeds=st.reseeds,
                            max_color=st.max_color, jp_sweeps=st.jp_sweeps, device_ms=st.device_ms,
-                           kernels=kernels, async_aborts=int(st.async_aborts))
+                           kernels=kernels, async_aborts=int(st.async_aborts), hubs=int(st.hubs))
 
-    def validate(self, colors=None):
+    def validate(self, colors=None, lo=None, hi=None):
         """validate_graph_coloring counts on the device (coloring.py:149-162): (#uncoloured,
         #conflicting listed pairs).
-        ``colors=None`` validates the last colouring still resident on the device."""
+        ``colors=None`` validates the last colouring still resident on the device.  ``lo`` /
+        ``hi``: the counts of the rows of vertices [lo, hi) only (gc_validate_range; disjoint
+        ranges covering the graph add up to the whole graph's counts)."""
         u, c = ctypes.c_int64(), ctypes.c_int64()
         arr = None if colors is None else np.ascontiguousarray(colors, dtype=np.int32)
-        nat.check("gc_validate", self._lib.gc_validate(self._h, _ptr(arr), ctypes.byref(u), ctypes.byref(c)))
+        if lo is None and hi is None:
+            nat.check("gc_validate", self._lib.gc_validate(self._h, _ptr(arr), ctypes.byref(u), ctypes.byref(c)))
+        else:
+            lo = 0 if lo is None else int(lo)
+            hi = self.n if hi is None else int(hi)
+            nat.check("gc_validate_range", self._lib.gc_validate_range(self._h, _ptr(arr), lo, hi, ctypes.byref(u),
+                                                                       ctypes.byref(c)))
         return u.value, c.value
+
+
+def release_cache():
+    """Give the library's parked device blocks back to the runtime (gc_release_cache).  The
+    allocator keeps freed blocks for the next graph of the same size (up to half the device's
+    memory); call this before handing a large share of HBM to another allocator (torch)."""
+    nat.check("gc_release_cache", nat.load().gc_release_cache())
 
 
 def _timing_mask(kernel_timing):

@@ -136,6 +136,9 @@ typedef struct gc_stats {
     /* outputs (continued) */
     int64_t async_aborts;  /* asynchronous JP launches that handed their rest to host
                               sweeps at their time budget (diagnostic; 0 expected)        */
+    int64_t hubs;          /* vertices with pushed hub state (forbidden-colour bitmaps) in
+                              this colouring; 0 when none is above the hub threshold or the
+                              hub index did not fit (then gc_color printed a warning)      */
 } gc_stats;
 
 /* Colour the graph.  colors_out (host int32[n], may be NULL): final state, -1 =
@@ -162,6 +165,15 @@ int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t* colors_de
    coloring.py:157-158).  colors == NULL validates the device result of the last
    gc_color on this handle without a host round trip.                                 */
 int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts);
+
+/* The same counts over the rows of vertices [lo, hi) only: every uncoloured vertex of the
+   range and every conflicting listed pair (v, u) with v in the range.  Disjoint ranges that
+   cover [0, n) add up to gc_validate's counts, so ranks that each hold the colouring split
+   validate_graph_coloring (coloring.py:149-162) by vertex range and sum the two counts (the
+   multi-GPU bench step: one all-reduce).  On a graph created GC_GRAPH_SYMMETRIC the pair
+   (v, u) is counted from the row of its lower-rank end (twice), as gc_validate does.        */
+int gc_validate_range(gc_graph* g, const int32_t* colors, int64_t lo, int64_t hi, int64_t* uncolored,
+                      int64_t* conflicts);
 
 /* ---- multi-GPU shards ------------------------------------------------ */
 /* One rank's share of a colouring on the graph g (every rank holds the whole CSR): the

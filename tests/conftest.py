@@ -65,6 +65,17 @@ def fixture_csr(rec):
     return ids, adj, rp, col
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _release_device_cache():
+    """After each test module, the library's parked device blocks go back to the runtime (the
+    allocator keeps up to half of HBM for the next graph of the same size; the next module may
+    need that memory for torch tensors).  Only if the module loaded the library."""
+    yield
+    mod = sys.modules.get("gcolor_amd._native")
+    if mod is not None and getattr(mod, "_lib", None) is not None:
+        mod._lib.gc_release_cache()
+
+
 @pytest.fixture(scope="session")
 def golden():
     return load_golden

@@ -49,3 +49,32 @@ def test_replica_workload():
     assert r3["scale"] == 24 and r3["seed"] == w["seed"] + 3 and "8 independent colourings" in r3["desc"]
     assert bench.replica_workload(bench.WORKLOADS["mesh512"], 4, 2)["dims"] == (512, 512, 512)
     assert w["seed"] == 1  # the table is not modified
+
+
+def test_bench_rejects_mismatched_world():
+    """Under a launcher, --gpus must equal the ranks started (the flag was ignored and
+    an un-launched N > 1 run printed n_gpus 1).  Checked before anything touches a GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), "--gpus", "2"], cwd=bench.REPO, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_spawn_ranks_command(monkeypatch):
+    """`bench.py --gpus N` without WORLD_SIZE starts torch.distributed.run with N ranks on
+    127.0.0.1 as a child process (never an exec) and returns its status."""
+    import subprocess
+    seen = {}
+
+    def fake_call(cmd):
+        seen["cmd"] = cmd
+        return 7
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    assert bench.spawn_ranks(4) == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == [os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "3"][-4:]

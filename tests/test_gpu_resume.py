@@ -268,3 +268,100 @@ def test_validate_symmetric_half(monkeypatch, half):
         for palette in (3, 400):
             c = rng.integers(-1, palette, n).astype(np.int32)
             assert tuple(dg.validate(c)) == tuple(oracle.c_validate(rp, col, c))
+
+
+def _sym_multigraph(seed, n=6000):
+    """The multigraph of test_validate_symmetric_half: duplicates, self-loops, a > 3000-entry row."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, n, 40000)
+    b = rng.integers(0, n, 40000)
+    a = np.concatenate([a, np.zeros(3000, np.int64), a[:500]])
+    b = np.concatenate([b, rng.integers(1, n, 3000), b[:500]])
+    keep = a != b
+    src = np.concatenate([a[keep], b[keep], np.arange(0, n, 97)])
+    dst = np.concatenate([b[keep], a[keep], np.arange(0, n, 97)])
+    order = np.lexsort((dst, src))
+    src, dst = src[order], dst[order]
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, src + 1, 1)
+    return np.cumsum(rp), dst.astype(np.int32)
+
+
+def _range_counts(rp, col, colors, lo, hi, half):
+    """gc_validate_range's counts restated in numpy: rows [lo, hi) of the directed count
+    (coloring.py:149-162), or -- symmetric graphs, low parts only -- 2 x the conflicts of the
+    rows' lower-rank entries (rank (deg, pos), coloring.py:64) + their self-loop entries."""
+    n = len(rp) - 1
+    deg = np.diff(rp)
+    e0, e1 = int(rp[lo]), int(rp[hi])
+    rows = np.repeat(np.arange(lo, hi), deg[lo:hi])
+    u = col[e0:e1].astype(np.int64)
+    same = colors[u] == colors[rows]
+    unc = int(np.count_nonzero(colors[lo:hi] == -1))
+    if not half:
+        return unc, int(np.count_nonzero(same))
+    key = deg.astype(np.int64) * n + np.arange(n)
+    low = key[u] < key[rows]
+    return unc, int(2 * np.count_nonzero(same & low) + np.count_nonzero(u == rows))
+
+
+@pytest.mark.parametrize("half", ["1", "0"], ids=["low_parts", "every_entry"])
+def test_validate_range(monkeypatch, half):
+    """gc_validate_range (the multi-GPU step's split of validate_graph_coloring, coloring.py:149-162):
+    each range's counts equal the numpy restatement of the rows it holds -- ranges cut inside tiles,
+    around the segmented > 3000-entry row of vertex 0, single vertices, empty -- and any cover of
+    [0, n) by disjoint ranges adds up to the oracle's counts, for the resident colouring and for
+    arbitrary colour arrays."""
+    from gcolor_amd.engine import DeviceGraph
+    monkeypatch.setenv("GC_VALIDATE_HALF", half)
+    rp, col = _sym_multigraph(12)
+    n = len(rp) - 1
+    rng = np.random.default_rng(5)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        g = dg.color("A")
+        arrays = [None, rng.integers(-1, 3, n).astype(np.int32), rng.integers(-1, 400, n).astype(np.int32)]
+        for c in arrays:
+            cc = g.colors if c is None else c
+            full = oracle.c_validate(rp, col, cc)
+            for cuts in ([0, 1, n], [0, 2, 3, 4000, n], sorted(set([0, n] + list(rng.integers(0, n, 7)))), [0, n // 2, n]):
+                tot = np.zeros(2, np.int64)
+                for lo, hi in zip(cuts[:-1], cuts[1:]):
+                    got = dg.validate(c, lo=lo, hi=hi)
+                    assert tuple(got) == _range_counts(rp, col, cc, lo, hi, half == "1"), (lo, hi)
+                    tot += got
+                assert tuple(tot) == tuple(full)
+            assert dg.validate(c, lo=17, hi=17) == (0, 0)
+        with pytest.raises(Exception):
+            dg.validate(None, lo=-1, hi=5)
+        with pytest.raises(Exception):
+            dg.validate(None, lo=5, hi=n + 1)
+
+
+@pytest.mark.parametrize("variant", ["A", "B"])
+def test_list_overflow_reported_and_halted(monkeypatch, variant):
+    """A staged list append that would pass its list's capacity writes nothing, halts the
+    pipeline (every later kernel returns at once instead of reading the list up to the
+    overflowed count) and comes back as GC_EHIP -- not a fault.  The capacity is
+    lowered to 16 entries (GC_TEST_LIST_CAP; the buffers keep n entries, so a kernel that read
+    past the logical end would still stay inside them); afterwards the same handle colours the
+    graph exactly again."""
+    from gcolor_amd import _native as nat
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    rp, col = uniform_csr(200_000, 16, 3)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        ref = dg.color(variant)
+        monkeypatch.setenv("GC_TEST_LIST_CAP", "16")
+        with pytest.raises(nat.GcolorError) as ei:
+            dg.color(variant)
+        assert ei.value.status == nat.GC_EHIP and "capacity" in str(ei.value)
+        monkeypatch.delenv("GC_TEST_LIST_CAP")
+        again = dg.color(variant)
+        assert np.array_equal(again.colors, ref.colors) and list(again.round_U) == list(ref.round_U)
+    with DeviceGraph.rmat(16, 16, seed=2) as dg:  # hubs: the asynchronous JP / fold paths
+        ref = dg.color(variant)
+        monkeypatch.setenv("GC_TEST_LIST_CAP", "16")
+        with pytest.raises(nat.GcolorError) as ei:
+            dg.color(variant)
+        assert ei.value.status == nat.GC_EHIP
+        monkeypatch.delenv("GC_TEST_LIST_CAP")
+        assert np.array_equal(dg.color(variant).colors, ref.colors)

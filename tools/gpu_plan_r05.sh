@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5's GPU sessions, one gpurun call each (<= 1200 s):
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_plan_r05.sh a
+#   a: FETCH_SIZE / WRITE_SIZE per op of the engine's access patterns, then
+#      C5's one-GPU step with the colouring's set-up phases and every large hipMalloc / hipFree
+#      timed (~1.36 s of R-MAT-28's step is outside the rounds), R-MAT-26 beside it
+set -uo pipefail
+cd "$(dirname "$0")/.."
+case ${1:-} in
+  a) exec_steps=(calib env:GC_PREP_TIMING=1 env:GC_ALLOC_TRACE=1 step:rmat28 step:rmat26 env:GC_PREP_TIMING= env:GC_ALLOC_TRACE=) ;;
+  # b: the allocator's idle cap at half of HBM (no ~3 s hipMalloc stall after a step's frees), the
+  #    range validation, the stage-overflow halt, exact launch counts, the RCCL one-rank group and
+  #    bench.py --gpus 2 (new tests first), every GPU test, smoke, C5's step and the default line
+  b) exec_steps=("file:tests/test_gpu_resume.py:validate_range~or~list_overflow"
+                 "file:tests/test_shard_gpu.py:one_rank_rccl" file:tests/test_bench_gpu.py tests smoke
+                 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
+                 bench:rmat24) ;;
+  *) echo "usage: $0 a|b" >&2; exit 2 ;;
+esac
+bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"

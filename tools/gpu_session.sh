@@ -81,6 +81,15 @@ for st in "$@"; do
       nm=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       hipcc --offload-arch=gfx950 -O3 "tools/ubench/$nm.hip" -o "$O/$nm" > "$log" 2>&1 &&
         timeout -k 10 120 "$O/$nm" ${a//,/ } >> "$log" 2>&1 ;;
+    calib)
+      # FETCH_SIZE / WRITE_SIZE per op of the engine's access patterns (tools/ubench/gather_bytes.hip)
+      C=$O/calib
+      mkdir -p "$C"
+      hipcc --offload-arch=gfx950 -O3 tools/ubench/gather_bytes.hip -o "$C/gather_bytes" > "$log" 2>&1 &&
+        timeout -k 10 120 "$C/gather_bytes" 5 > "$C/timing.txt" 2>> "$log" &&
+        ( cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$C/pmc_fetch" -o run -- "$C/gather_bytes" 5 ) >> "$log" 2>&1 &&
+        ( cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$C/pmc_write" -o run -- "$C/gather_bytes" 5 ) >> "$log" 2>&1 &&
+        python tools/ubench_pmc.py "$C" > "$C/calibration.json" 2>> "$log" && cat "$C/timing.txt" "$C/calibration.json" >> "$log" ;;
     rounds)
       mkdir -p "$O/rounds_$rest"
       ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/rounds_$rest" -o run -- \
