@@ -2615,6 +2615,7 @@ __global__ void k_shard_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
     if (c->halt == GC_H_SWEEPS) return;  // the last finish halted: everything stays for gc_shard_resume_hubs
+    if (c->loop_err == GC_LERR_LIST) return;  // a list overflowed: stay halted (shard_sync reports it)
     if (c->acc_round != round + 1) {  // a repeated seam (after a hub halt) keeps the first reset's count:
         c->acc_last = (long long)c->accepted;  // `accepted` was zeroed by it
         c->acc_round = round + 1;

@@ -52,7 +52,9 @@ __device__ __forceinline__ bool b_same(const GDev& g, int u, unsigned ku, unsign
 __global__ void k_b_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
-    c->halt = GC_RUN;
+    // a list append overflowed (gc_stage_fits): stay halted -- every fold kernel returns at
+    // once -- until the host's next wait reports it
+    c->halt = c->loop_err == GC_LERR_LIST ? GC_H_STALLED : GC_RUN;
     c->round = round;
     c->cur = 0;
     c->fcnt[0] = 0;
@@ -73,6 +75,7 @@ __global__ void k_b_reset(GDev g, long long round) {
 // (coloring_optimized.py:159-164); k_propose counted every proposer.
 __global__ void __launch_bounds__(GC_BLOCK) k_b_fail0(GDev g, GLists L) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     const long long cnt = (long long)c->fcnt[c->cur];
     const int* list = L.F[c->cur];
@@ -144,6 +147,7 @@ __device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl,
 // entries; eviction times unknown (-1).
 __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B, int* ev, const int* neq) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;  // a list overflowed (k_b_reset keeps the halt)
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     const int w = threadIdx.x / GC_WAVE;
     GcStage st{s_stage[w], 0, g.list_cap, &g.ctl->loop_err, &g.ctl->halt};
@@ -260,6 +264,7 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_b_ev(GDev g, BLists B, int* ev, int pass) {
+    if (g.ctl->halt) return;
     b_ev_pass(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
@@ -429,6 +434,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
 }
 
 __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int* ev, int pass) {
+    if (g.ctl->halt) return;
     b_adm_pass(g, B, ev, pass, blockIdx.x, gridDim.x);
 }
 
@@ -445,6 +451,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
 // bitmaps, pushed into the hubs listing them (gc_hub_push_wave)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev, int* big) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -708,6 +715,7 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
 // waves' scratch and clears that slot's counts (as k_b_ev does)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev, int pass, long long budget) {
     DevCtl* c = g.ctl;
+    if (c->halt) return;
     const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
     __shared__ BAsyncLds s_w[GC_WAVES_PER_BLOCK];
     const int lane = gc_lane();
