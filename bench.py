@@ -155,10 +155,11 @@ def pmc_summary(workload, variant):
     return per, os.path.relpath(p, REPO)
 
 
-def pmc_class_bytes(workload, variant):
+def pmc_class_bytes(workload, variant, key="hbm_bytes_per_launch"):
     """Per class: HBM bytes per launch of the class (FETCH_SIZE + WRITE_SIZE, KiB x 1024,
     summed over the class's kernels and divided by their launches) from the rocprofv3
-    --pmc passes of this bench command (tools/gpu_profile.sh -> tools/pmc_summary.py)."""
+    --pmc passes of this bench command (tools/gpu_profile.sh -> tools/pmc_summary.py);
+    key="hbm_bytes_per_launch_calibrated": 2 x FETCH_SIZE + WRITE_SIZE (calibration())."""
     per, src = pmc_summary(workload, variant)
     if per is None:
         return {}, src
@@ -167,12 +168,31 @@ def pmc_class_bytes(workload, variant):
         b = l = 0.0
         for k in names:
             e = per.get(k)
-            if e and "hbm_bytes_per_launch" in e:
-                b += e["hbm_bytes_per_launch"] * e["launches"]
+            if e and key in e:
+                b += e[key] * e["launches"]
                 l += e["launches"]
         if l:
             out[cls] = b / l
     return out, src
+
+
+def calibration():
+    """What rocprofv3's counters mean for this path's access patterns, measured on the box
+    (tools/ubench/gather_bytes.hip -> profiles/calib/gather_bytes.json): FETCH_SIZE counts
+    half of every line read -- 1/2 of a streaming read's bytes, 64 B per random 1-4 B gather
+    whose line is 128 B -- and random 4-B gathers past the caches top out at `gather_Gops`
+    (x 128 B: the HBM's achievable rate).  Calibrated HBM bytes = 2 x FETCH + WRITE."""
+    p = os.path.join(REPO, "profiles", "calib", "gather_bytes.json")
+    if not os.path.exists(p):
+        return None
+    c = json.load(open(p))
+    g = c["k_gather4_big"]
+    return {"source": os.path.relpath(p, REPO),
+            "fetch_counted_over_streamed_bytes": c["k_stream_read16"]["fetch_over_named"],
+            "fetch_counted_per_random_gather_B": g["fetch_bytes_per_op"],
+            "write_counted_per_random_store_B": c["k_scatter4_big"]["write_bytes_per_op"],
+            "gather_Gops": g["ops_per_s"] / 1e9,
+            "gather_ceiling_GBps": g["ops_per_s"] * 2 * g["fetch_bytes_per_op"] / 1e9}
 
 
 def cpu_baseline(w, host_csr, colors_gpu):
@@ -352,13 +372,18 @@ def capped_alg(kern, n, nnz):
 def pmc_step_frac(workload, variant, t):
     """Physical fraction of the whole step: rocprofv3 FETCH_SIZE + WRITE_SIZE of every kernel
     of the timed steps (profiles/pmc/<workload>.json "_step", a --selected-regions run of this
-    bench command) / t / peak."""
+    bench command) / t / peak -- as counted, and calibrated (2 x FETCH + WRITE, calibration())."""
     per, src = pmc_summary(workload, variant)
     st = per.get("_step") if per else None
     if not st or not st.get("steps"):
         return None
     b = st["bytes"] / st["steps"]
-    return {"bytes_per_step": b, "GBps": b / t / 1e9, "frac": b / t / 1e9 / HBM_PEAK_GBS, "source": src}
+    out = {"bytes_per_step": b, "GBps": b / t / 1e9, "frac": b / t / 1e9 / HBM_PEAK_GBS, "source": src}
+    if "fetch_bytes" in st:
+        bc = (2 * st["fetch_bytes"] + st["write_bytes"]) / st["steps"]
+        out.update({"bytes_per_step_calibrated": bc, "GBps_calibrated": bc / t / 1e9,
+                    "frac_calibrated": bc / t / 1e9 / HBM_PEAK_GBS})
+    return out
 
 
 def north_star(torch, barrier, args):
@@ -382,8 +407,33 @@ def north_star(torch, barrier, args):
            "algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
            "algorithmic_frac_capped": capped_alg(probe.kernels, S.n, S.nnz) / t / 1e9 / HBM_PEAK_GBS,
            "classes_probe_step": class_table(probe.kernels, pmc_class_bytes("rmat26", "A")[0]),
-           "pmc_frac": pmc_step_frac("rmat26", "A", t)}
+           # the physical figures: every kernel's bytes of a step (as counted, and calibrated:
+           # 2 x FETCH + WRITE) / t / peak, and the dominant class on the calibrated basis
+           "pmc_frac": pmc_step_frac("rmat26", "A", t),
+           "roofline_calibrated": calibrated_roofline("rmat26", "A", probe.kernels)}
     S.close()
+    return out
+
+
+def calibrated_roofline(workload, variant, kern):
+    """The dominant class (by event-timed time) on the calibrated physical basis: 2 x FETCH_SIZE
+    + WRITE_SIZE per launch (calibration()) / the class's average launch time, against the HBM
+    peak and against the measured random-gather ceiling (what a gather-bound kernel can reach)."""
+    cal = calibration()
+    pmc_c, src = pmc_class_bytes(workload, variant, "hbm_bytes_per_launch_calibrated")
+    timed = {k: v for k, v in kern.items() if v["launches"] and v["ms"] > 0}
+    if not cal or not timed:
+        return None
+    cls = max(timed, key=lambda k: timed[k]["ms"])
+    v = timed[cls]
+    avg_ms = v["ms"] / v["launches"]
+    out = {"kernel": cls, "kernels": CLASS_KERNELS.get(cls), "avg_launch_ms": avg_ms, "launches_per_step": v["launches"],
+           "peak": HBM_PEAK_GBS, "gather_ceiling": cal["gather_ceiling_GBps"], "unit": "GB/s",
+           "basis": "2 x FETCH_SIZE + WRITE_SIZE per launch (profiles/calib/gather_bytes.json)", "source": src}
+    if cls in pmc_c:
+        a = pmc_c[cls] / (avg_ms / 1e3) / 1e9
+        out.update({"traffic": pmc_c[cls], "achieved": a, "frac": a / HBM_PEAK_GBS,
+                    "frac_of_gather_ceiling": a / cal["gather_ceiling_GBps"]})
     return out
 
 
@@ -789,6 +839,13 @@ def main():
                  " and no rocprofv3 summary of this build (profiles/pmc)")
         achieved = None
     balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
+    cal_roof = None
+    pmc_c, _ = pmc_class_bytes(args.workload, V, "hbm_bytes_per_launch_calibrated")
+    cal = calibration()
+    if cal and dom_class in pmc_c and dom["ms"] > 0:
+        a = pmc_c[dom_class] / (avg_ms / 1e3) / 1e9
+        cal_roof = {"achieved": a, "frac": a / HBM_PEAK_GBS, "traffic": pmc_c[dom_class],
+                    "gather_ceiling": cal["gather_ceiling_GBps"], "frac_of_gather_ceiling": a / cal["gather_ceiling_GBps"]}
 
     if rank != 0:
         if dist is not None:
@@ -884,7 +941,11 @@ def main():
                      "algorithmic_bytes_per_launch": alg_per_launch, "avg_launch_ms": avg_ms,
                      "launches_per_step": dom["launches"],
                      "share_of_step": dom["ms"] / (t_ev * 1e3) if t_ev else None,
-                     "event_pass_ms_per_step": t_ev and t_ev * 1e3},
+                     "event_pass_ms_per_step": t_ev and t_ev * 1e3,
+                     # the same class on the calibrated basis (2 x FETCH + WRITE: FETCH_SIZE counts
+                     # half of every line read, profiles/calib/gather_bytes.json)
+                     "calibrated": cal_roof},
+        "calibration": calibration(),
         "classes_probe_step": classes,
         # whole job, §8d algorithmic bytes / t: a work-efficiency ratio against the peak, NOT
         # bandwidth (hub bitmaps skip row reads §8d credits); the capped figure credits no class

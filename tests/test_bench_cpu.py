@@ -78,3 +78,28 @@ def test_spawn_ranks_command(monkeypatch):
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == [os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "3"][-4:]
+
+
+def test_calibrated_fractions(tmp_path, monkeypatch):
+    """The calibrated physical basis (2 x FETCH_SIZE + WRITE_SIZE: FETCH_SIZE counts half of
+    every line read, profiles/calib/gather_bytes.json) in the step fraction and the dominant
+    class's roofline; the calibration itself is the committed measurement."""
+    cal = bench.calibration()
+    assert cal and cal["fetch_counted_over_streamed_bytes"] == 0.5
+    assert 60 <= cal["fetch_counted_per_random_gather_B"] <= 68 and cal["gather_Gops"] > 10
+    calib_src = os.path.join(bench.REPO, "profiles", "calib", "gather_bytes.json")
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    os.makedirs(tmp_path / "profiles" / "pmc")
+    os.makedirs(tmp_path / "profiles" / "calib")
+    (tmp_path / "profiles" / "calib" / "gather_bytes.json").write_text(open(calib_src).read())
+    monkeypatch.setattr(bench, "lib_sha16", lambda: "abc")
+    per = {"k_sweep_async": {"launches": 4, "hbm_bytes_per_launch": 3e6, "hbm_bytes_per_launch_calibrated": 5e6},
+           "_step": {"steps": 1, "bytes": 3e9, "fetch_bytes": 2e9, "write_bytes": 1e9}, "_build": "abc"}
+    (tmp_path / "profiles" / "pmc" / "rmat26.json").write_text(json.dumps(per))
+    f = bench.pmc_step_frac("rmat26", "A", 1.0)
+    assert f["bytes_per_step_calibrated"] == 5e9 and abs(f["frac_calibrated"] - 5.0 / bench.HBM_PEAK_GBS) < 1e-12
+    kern = {"sweep": {"ms": 2.0, "launches": 4, "bytes": 0.0}, "propose": {"ms": 1.0, "launches": 4, "bytes": 1.0}}
+    r = bench.calibrated_roofline("rmat26", "A", kern)
+    assert r["kernel"] == "sweep" and r["traffic"] == 5e6
+    assert abs(r["achieved"] - 5e6 / 0.5e-3 / 1e9) < 1e-9
+    assert abs(r["frac_of_gather_ceiling"] - r["achieved"] / cal["gather_ceiling_GBps"]) < 1e-12

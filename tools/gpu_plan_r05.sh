@@ -15,6 +15,10 @@ case ${1:-} in
                  "file:tests/test_shard_gpu.py:one_rank_rccl" file:tests/test_bench_gpu.py tests smoke
                  "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
                  bench:rmat24) ;;
-  *) echo "usage: $0 a|b" >&2; exit 2 ;;
+  # c: the numpy replica of the device R-MAT generator (the full-size fixtures are built from it)
+  #    against the device graph; the floor of a small round: six kernel launches against one
+  #    resident launch confined to one XCD, or spanning the device (tools/ubench/round_floor.hip)
+  c) exec_steps=("py:tools/check_rmat_replica.py:12,16,20" ubench:round_floor:200) ;;
+  *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"

@@ -5,10 +5,17 @@
 
 Per kernel name: launches, average duration (kernel trace), and FETCH_SIZE / WRITE_SIZE
 per launch from the two separate --pmc passes.  Units: rocprofv3 reports both counters in
-KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a 16-B-per-lane coalesced streaming
-read (MI355X_MICROARCH.md §HBM); the gathers here are 1-8 B per lane and uncalibrated, so
-the bytes are reported as counted (x1024), with the x2 streaming-read correction given
-separately as an upper bound.
+KiB; the bytes are given as counted (x1024) and calibrated.
+
+Calibration (round 5, tools/ubench/gather_bytes.hip, profiles/calib/gather_bytes.json):
+  * streaming reads, 16 B and 4 B per lane: FETCH_SIZE = 1/2 of the bytes read (as
+    MI355X_MICROARCH.md states for 16 B);
+  * random 1-B and 4-B gathers past the caches: FETCH_SIZE = 64 B per gather, at a measured
+    ceiling of 49.7 G gathers/s -- x2 (the 128-B line the L2 requests) is 6.36 TB/s, the
+    HBM's achievable rate, so x2 is the physical reading there too;
+  * streaming stores: WRITE_SIZE exact; random 1-B / 4-B stores and 32-bit atomics:
+    WRITE_SIZE = 32 B per store (the write granule), counted as moved.
+So the calibrated HBM bytes of a kernel are 2 x FETCH_SIZE + WRITE_SIZE.
 """
 import collections
 import csv
@@ -57,12 +64,15 @@ def main(d, steps=None):
             e["write_bytes_per_launch"] = v * 1024 / c
         if "fetch_bytes_per_launch" in e and "write_bytes_per_launch" in e:
             e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
+            # calibrated: FETCH_SIZE counts half of every read line (streams and gathers alike)
+            e["hbm_bytes_per_launch_calibrated"] = 2 * e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
         out[k] = e
     if tag == "3" and os.path.isdir(os.path.join(d, "pmc_fetch1")):
         f3, w3 = totals(d, "3")
         f1, w1 = totals(d, "1")
         fb, wb = (f3 - f1) / 2, (w3 - w1) / 2
         out["_step"] = {"steps": 1, "bytes": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
+                        "bytes_calibrated": 2 * fb + wb,
                         "note": "FETCH_SIZE + WRITE_SIZE of every kernel, (run at 3 timed steps - run at 1) / 2: "
                                 "one step, as counted (KiB x 1024)"}
     # the build the counters describe: bench.py uses a summary only for the same libgcolor.so
