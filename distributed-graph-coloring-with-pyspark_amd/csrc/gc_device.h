@@ -221,3 +221,24 @@ __device__ __forceinline__ void gc_stat_add(const GDev& g, int cls, ull lsum, ul
     }
     __syncthreads();
 }
+
+// Residency probe (budget < 0 in k_sweep_async / k_b_async: the SAME kernel, so the same
+// registers, SGPRs and LDS): lane 0 of every workgroup arrives on c->async_done[0] and waits
+// until every workgroup of the grid has arrived or ~100 us have passed; the first to leave
+// records the arrivals it saw in c->async_done[1].  Resident workgroups all start at once and
+// none leaves before the wait ends, so that record is the number that fit on the device at
+// once -- what the asynchronous kernels' static slices need (gc_resident_blocks_per_cu's
+// runtime query cannot see SGPR limits: k_b_async's 106 SGPRs allow 7 waves per SIMD where the
+// runtime answered 8).
+__device__ __forceinline__ void gc_residency_probe(DevCtl* c) {
+    if (threadIdx.x != 0) return;
+    atomicAdd(&c->async_done[0], 1ull);
+    const ull t0 = wall_clock64();
+    ull v = 0;
+    for (;;) {
+        v = __hip_atomic_load(&c->async_done[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= (ull)gridDim.x || wall_clock64() - t0 > 10000) break;  // 100 MHz: 100 us
+        __builtin_amdgcn_s_sleep(4);
+    }
+    atomicCAS(&c->async_done[1], 0ull, v);
+}

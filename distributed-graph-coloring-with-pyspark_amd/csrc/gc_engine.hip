@@ -265,9 +265,9 @@ struct Run {
         if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) != hipSuccess || rate_khz <= 0)
             return;
         int bpc = getenv("GC_ASYNC_BPC") ? atoi(getenv("GC_ASYNC_BPC")) : 2;
-        const int occ = gcl_sweep_async_blocks_per_cu();
-        bpc = std::max(1, std::min(bpc, occ - (occ > 1 ? 1 : 0)));  // the occupancy answer can be one too many
+        const int occ = gcl_sweep_async_resident(d, g->stream);  // resident workgroups per CU, measured (gc_residency_probe)
         if (occ <= 0) return;
+        bpc = std::max(1, std::min(bpc, occ));
         const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
         async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
         async_grid = cus * bpc;

@@ -28,6 +28,9 @@
 
 #include <algorithm>
 
+#include <map>
+#include <mutex>
+
 #include "gcolor.h"
 #include "gc_internal.h"
 #include "gc_launch.h"
@@ -1583,6 +1586,10 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 // profiles/r04/c: removed.)
 __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget) {
     DevCtl* c = g.ctl;
+    if (budget < 0) {  // residency probe (gcl_sweep_async_resident)
+        gc_residency_probe(c);
+        return;
+    }
     if (c->halt) return;
     __shared__ GcAsyncLds s_w[GC_WAVES_PER_BLOCK];
     const int w = threadIdx.x / GC_WAVE;
@@ -3167,10 +3174,57 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
 void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
     GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
 }
-int gcl_sweep_async_blocks_per_cu() {
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sweep_async, GC_BLOCK, 0) != hipSuccess) return 0;
-    return b;
+int gc_resident_blocks_per_cu(const void* fn, int block) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, block, 0) != hipSuccess) return 0;
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, fn) == hipSuccess && a.numRegs > 0) {
+        const int vg = (a.numRegs + 7) / 8 * 8;
+        const int waves_simd = std::min(8, 512 / vg);
+        const int waves_block = (block + GC_WAVE - 1) / GC_WAVE;
+        int by_regs = waves_simd * 4 / waves_block;  // 4 SIMDs per CU
+        if (a.sharedSizeBytes > 0) by_regs = std::min(by_regs, (int)((160u << 10) / a.sharedSizeBytes));
+        occ = std::min(occ, by_regs);
+    }
+    return occ;
+}
+int gcl_sweep_async_blocks_per_cu() { return gc_resident_blocks_per_cu((const void*)k_sweep_async, GC_BLOCK); }
+
+// Resident workgroups per CU of a kernel with a residency-probe mode, measured once per
+// device and cached (gc_residency_probe; `launch` starts the kernel in probe mode on `grid`
+// workgroups).  The control block's async_done words are used and zeroed again.
+int gc_measure_resident(const void* key, gc_graph_ctl_view v, int query, void (*launch)(const GDev&, int, hipStream_t)) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> cache;
+    int dev = 0;
+    hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({key, dev});
+        if (it != cache.end()) return it->second;
+    }
+    int cus = 0;
+    if (query <= 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return query;
+    const int grid = cus * std::min(8, query + 1);  // one more per CU than the runtime allows
+    ull r[2] = {0, 0};
+    if (hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess) return std::max(1, query - 1);
+    launch(*v.g, grid, v.s);
+    if (hipMemcpyAsync(r, v.g->ctl->async_done, sizeof(r), hipMemcpyDeviceToHost, v.s) != hipSuccess ||
+        hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess || hipStreamSynchronize(v.s) != hipSuccess)
+        return std::max(1, query - 1);
+    const int per_cu = std::max(1, std::min(query, (int)(r[1] / (ull)cus)));
+    std::lock_guard<std::mutex> lk(mu);
+    cache[{key, dev}] = per_cu;
+    return per_cu;
+}
+static void launch_sweep_async_probe(const GDev& g, int grid, hipStream_t s) {
+    GLists L{};
+    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, 0, 0, -1ll);
+}
+int gcl_sweep_async_resident(const GDev& g, hipStream_t s) {
+    return gc_measure_resident((const void*)k_sweep_async, gc_graph_ctl_view{&g, s}, gcl_sweep_async_blocks_per_cu(),
+                               launch_sweep_async_probe);
 }
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s) {
     GC_LAUNCH(k_pull, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, allow_big);

@@ -117,6 +117,24 @@ void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t
 // asynchronous JP after sweep S on a resident grid (budget in wall-clock ticks; par alternates per launch)
 void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s);
 int gcl_sweep_async_blocks_per_cu();
+// Workgroups of `block` threads of kernel `fn` that are RESIDENT on a CU at once: the
+// runtime's occupancy answer, bounded by what the kernel's own VGPR count and static LDS allow
+// (512 VGPRs per SIMD lane in granules of 8, at most 8 waves per SIMD, 160 KB of LDS per CU).
+// The runtime answered 8 for k_b_async, whose 66 VGPRs allow 7 waves per SIMD (the compiler's
+// resource-usage remark says the same): a grid sized from the runtime's answer had an eighth of
+// its workgroups wait for a CU while the resident ones spun on their slices (round 4's
+// 8-workgroups-per-CU cliff, R-MAT-24 variant B 365 ms -> 2.0 s).  Persistent and
+// asynchronous kernels size their grids from this.
+int gc_resident_blocks_per_cu(const void* fn, int block);
+// the same, measured on the device: the kernel launched in its residency-probe mode
+// (gc_residency_probe), once per device, capped by the runtime's answer
+struct gc_graph_ctl_view {
+    const GDev* g;
+    hipStream_t s;
+};
+int gc_measure_resident(const void* key, gc_graph_ctl_view v, int query, void (*launch)(const GDev&, int, hipStream_t));
+int gcl_sweep_async_resident(const GDev& g, hipStream_t s);
+int gcl_b_async_resident(const GDev& g, hipStream_t s);
 void gcl_pull(const GDev& g, int allow_big, hipStream_t s);  // pull half of a big round
 void gcl_front_build(const GDev& g, const GLists& L, unsigned* bsum, hipStream_t s);  // next list of a big round
 // tclose: the commit's last workgroup also closes the round (no k_close; ROUND mode only,

@@ -715,6 +715,10 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
 // waves' scratch and clears that slot's counts (as k_b_ev does)
 __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev, int pass, long long budget) {
     DevCtl* c = g.ctl;
+    if (budget < 0) {  // residency probe (gcl_b_async_resident)
+        gc_residency_probe(c);
+        return;
+    }
     if (c->halt) return;
     const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
     __shared__ BAsyncLds s_w[GC_WAVES_PER_BLOCK];
@@ -780,10 +784,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
 }
 
 }  // namespace
-int gcl_b_async_blocks_per_cu() {
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_b_async, GC_BLOCK, 0) != hipSuccess) return 0;
-    return b;
+int gcl_b_async_blocks_per_cu() { return gc_resident_blocks_per_cu((const void*)k_b_async, GC_BLOCK); }
+static void launch_b_async_probe(const GDev& g, int grid, hipStream_t s) {
+    BLists B{};
+    GC_LAUNCH(k_b_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, B, (int*)nullptr, 0, -1ll);
+}
+int gcl_b_async_resident(const GDev& g, hipStream_t s) {
+    return gc_measure_resident((const void*)k_b_async, gc_graph_ctl_view{&g, s}, gcl_b_async_blocks_per_cu(),
+                               launch_b_async_probe);
 }
 namespace {
 
@@ -852,7 +860,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
             rate_khz > 0) {
             const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 4;
-            b_async_grid = std::min(bpc, std::max(1, gcl_b_async_blocks_per_cu())) * cus;  // resident: every wave's slice progresses
+            // every workgroup resident (gc_resident_blocks_per_cu): the static slices all progress
+            b_async_grid = std::min(bpc, std::max(1, gcl_b_async_resident(d, s))) * cus;
             const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
             b_async_budget = std::max(0ll, us) * (long long)rate_khz / 1000;
         }

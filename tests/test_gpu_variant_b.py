@@ -260,3 +260,22 @@ def test_rmat20_variant_b_against_oracle(monkeypatch, env):
         g = dg.color("B")
         assert_same_run(g, oracle.c_color(rp, col, "B"))
         assert dg.validate() == (0, 0)
+
+
+def test_async_grids_sized_from_measured_residency(monkeypatch):
+    """The asynchronous kernels' grids (variant B's fold k_b_async, variant A's k_sweep_async)
+    are capped at the workgroups measured resident (gc_residency_probe): asking for 8 per CU --
+    round 4's cliff, when the runtime's occupancy answer (8) was one more than fit (SGPR-bound
+    7) and an eighth of the static slices waited for the 20 ms budget in every big round -- now
+    gives the same colouring with no give-up."""
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(20, 16, seed=5) as dg:
+        ref_b = dg.color("B")
+        ref_a = dg.color("A")
+        monkeypatch.setenv("GC_B_ASYNC_BPC", "8")
+        monkeypatch.setenv("GC_ASYNC_BPC", "8")
+        b = dg.color("B")
+        a = dg.color("A")
+        assert np.array_equal(b.colors, ref_b.colors) and list(b.round_U) == list(ref_b.round_U)
+        assert np.array_equal(a.colors, ref_a.colors) and list(a.round_U) == list(ref_a.round_U)
+        assert b.async_aborts == 0 and a.async_aborts == 0

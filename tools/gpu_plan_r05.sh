@@ -19,6 +19,12 @@ case ${1:-} in
   #    against the device graph; the floor of a small round: six kernel launches against one
   #    resident launch confined to one XCD, or spanning the device (tools/ubench/round_floor.hip)
   c) exec_steps=("py:tools/check_rmat_replica.py:12,16,20" ubench:round_floor:200) ;;
-  *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
+  # d: the asynchronous kernels' grids capped at the measured residency (a probe launch of the
+  #    same kernel): the variant B and hub tests, then the grid A/Bs (variant B 4 / 6 / 8 per CU,
+  #    8 now meaning the measured maximum; variant A 2 / 4 / 8)
+  d) exec_steps=("file:tests/test_gpu_variant_b.py:residency~or~rmat20" file:tests/test_gpu_hubs.py
+                 env:AB_VARIANT=B ab:rmat24:3:base,bpc6=GC_B_ASYNC_BPC:6,bpc8=GC_B_ASYNC_BPC:8 env:AB_VARIANT=
+                 ab:rmat24:4:base,bpc4=GC_ASYNC_BPC:4,bpc8=GC_ASYNC_BPC:8) ;;
+  *) echo "usage: $0 a|b|c|d" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
