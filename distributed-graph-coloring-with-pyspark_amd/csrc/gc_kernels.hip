@@ -3214,6 +3214,9 @@ int gc_measure_resident(const void* key, gc_graph_ctl_view v, int query, void (*
         hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess || hipStreamSynchronize(v.s) != hipSuccess)
         return std::max(1, query - 1);
     const int per_cu = std::max(1, std::min(query, (int)(r[1] / (ull)cus)));
+    if (getenv("GC_DEBUG"))
+        fprintf(stderr, "[gc] residency probe: %llu of %d workgroups resident at once (runtime answer %d per CU) -> %d per CU\n",
+                r[1], grid, query, per_cu);
     std::lock_guard<std::mutex> lk(mu);
     cache[{key, dev}] = per_cu;
     return per_cu;

@@ -25,6 +25,8 @@ case ${1:-} in
   d) exec_steps=("file:tests/test_gpu_variant_b.py:residency~or~rmat20" file:tests/test_gpu_hubs.py
                  env:AB_VARIANT=B ab:rmat24:3:base,bpc6=GC_B_ASYNC_BPC:6,bpc8=GC_B_ASYNC_BPC:8 env:AB_VARIANT=
                  ab:rmat24:4:base,bpc4=GC_ASYNC_BPC:4,bpc8=GC_ASYNC_BPC:8) ;;
-  *) echo "usage: $0 a|b|c|d" >&2; exit 2 ;;
+  # e: the asynchronous kernels at 2..8 workgroups per CU requested (measured residency, give-ups)
+  e) exec_steps=("py:tools/b_grid_probe.py:20") ;;
+  *) echo "usage: $0 a|b|c|d|e" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
