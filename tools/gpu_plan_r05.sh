@@ -27,6 +27,13 @@ case ${1:-} in
                  ab:rmat24:4:base,bpc4=GC_ASYNC_BPC:4,bpc8=GC_ASYNC_BPC:8) ;;
   # e: the asynchronous kernels at 2..8 workgroups per CU requested (measured residency, give-ups)
   e) exec_steps=("py:tools/b_grid_probe.py:20") ;;
-  *) echo "usage: $0 a|b|c|d|e" >&2; exit 2 ;;
+  # f: the hub threshold against the whole step (the hub index's build grows with the hub
+  #    entries: R-MAT-28 hin count 70 + fill 100 + hlow sort 35 ms at 512), and variant B's
+  #    fold grid 4 vs 6 per CU
+  f) exec_steps=(ab:rmat24:5:base,t384=GC_HUB_T:384,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048
+                 ab:rmat26:3:base,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048
+                 ab:rmat28:2:base,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048
+                 env:AB_VARIANT=B ab:rmat24:4:base,bpc6=GC_B_ASYNC_BPC:6 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
