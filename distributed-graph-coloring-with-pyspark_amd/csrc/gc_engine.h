@@ -107,6 +107,11 @@ struct gc_graph {
     ull* hb_bits = nullptr;       // hub-transpose build only: bit per entry (col[e] is a hub)
     long long* hb_wpre = nullptr; //   and the exclusive prefix of the words' popcounts
     uint2* hb_mp = nullptr;       //   and hubmap / hubpre interleaved per word
+    // by-product of the creation's rank partition (symmetric graphs): byte e = 1 iff col[e] is
+    // a hub (deg > hubflag_t) -- the hub transpose's count pass then streams these bytes
+    // instead of gathering a hub bit per entry; freed by that pass or by a re-partition
+    unsigned char* hubflag = nullptr;
+    int hubflag_t = -1;
 };
 
 // caching allocator (gc_alloc.hip): every device / pinned-host buffer of the library
@@ -122,12 +127,17 @@ int gc_build_tiling(gc_graph* g);
 // with class 0 = lower key, 1 = equal key and earlier position (both lower rank), 2 =
 // higher rank; nlow = c0 + c1, neq = c1 (neq may be null).  prio 0: key = deg (coloring.py:64),
 // 1: key = prio_hash(seed, v).  *bad (device) counts entries outside [0, n).
-int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad);
+int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad,
+                 unsigned char* hubflag = nullptr, int hub_t = -1);
+// the hub threshold of the colourings (GC_HUB_T, "off" or < 0: none; default GC_HUB_T)
+int gc_hub_threshold();
+// whether the rank partition can mark hub entries (gc_prep.hip: 3 bits per entry in seg_cls)
+bool gc_partition_hubflags_supported();
 // -> ctl->uncolored, ctl->conflicts; c8 (optional): the byte mirror of `colors` (the resident colouring)
 int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8, long long lo, long long hi);
 // symmetric graphs: hub transpose (hin_rp / hin_col: the hubs listed in each row) and the
 // lower-rank hubs of every hub row (hlow counts -> klow[x]); hubmap / hid / hub_v ready
-int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow);
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow, int T);
 int gc_hub_transpose_fill(gc_graph* g, long long H);
 void gc_hub_bits_free(gc_graph* g);
 

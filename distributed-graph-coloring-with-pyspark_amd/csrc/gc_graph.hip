@@ -169,7 +169,7 @@ void gc_free_all(gc_graph* g) {
     hipSetDevice(g->device);
     if (g->stream) hipStreamSynchronize(g->stream);  // parked blocks are idle (gc_alloc.hip)
     {
-        void* prep[] = {g->kb, g->tile_r0, g->seg_row, g->seg_j, g->seg_aux, g->seg_cls, g->seg_base, g->hubmap};
+        void* prep[] = {g->kb, g->tile_r0, g->seg_row, g->seg_j, g->seg_aux, g->seg_cls, g->seg_base, g->hubmap, g->hubflag};
         for (void* p : prep)
             if (p) gc_dfree(p);
     }
@@ -247,7 +247,16 @@ int gc_alloc_graph_common(gc_graph* g, const int* src) {
     }
     g->maxdeg = (long long)g->hctl->seedkey;
     if (g->maxdeg >= (1ll << 31)) { gc_set_error("degree too large"); return GC_EINVAL; }
-    int rc = gc_partition(g, src, g->col, GC_PRIORITY_REF, 0, &g->ctl->conflicts);
+    // symmetric graphs with hubs: the partition also marks the hub entries (a byte each), so
+    // the hub transpose streams them instead of gathering a hub bit per entry (R-MAT-28: ~60 ms)
+    const int hub_t = gc_hub_threshold();
+    const bool flags_on = !(getenv("GC_HUB_FLAGS") && atoi(getenv("GC_HUB_FLAGS")) == 0);  // 0: A/B against the gathers
+    if ((g->flags & GC_GRAPH_SYMMETRIC) && hub_t >= 0 && g->maxdeg > hub_t && g->nnz > 0 &&
+        gc_partition_hubflags_supported() && flags_on) {
+        if (gc_dmalloc((void**)&g->hubflag, (size_t)g->nnz) == hipSuccess) g->hubflag_t = hub_t;
+        else g->hubflag = nullptr;  // no room: the transpose gathers instead
+    }
+    int rc = gc_partition(g, src, g->col, GC_PRIORITY_REF, 0, &g->ctl->conflicts, g->hubflag, g->hubflag_t);
     if (rc) return rc;
     GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
     GC_HIP(hipStreamSynchronize(s));

@@ -278,7 +278,7 @@ int build(gc_graph* g, int T, int W) {
         // the entries): hin_rp directly, each hub row's lower-rank hubs (a prefix of its hin
         // row) into klow
         GC_HIP(gc_dmalloc((void**)&klow, sizeof(long long) * (size_t)(H + 1)));
-        if ((rc = gc_hub_transpose_sym(g, H, g->hin_rp, klow))) { gc_dfree(pos); gc_dfree(klow); return rc; }
+        if ((rc = gc_hub_transpose_sym(g, H, g->hin_rp, klow, T))) { gc_dfree(pos); gc_dfree(klow); return rc; }
     } else {
         // hub transpose: reuse pos as the per-target counter
         GC_HIP(hipMemsetAsync(pos, 0, sizeof(long long) * (size_t)(n + 1), s));
@@ -407,8 +407,10 @@ void gc_hubs_free(gc_graph* g) {
     g->hub_t = -1;
 }
 
+int gc_hub_threshold() { return env_int("GC_HUB_T", GC_HUB_T); }
+
 int gc_hubs_prepare(gc_graph* g, GDev& d) {
-    const int T = env_int("GC_HUB_T", GC_HUB_T);
+    const int T = gc_hub_threshold();
     const int W = std::max(1, env_int("GC_HUB_W", GC_HUB_W));
     if (T < 0 || g->maxdeg <= T || g->borrowed) return GC_OK;
     // (hlow, the lower-rank hubs of each hub, follows the row partition it was built under)

@@ -268,8 +268,15 @@ struct PartArgs {
     ull seed;
     ull* bad;
     ull* seg_aux;       // per segment: packed class counts
-    unsigned* seg_cls;  // per segment x thread: 2-bit classes
+    unsigned* seg_cls;  // per segment x thread: 2-bit classes (bits 0..15), hub flags (bits 16..23)
+    unsigned char* hflag;  // or null: byte per output entry, 1 iff the entry is a hub (deg > hub_t)
+    int hub_t;
+    unsigned hub_code;  // gc_deg_code(hub_t + 1)
+    int hub_amb;        // the code's bucket also holds degrees <= hub_t: those entries gather deg
 };
+
+// Hub flags need a third bit per entry in seg_cls (8 entries per thread: bits 16..23).
+#define GC_PART_HUBFLAG (GC_PER <= 8)
 
 __device__ __forceinline__ unsigned owner_key(const PartArgs& a, int prio, int v) {
     return prio ? gc_prio_hash(a.seed, v) : (unsigned)a.deg[v];
@@ -279,8 +286,9 @@ __device__ __forceinline__ unsigned owner_key(const PartArgs& a, int prio, int v
 // earlier position, 2 the rest (higher rank, self-loops, out-of-range entries)
 template <int PRIO>
 __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u, const unsigned* kv, const int* v,
-                                         unsigned* m0, unsigned* m1, unsigned* m2, ull* nbad) {
+                                         unsigned* m0, unsigned* m1, unsigned* m2, ull* nbad, unsigned* mh) {
     int cls[GC_PER];
+    *mh = 0;
     if (PRIO) {
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
@@ -322,6 +330,30 @@ __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u
             for (int k = 0; k < GC_PER; ++k)
                 if (full[k]) cls[k] = du[k] < kv[k] ? 0 : (du[k] > kv[k] ? 2 : (u[k] < v[k] ? 1 : 2));
         }
+        // hub entries (deg(u) > hub_t) from the same byte key: exact except in the code's
+        // bucket when it also holds degrees <= hub_t, where deg(u) is gathered (R-MAT: few)
+        if (a.hflag) {
+            unsigned h = 0;
+            bool amb[GC_PER];
+            bool any_amb = false;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                amb[k] = false;
+                if (k < nv && (unsigned)u[k] < (unsigned)a.T.n) {
+                    if (kb8[k] > a.hub_code) h |= 1u << k;
+                    else if (kb8[k] == a.hub_code) {
+                        if (a.hub_amb) { amb[k] = true; any_amb = true; }
+                        else h |= 1u << k;
+                    }
+                }
+            }
+            if (any_amb) {
+#pragma unroll
+                for (int k = 0; k < GC_PER; ++k)
+                    if (amb[k] && a.deg[u[k]] > a.hub_t) h |= 1u << k;
+            }
+            *mh = h;
+        }
     }
     unsigned a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll
@@ -354,8 +386,8 @@ __device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad
         kv[k] = S.key[rk[k]];
         vv[k] = r0 + rk[k];
     }
-    unsigned m0, m1, m2;
-    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad);
+    unsigned m0, m1, m2, mh;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad, &mh);
     const ull mine = pack3(__popc(m0), __popc(m1), __popc(m2));
     ull total;
     const ull prefix = block_excl_scan(mine, S.w, &total);  // (its barriers: every S.buf read is done)
@@ -372,10 +404,19 @@ __device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad
         const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
         const unsigned rank = f16(prefix, c) + __popc(mc & (bit - 1u)) - f16(b, c);
         const unsigned start = c == 0 ? 0u : (c == 1 ? c0 : c0 + c1);
-        S.buf[S.off[r] + (int)(start + rank)] = u[k];
+        // (a hub entry carries its flag in bit 31: vertex ids are < 2^31)
+        S.buf[S.off[r] + (int)(start + rank)] = (int)((unsigned)u[k] | (((mh >> k) & 1u) << 31));
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < NE; i += blockDim.x) a.dst[eb + i] = S.buf[i];
+    if (a.hflag) {
+        for (int i = threadIdx.x; i < NE; i += blockDim.x) {
+            const unsigned x = (unsigned)S.buf[i];
+            a.dst[eb + i] = (int)(x & 0x7FFFFFFFu);
+            a.hflag[eb + i] = (unsigned char)(x >> 31);
+        }
+    } else {
+        for (int i = threadIdx.x; i < NE; i += blockDim.x) a.dst[eb + i] = S.buf[i];
+    }
     for (int r = threadIdx.x; r < R; r += blockDim.x) {
         if (hl && r == R - 1) continue;  // the heavy row: its segments' second pass
         const ull b = S.base[r], b1 = S.base[r + 1];
@@ -406,11 +447,14 @@ __device__ void part_seg1(const PartArgs& a, TileLdsP& S, long long s, ull* nbad
         vv[k] = v;
         kv[k] = key;
     }
-    unsigned m0, m1, m2;
-    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad);
+    unsigned m0, m1, m2, mh;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad, &mh);
     unsigned cls = 0;
 #pragma unroll
     for (int k = 0; k < GC_PER; ++k) cls |= (((m1 >> k) & 1u) | (((m2 >> k) & 1u) << 1)) << (2 * k);
+#if GC_PART_HUBFLAG
+    cls |= mh << 16;
+#endif
     a.seg_cls[s * GC_BLOCK + threadIdx.x] = cls;
     const ull tot = block_sum(pack3(__popc(m0), __popc(m1), __popc(m2)), S.w);
     if (threadIdx.x == 0) a.seg_aux[s] = tot;
@@ -473,6 +517,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
         int nv = len - j0;
         nv = nv < 0 ? 0 : (nv > GC_PER ? GC_PER : nv);
         const unsigned cls = a.seg_cls[s * GC_BLOCK + threadIdx.x];
+#if GC_PART_HUBFLAG
+        const unsigned mh = a.hflag ? cls >> 16 : 0u;
+#else
+        const unsigned mh = 0u;
+#endif
         int u[GC_PER];
         unsigned m0 = 0, m1 = 0, m2 = 0;
 #pragma unroll
@@ -497,7 +546,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
             const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : 2);
             const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
             const unsigned sec = c == 0 ? 0u : (c == 1 ? L0 : L0 + L1);
-            buf[sec + f16(prefix, c) + __popc(mc & (bit - 1u))] = u[k];
+            buf[sec + f16(prefix, c) + __popc(mc & (bit - 1u))] = (int)((unsigned)u[k] | (((mh >> k) & 1u) << 31));
         }
         __syncthreads();
         const long long T0 = (long long)s_tot[0], T1 = (long long)s_tot[1];
@@ -507,7 +556,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
             if (i < (int)L0) pos = P0 + i;
             else if (i < (int)(L0 + L1)) pos = T0 + P1 + (i - (int)L0);
             else pos = T0 + T1 + P2 + (i - (int)(L0 + L1));
-            a.dst[rs + pos] = buf[i];
+            const unsigned x = (unsigned)buf[i];
+            if (a.hflag) {
+                a.dst[rs + pos] = (int)(x & 0x7FFFFFFFu);
+                a.hflag[rs + pos] = (unsigned char)(x >> 31);
+            } else {
+                a.dst[rs + pos] = (int)x;
+            }
         }
         if (j == 0 && threadIdx.x == 0) {
             a.nlow[v] = (int)(T0 + T1);
@@ -694,6 +749,37 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hbit(const int* col, long long nnz
     }
 }
 
+// the same bits from the rank partition's hub flags (gc_graph::hubflag, a byte per entry):
+// a coalesced byte stream per wave, no gather
+__global__ void __launch_bounds__(GC_BLOCK) k_hbit_flags(const unsigned char* flag, long long nnz, ull* bits,
+                                                        long long* wcnt, long long nw) {
+    const int lane = gc_lane();
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / GC_WAVE;
+    const long long nwaves = (long long)gridDim.x * blockDim.x / GC_WAVE;
+    for (long long w0 = wave * GC_WAVE; w0 < nw; w0 += nwaves * GC_WAVE) {
+        ull mine = 0;
+#pragma unroll 1
+        for (int k0 = 0; k0 < GC_WAVE; k0 += 8) {
+            unsigned f[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const long long e = (w0 + k0 + k) * GC_WAVE + lane;
+                f[k] = e < nnz ? (unsigned)flag[e] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const ull m = __ballot(f[k] != 0u);
+                if (lane == k0 + k) mine = m;
+            }
+        }
+        const long long w = w0 + lane;
+        if (w < nw) {
+            bits[w] = mine;
+            wcnt[w] = (long long)__popcll(mine);
+        }
+    }
+}
+
 __device__ __forceinline__ long long hb_rank(const ull* bits, const long long* wpre, long long e) {
     const long long w = e >> 6;
     const int b = (int)(e & 63);
@@ -860,7 +946,10 @@ int gc_build_tiling(gc_graph* g) {
     return GC_OK;
 }
 
-int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad) {
+bool gc_partition_hubflags_supported() { return GC_PART_HUBFLAG; }
+
+int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad, unsigned char* hubflag,
+                 int hub_t) {
     if (g->n == 0 || g->nnz == 0) {
         if (g->n) {
             GC_HIP(hipMemsetAsync(g->nlow, 0, sizeof(int) * (size_t)g->n, g->stream));
@@ -882,6 +971,10 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
     a.bad = bad;
     a.seg_aux = g->seg_aux;
     a.seg_cls = g->seg_cls;
+    a.hflag = (GC_PART_HUBFLAG && !prio && hub_t >= 0) ? hubflag : nullptr;
+    a.hub_t = hub_t;
+    a.hub_code = hub_t >= 0 ? gc_deg_code((long long)hub_t + 1) : 0u;
+    a.hub_amb = hub_t >= 0 && gc_deg_code((long long)hub_t) == a.hub_code;
     const int grid = prep_grid(g);
     if (prio) hipLaunchKernelGGL(k_part1<1>, dim3(grid), dim3(GC_BLOCK), 0, g->stream, a);
     else hipLaunchKernelGGL(k_part1<0>, dim3(grid), dim3(GC_BLOCK), 0, g->stream, a);
@@ -938,7 +1031,7 @@ int gc_validate_tiles(gc_graph* g, const int* colors, const unsigned char* c8, l
 // the count pass (hubmap / hubpre / hperm / hid ready): the entry bits and their word
 // prefix (kept on g until the fill), hin_rp (n + 1: the exclusive prefix itself) and klow
 // (H + 1, zeroed here)
-int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow) {
+int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long* klow, int T) {
     const hipStream_t s = g->stream;
     const long long n = g->n, nnz = g->nnz;
     const long long nw = (nnz + 63) / 64;
@@ -956,11 +1049,22 @@ int gc_hub_transpose_sym(gc_graph* g, long long H, long long* hin_rp, long long*
     GC_HIP(hipMemsetAsync(wcnt + nw, 0, sizeof(long long), s));
     GC_HIP(hipMemsetAsync(klow, 0, sizeof(long long) * (size_t)(H + 1), s));
     const int grid = (int)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 8192));
-    if (nw > 0)
+    // the rank partition marked the hub entries for this threshold (gc_alloc_graph_common):
+    // stream its flag bytes; else gather each entry's hub bit
+    const bool flags = g->hubflag && g->hubflag_t == T;
+    if (nw > 0 && flags)
+        hipLaunchKernelGGL(k_hbit_flags, dim3(grid), dim3(GC_BLOCK), 0, s, (const unsigned char*)g->hubflag, nnz,
+                           g->hb_bits, wcnt, nw);
+    else if (nw > 0)
         hipLaunchKernelGGL(k_hbit, dim3(grid), dim3(GC_BLOCK), 0, s, (const int*)g->col, nnz, n,
                            (const uint2*)g->hb_mp, g->hb_bits, wcnt, nw);
-    int rc = scan_ll(wcnt, g->hb_wpre, nw + 1, s);
+    int rc = scan_ll(wcnt, g->hb_wpre, nw + 1, s);  // (synchronises the stream)
     gc_dfree(wcnt);
+    if (g->hubflag) {  // used once: the hub index is kept with the graph
+        gc_dfree(g->hubflag);
+        g->hubflag = nullptr;
+        g->hubflag_t = -1;
+    }
     if (rc) return rc;
     hipLaunchKernelGGL(k_hin_rank, dim3(small_grid(n + 1)), dim3(GC_BLOCK), 0, s, (const long long*)g->rp, n,
                        (const ull*)g->hb_bits, (const long long*)g->hb_wpre, (const int*)g->nlow, (const int*)g->hid,

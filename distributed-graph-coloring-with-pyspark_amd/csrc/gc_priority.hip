@@ -198,6 +198,12 @@ int gc_set_priority(gc_graph* g, int prio, uint64_t seed) {
             gc_set_error("allocation of the partition scratch (%lld entries) failed", g->nnz);
             return GC_ENOMEM;
         }
+        if (g->hubflag) {  // the creation's hub flags follow the (deg, pos) row order: no longer valid
+            hipStreamSynchronize(s);
+            gc_dfree(g->hubflag);
+            g->hubflag = nullptr;
+            g->hubflag_t = -1;
+        }
         int rc = gc_partition(g, g->col, tmp, prio, seed, &g->ctl->conflicts);
         hipError_t ec = hipSuccess;
         if (rc == GC_OK) ec = hipMemcpyAsync(g->col, tmp, sizeof(int) * (size_t)g->nnz, hipMemcpyDeviceToDevice, s);

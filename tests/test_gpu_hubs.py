@@ -150,3 +150,25 @@ def test_commit_big_tiles(monkeypatch, bigrow, hub_t):
     _check(rp, col, symmetric=True, bounded=False)
     rp, col = _random_directed(3000, 30000, 11)
     _check(rp, col)
+
+
+@pytest.mark.parametrize("hub_t", ["512", "95", "100", "1"])
+def test_partition_hub_flags_match_gathered_bits(monkeypatch, hub_t):
+    """The rank partition marks hub entries from the byte key it gathers anyway (gc_prep.hip,
+    round 5; deg gathered only in the key's bucket when it straddles the threshold: 512 and
+    100 straddle, 95 does not) and the hub transpose streams those flags; GC_HUB_FLAGS=0 gathers
+    a hub bit per entry as before.  Both give the oracle's colouring, round for round -- on an
+    R-MAT graph whose hub rows are split into partition segments (rows > 1024 entries)."""
+    from gcolor_amd.engine import DeviceGraph
+    monkeypatch.setenv("GC_HUB_T", hub_t)
+    with DeviceGraph.rmat(16, 16, seed=7) as dg:
+        rp, col = dg.export()
+    assert np.diff(rp).max() > 2048
+    o = oracle.c_color(rp, col, "A")
+    for flags in ("1", "0"):
+        monkeypatch.setenv("GC_HUB_FLAGS", flags)
+        with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+            g = dg.color("A")
+            assert g.hubs > 0
+            assert_same_run(g, o)
+            assert dg.validate() == (0, 0)

@@ -34,6 +34,12 @@ case ${1:-} in
                  ab:rmat26:3:base,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048
                  ab:rmat28:2:base,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048
                  env:AB_VARIANT=B ab:rmat24:4:base,bpc6=GC_B_ASYNC_BPC:6 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f" >&2; exit 2 ;;
+  # g: hub flags from the rank partition (the hub transpose's count streams them instead of a
+  #    gathered hub bit per entry): the hub tests, every GPU test, the phase times of R-MAT-28 /
+  #    R-MAT-26, and the A/B against the gathers (GC_HUB_FLAGS=0)
+  g) exec_steps=(file:tests/test_gpu_hubs.py tests env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 env:GC_PREP_TIMING=
+                 ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
+                 ab:rmat28:2:base,gather=GC_HUB_FLAGS:0) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
