@@ -17,7 +17,8 @@ what a test needs to compare a full colouring exactly:
 
 Output: tests/golden/rmat_oracle_s<scale>.json.  Usage:
   python tests/golden/make_rmat_fixtures.py 24 A B     (C3, both variants: ~40 min)
-  python tests/golden/make_rmat_fixtures.py 22 A       (the CPU test of gcolor_omp.c)
+  python tests/golden/make_rmat_fixtures.py pin22      (the CPU pin of gcolor_omp.c: the oracle
+                                                       on tests/test_oracle_omp.py's R-MAT-22)
 """
 import hashlib
 import json
@@ -81,7 +82,32 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def pin_fixture(scale):
+    """The single-thread oracle's variant-A run on tests/test_oracle_omp.py's numpy R-MAT graph
+    (rmat_csr(scale, 16, seed=scale)): the pin of the multi-core restatement gcolor_omp.c at a
+    size where the oracle takes minutes (tests/test_oracle_omp.py::test_rmat_pinned_fixture)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle import oracle
+    from test_oracle_omp import rmat_csr
+    rp, col = rmat_csr(scale, 16, seed=scale)
+    t0 = time.time()
+    o = oracle.c_color(rp, col, "A", max_rounds=1 << 14)
+    rec = {"generator": f"tests/test_oracle_omp.py rmat_csr({scale}, 16, seed={scale})", "scale": scale,
+           "n": int(len(rp) - 1), "nnz": int(len(col)), "rp_sha256": sha(rp), "col_sha256": sha(col),
+           "oracle": "oracle/gcolor_oracle.c (one thread)", "seconds": round(time.time() - t0, 1),
+           "status": int(o["status"]), "rounds": int(o["rounds"]), "max_color": int(o["max_color"]),
+           "colors_sha256": sha(o["colors"].astype(np.int32)),
+           "colored_round_sha256": sha(o["colored_round"].astype(np.int32)),
+           **{"round_" + k: [int(x) for x in o["round_" + k]] for k in ("U", "F", "maxmex", "accepted", "seeds")}}
+    out_path = os.path.join(HERE, f"rmat_csr_oracle_s{scale}.json")
+    with open(out_path, "w") as f:
+        json.dump(rec, f)
+    print("wrote", out_path, rec["rounds"], "rounds", rec["seconds"], "s")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1].startswith("pin"):
+        return pin_fixture(int(sys.argv[1][3:]))
     scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     variants = sys.argv[2:] or ["A", "B"]
     from oracle import oracle
