@@ -40,6 +40,8 @@ case ${1:-} in
   g) exec_steps=(file:tests/test_gpu_hubs.py tests env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 env:GC_PREP_TIMING=
                  ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
                  ab:rmat28:2:base,gather=GC_HUB_FLAGS:0) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g" >&2; exit 2 ;;
+  # h: variant B's 7-per-CU cliff under a 10x longer give-up budget (slow progress or a stall?)
+  h) exec_steps=("py:tools/b_cliff_probe.py") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
