@@ -42,6 +42,13 @@ case ${1:-} in
                  ab:rmat28:2:base,gather=GC_HUB_FLAGS:0) ;;
   # h: variant B's 7-per-CU cliff under a 10x longer give-up budget (slow progress or a stall?)
   h) exec_steps=("py:tools/b_cliff_probe.py") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h" >&2; exit 2 ;;
+  # i: the R-MAT-27 fixture of the multi-core restatement (minutes on 16 threads, heartbeats),
+  #    then every GPU test, the phase times and the hub-flag A/Bs of session g
+  i) exec_steps=("py:tools/make_rmat27_omp_fixture.py:gpurun_out/r05i/rmat_omp_s27.json" tests) ;;
+  # j: the phase times with the partition's hub flags, the A/B against the gathers, variant B's cliff
+  j) exec_steps=(env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 step:rmat24 env:GC_PREP_TIMING=
+                 ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
+                 ab:rmat28:2:base,gather=GC_HUB_FLAGS:0 "py:tools/b_cliff_probe.py") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
