@@ -290,11 +290,14 @@ struct Run {
     // hub) and lights narrow enough for k_propose's 2048-bit window; the bitmaps must cover
     // every colour the enqueued rounds can reach (maxcolor grows by at most one a round: the
     // last snapshot's maxcolor plus a margin of the rounds in flight).
-    const bool inline_pb = !(getenv("GC_INLINE_PB") && atoi(getenv("GC_INLINE_PB")) == 0);
+    bool inline_pb = !(getenv("GC_INLINE_PB") && atoi(getenv("GC_INLINE_PB")) == 0);
     long long maxc_hint = 1ll << 40;  // the last snapshot's maxcolor (none yet: no inlining; a resumed colouring's colours are unknown here)
+    // GC_TEST_INL_MARGIN (tests only) replaces the margin, so a test can make the inlined
+    // proposals outrun a small bitmap and exercise the fallback of color_impl
+    const long long inl_margin = getenv("GC_TEST_INL_MARGIN") ? atoll(getenv("GC_TEST_INL_MARGIN")) : 2 + 4ll * batch_max + 16;
     bool inline_now() const {
         return inline_pb && !resort_hint && d.hbits_w && !d.hub_repl && d.heavy_t < 2048 &&
-               maxc_hint + 2 + 4ll * batch_max + 16 <= 32ll * d.hbits_w;
+               maxc_hint + inl_margin <= 32ll * d.hbits_w;
     }
     // Fused commits (k_commit<1>) make the next round's proposals themselves, so a round
     // after one runs no k_propose: low-degree graphs (no heavy or wide proposer, no hubs),
@@ -691,7 +694,8 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     int rc = gc_alloc_run_state(g);
     if (rc) return rc;
     cc.mark("run state", g->stream);
-    if (stats) {
+    auto clear_stats = [&]() {
+        if (!stats) return;
         // keep caller's round buffers, clear outputs
         gc_stats keep = *stats;
         memset(stats, 0, sizeof(*stats));
@@ -702,7 +706,8 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
         stats->round_accepted = keep.round_accepted;
         stats->round_seeds = keep.round_seeds;
         stats->max_color = -1;
-    }
+    };
+    clear_stats();
     if (opt->variant == GC_VARIANT_B && (opt->priority != GC_PRIORITY_REF || opt->speculative)) {
         gc_set_error("gc_color: seeded priorities and the speculative mode are variant A only");
         return GC_EINVAL;
@@ -716,8 +721,10 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     cc.mark("priority", g->stream);
     if (opt->variant == GC_VARIANT_B) return gc_color_variant_b(g, opt, colors_out, cround_out, stats);
     if (opt->speculative) return gc_color_speculative(g, opt, colors_out, cround_out, stats);
+    for (int attempt = 0;; ++attempt) {
     Run run{g, opt, stats, KTimer{g, (unsigned)opt->kernel_timing, stats}, gc_view(g), gc_lists(g), g->stream,
             {}, 0};
+    if (attempt) run.inline_pb = false;
     // hubs: forbidden-colour bitmaps for their proposals; the hub JP (hubs rank above every
     // light vertex) only under (deg, pos) -- seeded ranks resolve hubs by row scans
     if ((rc = gc_hubs_prepare(g, run.d))) return rc;
@@ -743,7 +750,16 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
     cc.mark("set-up", g->stream);
     rc = run.go(colors_out, cround_out, rs);  // stats->rounds may exceed round_cap: the caller re-asks
     cc.mark("rounds", g->stream);
+    // A hub proposed inside k_propose<1> whose bitmap no longer covered the colours in use (the
+    // host's margin on the last snapshot's max colour was too small: never seen) is reported by
+    // the device as GC_LERR_INL; the colouring is then run again without the inlined proposals
+    // (k_propose_block scans such a hub's row) instead of failing.
+    if (rc == GC_EHIP && attempt == 0 && run.inline_pb && g->hctl->loop_err == GC_LERR_INL) {
+        clear_stats();
+        continue;
+    }
     return rc;
+    }
 }
 
 extern "C" int gc_color(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,

@@ -163,7 +163,11 @@ int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t* colors_de
 /* validate_graph_coloring counts: #uncoloured and the directed count of listed pairs
    (v, u in N(v)) with colour[u] == colour[v] (self-loops and duplicates count, as in
    coloring.py:157-158).  colors == NULL validates the device result of the last
-   gc_color on this handle without a host round trip.                                 */
+   gc_color on this handle without a host round trip.
+   On a graph created with GC_GRAPH_SYMMETRIC the count is 2 x the conflicts of the rows'
+   lower-rank entries + the self-loop entries (half the gathers; GC_VALIDATE_HALF=0 counts
+   every entry): exact when the rows ARE symmetric, which the flag asserts -- the library does
+   not check it.  Create an asymmetric graph without the flag (then every entry is counted).  */
 int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t* conflicts);
 
 /* The same counts over the rows of vertices [lo, hi) only: every uncoloured vertex of the

@@ -172,3 +172,21 @@ def test_partition_hub_flags_match_gathered_bits(monkeypatch, hub_t):
             assert g.hubs > 0
             assert_same_run(g, o)
             assert dg.validate() == (0, 0)
+
+
+def test_inline_proposal_overrun_falls_back(monkeypatch):
+    """Hubs proposed inside k_propose<1> need their bitmaps to cover every colour the enqueued
+    rounds can reach (the host keeps a margin over the last snapshot's max colour).  With the
+    margin forced negative (GC_TEST_INL_MARGIN) and 1-word bitmaps (32 colours), the device
+    reports the overrun and the colouring is run again without the inlined proposals
+    (no hard error) -- the oracle's colouring, round for round."""
+    from gcolor_amd.engine import DeviceGraph
+    with DeviceGraph.rmat(12, 16, seed=3) as dg:
+        rp, col = dg.export()
+    o = oracle.c_color(rp, col, "A")
+    assert o["max_color"] > 40
+    monkeypatch.setenv("GC_HUB_T", "8")
+    monkeypatch.setenv("GC_HUB_W", "1")
+    monkeypatch.setenv("GC_TEST_INL_MARGIN", "-1000")
+    with DeviceGraph.from_csr(rp, col, symmetric=True) as dg:
+        assert_same_run(dg.color("A"), o)
