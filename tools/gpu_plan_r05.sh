@@ -49,6 +49,15 @@ case ${1:-} in
   j) exec_steps=(env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 step:rmat24 env:GC_PREP_TIMING=
                  ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
                  ab:rmat28:2:base,gather=GC_HUB_FLAGS:0 "py:tools/b_cliff_probe.py") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j" >&2; exit 2 ;;
+  # k: the rocprofv3 summaries of THIS build (kernel trace + FETCH / WRITE passes -> profiles/pmc),
+  #    the five single-GPU workloads the bench lines read them for
+  k) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26
+                 "profile:mesh512:--steps,3" "profile:uniform10M") ;;
+  # l: the N > 1 step rehearsed at scale: bench.py --gpus 2 (it starts the two ranks itself) on
+  #    R-MAT-26, both ranks on this box's one GPU over gloo
+  l) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
+                 "bench:rmat26:--gpus,2,--steps,2,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=
+                 "bench:rmat26:--sharded,--steps,2,--warmup,1") ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
