@@ -308,52 +308,40 @@ __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u
             const bool ok = k < nv && (unsigned)u[k] < (unsigned)a.T.n;
             kb8[k] = ok ? (unsigned)a.kb[u[k]] : 0u;
         }
-        bool full[GC_PER];
-        bool any_full = false;
+        // fullm: entries whose class needs the full degree (equal bucketed codes); hamb: entries
+        // whose hub flag does (the key's bucket straddles the hub threshold) -- one gather pass
+        // serves both, and bit masks keep the registers of the flag-free kernel (occupancy)
+        unsigned fullm = 0, hamb = 0, h = 0;
+        const unsigned hc = a.hub_code;
+        const bool hf = a.hflag != nullptr;
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
-            full[k] = false;
             cls[k] = 3;
             if (k < nv) {
                 if ((unsigned)u[k] >= (unsigned)a.T.n) { cls[k] = 2; ++*nbad; continue; }
                 const unsigned kv8 = gc_deg_code((long long)kv[k]);
                 if (kb8[k] != kv8) cls[k] = kb8[k] < kv8 ? 0 : 2;
                 else if (kv8 < GC_DEG_CODE_EXACT) cls[k] = u[k] < v[k] ? 1 : 2;
-                else { full[k] = true; any_full = true; }
-            }
-        }
-        if (any_full) {
-            unsigned du[GC_PER];
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) du[k] = full[k] ? (unsigned)a.deg[u[k]] : 0u;
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k)
-                if (full[k]) cls[k] = du[k] < kv[k] ? 0 : (du[k] > kv[k] ? 2 : (u[k] < v[k] ? 1 : 2));
-        }
-        // hub entries (deg(u) > hub_t) from the same byte key: exact except in the code's
-        // bucket when it also holds degrees <= hub_t, where deg(u) is gathered (R-MAT: few)
-        if (a.hflag) {
-            unsigned h = 0;
-            bool amb[GC_PER];
-            bool any_amb = false;
-#pragma unroll
-            for (int k = 0; k < GC_PER; ++k) {
-                amb[k] = false;
-                if (k < nv && (unsigned)u[k] < (unsigned)a.T.n) {
-                    if (kb8[k] > a.hub_code) h |= 1u << k;
-                    else if (kb8[k] == a.hub_code) {
-                        if (a.hub_amb) { amb[k] = true; any_amb = true; }
-                        else h |= 1u << k;
-                    }
+                else fullm |= 1u << k;
+                // hub entries (deg(u) > hub_t) from the same byte key: exact except in the
+                // code's bucket when it also holds degrees <= hub_t (R-MAT: few entries)
+                if (hf && kb8[k] >= hc) {
+                    if (kb8[k] > hc || !a.hub_amb) h |= 1u << k;
+                    else hamb |= 1u << k;
                 }
             }
-            if (any_amb) {
-#pragma unroll
-                for (int k = 0; k < GC_PER; ++k)
-                    if (amb[k] && a.deg[u[k]] > a.hub_t) h |= 1u << k;
-            }
-            *mh = h;
         }
+        if (fullm | hamb) {
+            unsigned du[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) du[k] = ((fullm | hamb) >> k) & 1u ? (unsigned)a.deg[u[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                if ((fullm >> k) & 1u) cls[k] = du[k] < kv[k] ? 0 : (du[k] > kv[k] ? 2 : (u[k] < v[k] ? 1 : 2));
+                if (((hamb >> k) & 1u) && du[k] > (unsigned)a.hub_t) h |= 1u << k;
+            }
+        }
+        *mh = h;
     }
     unsigned a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll

@@ -46,7 +46,7 @@ case ${1:-} in
   #    then every GPU test, the phase times and the hub-flag A/Bs of session g
   i) exec_steps=("py:tools/make_rmat27_omp_fixture.py:gpurun_out/r05i/rmat_omp_s27.json" tests) ;;
   # j: the phase times with the partition's hub flags, the A/B against the gathers, variant B's cliff
-  j) exec_steps=(env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 step:rmat24 env:GC_PREP_TIMING=
+  j) exec_steps=(file:tests/test_gpu_fullsize.py:rmat27_engine env:GC_PREP_TIMING=1 step:rmat28 step:rmat26 step:rmat24 env:GC_PREP_TIMING=
                  ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
                  ab:rmat28:2:base,gather=GC_HUB_FLAGS:0 "py:tools/b_cliff_probe.py") ;;
   # k: the rocprofv3 summaries of THIS build (kernel trace + FETCH / WRITE passes -> profiles/pmc),
@@ -58,6 +58,11 @@ case ${1:-} in
   l) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
                  "bench:rmat26:--gpus,2,--steps,2,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=
                  "bench:rmat26:--sharded,--steps,2,--warmup,1") ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l" >&2; exit 2 ;;
+  # m: the partition's hub flags at the flag-free kernel's occupancy (bit masks: 95 VGPRs, 5 waves
+  #    per SIMD, was 102 / 4): hub + parity tests, the A/B against the gathers again
+  m) exec_steps=(file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py
+                 ab:rmat26:3:base,gather=GC_HUB_FLAGS:0 ab:rmat24:5:base,gather=GC_HUB_FLAGS:0
+                 ab:rmat28:2:base,gather=GC_HUB_FLAGS:0) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
