@@ -611,13 +611,18 @@ def run_multi(args, world, rank, local_rank, dist, torch):
     S = MultiStep(args, w, world, rank, comm, torch, dist)
     gen_s = time.time() - t0
     m = S.nnz // 2
+    if rank == 0:
+        progress(f"graph and resident CSR ready in {gen_s:.1f} s; warmup")
 
     def barrier():
         torch.cuda.synchronize()
         dist.barrier()
 
-    for _ in range(max(args.warmup, 1)):
+    for i in range(max(args.warmup, 1)):
+        a = time.perf_counter()
         res, _ = S.step(False)
+        if rank == 0:
+            progress(f"warmup step {i}: {(time.perf_counter() - a) * 1e3:.1f} ms (switch at round {res.switch_round})")
     if rank == 0:
         progress("warmup done; timed steps")
     barrier()

@@ -56,8 +56,8 @@ case ${1:-} in
   # l: the N > 1 step rehearsed at scale: bench.py --gpus 2 (it starts the two ranks itself) on
   #    R-MAT-26, both ranks on this box's one GPU over gloo
   l) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
-                 "bench:rmat26:--gpus,2,--steps,2,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=
-                 "bench:rmat26:--sharded,--steps,2,--warmup,1") ;;
+                 "bench:rmat24:--gpus,2,--steps,2,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=
+                 "bench:rmat26:--sharded,--steps,2,--warmup,1" "bench:rmat28:--sharded,--steps,2,--warmup,1") ;;
   # m: the partition's hub flags at the flag-free kernel's occupancy (bit masks: 95 VGPRs, 5 waves
   #    per SIMD, was 102 / 4): hub + parity tests, the A/B against the gathers again
   m) exec_steps=(file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py
