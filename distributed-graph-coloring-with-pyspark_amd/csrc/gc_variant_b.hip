@@ -764,7 +764,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
         if (n1 + n2 == 0) break;
         if ((stop = b_async_stop(c, t0, budget))) break;
         if (n1 + n2 == before) {
-            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+            if (++idle > 2) {
+#ifdef GC_B_IDLE_ACQ  // (experiment: invalidate this XCD's non-coherent lines before polling again)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+                __builtin_amdgcn_s_sleep(2);
+            }
         } else {
             idle = 0;
         }
