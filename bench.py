@@ -255,7 +255,8 @@ class StepRunner:
     def step(self, timing=None):
         from gcolor_amd.engine import DeviceGraph
         a = time.perf_counter()
-        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym)
+        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym,
+                                     stream=self.torch.cuda.current_stream().cuda_stream)
         b = time.perf_counter()
         r = dg.color(self.V, kernel_timing=timing, want_rounds=False, want_colors=False, **self.mode)
         c = time.perf_counter()
@@ -549,7 +550,8 @@ class MultiStep:
         from gcolor_amd.engine import DeviceGraph
         torch = self.torch
         a = time.perf_counter()
-        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym)
+        dg = DeviceGraph.from_device(self.d_rp.data_ptr(), self.d_col.data_ptr(), self.n, self.nnz, symmetric=self.sym,
+                                     stream=torch.cuda.current_stream().cuda_stream)
         ops = self.sh.HipShard(dg, self.lo, self.hi)
         b = time.perf_counter()
         res = self.colour(ops, dg, want_colors)

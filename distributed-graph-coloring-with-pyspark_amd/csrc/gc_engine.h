@@ -174,6 +174,10 @@ inline int gc_read_dev(hipStream_t s, T* host, const T* dev, size_t count = 1) {
         if (rr_) return rr_;                                     \
     } while (0)
 
+// Order the library stream `s` after the caller's device inputs: an event on the stream set
+// with gc_set_input_stream (this thread), else a device-wide synchronisation.
+int gc_order_after_inputs(hipStream_t s);
+
 int gc_alloc_graph_common(gc_graph* g, const int* src);  // deg, maxdeg, rank partition of src, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi);  // the same, symmetric graphs (no atomics)

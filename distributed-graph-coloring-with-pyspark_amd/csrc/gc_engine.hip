@@ -46,6 +46,29 @@ extern "C" int gc_set_device(int32_t device) {
 
 thread_local long long gc_tl_launches = 0;
 
+static thread_local hipStream_t t_input_stream = nullptr;
+static thread_local bool t_input_stream_set = false;
+
+extern "C" int gc_set_input_stream(void* stream, int32_t enable) {
+    t_input_stream = (hipStream_t)stream;
+    t_input_stream_set = enable != 0;
+    return GC_OK;
+}
+
+int gc_order_after_inputs(hipStream_t s) {
+    if (!t_input_stream_set) {
+        GC_HIP(hipDeviceSynchronize());
+        return GC_OK;
+    }
+    hipEvent_t ev;
+    GC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, t_input_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+    hipEventDestroy(ev);  // released once the wait completes
+    GC_HIP(e);
+    return GC_OK;
+}
+
 GDev gc_view(const gc_graph* g) {
     GDev d;
     d.n = (int)g->n;
@@ -777,7 +800,7 @@ extern "C" int gc_color_resume(gc_graph* g, const gc_options* opt, const int32_t
     // the caller's device buffers may still be being written on another stream (torch's):
     // the library's own stream is non-blocking, so order its first read after them
     GC_HIP(hipSetDevice(g->device));
-    GC_HIP(hipDeviceSynchronize());
+    if (int rc = gc_order_after_inputs(g->stream)) return rc;
     const ResumeArgs rs{colors_dev, cround_dev, front_dev, (long long)nfront, (long long)round0};
     return color_impl(g, opt, colors_out, cround_out, stats, &rs);
 }

@@ -382,12 +382,17 @@ extern "C" int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64
 extern "C" int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                                       uint32_t flags, gc_graph** out) {
     if (!d_row_ptr || (nnz > 0 && !d_col)) { gc_set_error("gc_graph_create_device: null input"); return GC_EINVAL; }
-    // the caller's CSR may still be being written on another stream (torch's); the library's
-    // stream is non-blocking, so its first read is ordered after all work on the device
-    GC_HIP(hipDeviceSynchronize());
     gc_graph* g;
     int rc = new_graph(out, n, nnz, flags, &g);
     if (rc) return rc;
+    // the caller's CSR may still be being written on another stream (torch's); the library's
+    // stream is non-blocking, so its first read is ordered after that stream's work (or after
+    // all work on the device when the caller named no stream)
+    if ((rc = gc_order_after_inputs(g->stream))) {
+        gc_free_all(g);
+        delete g;
+        return rc;
+    }
     if (hipMemcpyAsync(g->rp, d_row_ptr, sizeof(long long) * (size_t)(n + 1), hipMemcpyDeviceToDevice, g->stream) !=
         hipSuccess) {
         gc_set_error("D2D copy failed");

@@ -28,7 +28,7 @@ KERNEL_CLASSES = ["init", "propose", "resolve", "sweep", "commit", "reseed", "va
 # Every symbol include/gcolor.h declares (checked by tests/test_abi.py).
 EXPORTS = ["gc_graph_create", "gc_graph_create_device", "gc_graph_create_rmat", "gc_graph_create_mesh",
            "gc_graph_destroy", "gc_graph_info", "gc_graph_device", "gc_graph_export", "gc_graph_export_device", "gc_graph_lower_counts", "gc_color", "gc_color_resume", "gc_validate", "gc_validate_range",
-           "gc_gen_uniform", "gc_last_error", "gc_release_cache", "gc_device_count", "gc_set_device",
+           "gc_gen_uniform", "gc_last_error", "gc_release_cache", "gc_set_input_stream", "gc_device_count", "gc_set_device",
            "gc_shard_create", "gc_shard_destroy", "gc_shard_begin", "gc_shard_propose", "gc_shard_apply",
            "gc_shard_sweep", "gc_shard_finish", "gc_shard_reseed", "gc_shard_colors", "gc_shard_set_stream",
            "gc_shard_propose_async", "gc_shard_sweep_async", "gc_shard_pack",
@@ -111,6 +111,7 @@ def load():
         "gc_gen_uniform": ([I64, I32, U64, P, P, I64, _I64P], ctypes.c_int),
         "gc_last_error": ([], ctypes.c_char_p),
         "gc_release_cache": ([], ctypes.c_int),
+        "gc_set_input_stream": ([P, ctypes.c_int32], ctypes.c_int),
         "gc_device_count": ([ctypes.POINTER(I32)], ctypes.c_int),
         "gc_set_device": ([I32], ctypes.c_int),
         "gc_shard_create": ([P, I64, I64, PP], ctypes.c_int),

@@ -6,6 +6,7 @@
 coloring_optimized.py:70) and ``DeviceGraph.validate`` replaces
 ``validate_graph_coloring`` (coloring.py:149-162).  All compute runs in libgcolor.so.
 """
+import contextlib
 import ctypes
 from dataclasses import dataclass, field
 
@@ -67,6 +68,19 @@ class ColorResult:
         return sum(k["bytes"] for k in self.kernels.values())
 
 
+@contextlib.contextmanager
+def _input_stream(lib, stream):
+    """gc_set_input_stream around one call (per thread; restored to the device-wide wait)."""
+    if stream is None:
+        yield
+        return
+    nat.check("gc_set_input_stream", lib.gc_set_input_stream(ctypes.c_void_p(int(stream)), 1))
+    try:
+        yield
+    finally:
+        lib.gc_set_input_stream(None, 0)
+
+
 class DeviceGraph:
     """An HBM-resident CSR graph (file positions; adjacency exactly as listed)."""
 
@@ -98,15 +112,19 @@ class DeviceGraph:
         return cls(h)
 
     @classmethod
-    def from_device(cls, d_row_ptr, d_col, n, nnz, symmetric=False):
+    def from_device(cls, d_row_ptr, d_col, n, nnz, symmetric=False, stream=None):
         """A graph from a CSR already resident in HBM: device pointers (ints, e.g. a torch
         tensor's ``data_ptr()``) to int64[n+1] offsets and int32[nnz] positions.  The rows are
-        read in place and rank-partitioned into the graph's own array (gc_graph_create_device)."""
+        read in place and rank-partitioned into the graph's own array (gc_graph_create_device).
+        ``stream``: the hipStream_t (int, e.g. ``torch.cuda.current_stream().cuda_stream``) the
+        CSR was written on -- the first read waits for that stream only; None waits for the
+        whole device."""
         lib = nat.load()
         h = ctypes.c_void_p()
-        nat.check("gc_graph_create_device", lib.gc_graph_create_device(
-            ctypes.c_void_p(d_row_ptr), ctypes.c_void_p(d_col), int(n), int(nnz),
-            nat.GC_GRAPH_SYMMETRIC if symmetric else 0, ctypes.byref(h)))
+        with _input_stream(lib, stream):
+            nat.check("gc_graph_create_device", lib.gc_graph_create_device(
+                ctypes.c_void_p(d_row_ptr), ctypes.c_void_p(d_col), int(n), int(nnz),
+                nat.GC_GRAPH_SYMMETRIC if symmetric else 0, ctypes.byref(h)))
         return cls(h)
 
     @classmethod
@@ -187,20 +205,22 @@ class DeviceGraph:
         return self._color(opt, want_rounds, want_colors, ROUND_CAP)
 
     def resume(self, colors_dev, front_dev, nfront, round0, cround_dev=None, num_colors=None, e1=True,
-               want_rounds=True, want_colors=True, kernel_timing=False):
+               want_rounds=True, want_colors=True, kernel_timing=False, stream=None):
         """The colouring continued from round ``round0`` of a run in progress (gc_color_resume):
         the rest of graph_coloring's loop (coloring.py:85-132) from a round start.
         ``colors_dev`` / ``cround_dev`` / ``front_dev`` are DEVICE pointers (ints) of int32 arrays
         -- the colours so far (-1 uncoloured), the round each was coloured in (or None), and the
         ``nfront`` uncoloured vertices with a coloured listed neighbour.  Variant A, reference
-        rank.  The records are those of rounds round0, round0 + 1, ..."""
+        rank.  The records are those of rounds round0, round0 + 1, ...  ``stream``: as in
+        from_device, the stream those buffers were written on (None: the whole device)."""
         opt = nat.GcOptions(variant=nat.GC_VARIANT_A, e1=1 if e1 else 0,
                             num_colors=-1 if num_colors is None else int(num_colors),
                             kernel_timing=_timing_mask(kernel_timing), priority=nat.GC_PRIORITY_REF, seed=0,
                             speculative=0, reserved=0)
         args = (ctypes.c_void_p(colors_dev), ctypes.c_void_p(cround_dev) if cround_dev else None,
                 ctypes.c_void_p(front_dev) if front_dev else None, int(nfront), int(round0))
-        return self._color(opt, want_rounds, want_colors, ROUND_CAP, resume=args)
+        with _input_stream(self._lib, stream):
+            return self._color(opt, want_rounds, want_colors, ROUND_CAP, resume=args)
 
     def _color(self, opt, want_rounds, want_colors, cap, resume=None):
         st = nat.GcStats()

@@ -646,11 +646,12 @@ def engine_resume(dg, lock=None):
     """``resume`` for ``hybrid_color``: the one-GPU engine (DeviceGraph.resume, gc_color_resume)
     continues from the replicated state; ``lock`` serialises ranks that share ``dg`` (threads)."""
     def run(colors, cround, front, round0, num_colors, e1, track_rounds, want_colors):
-        if colors.is_cuda:  # the state (and the all-gathered frontier) settled on torch's stream
-            torch.cuda.current_stream(colors.device).synchronize()
+        # the state (and the all-gathered frontier) are produced on torch's stream: the engine's
+        # first read waits on that stream (an event), not on the host
+        stream = torch.cuda.current_stream(colors.device).cuda_stream if colors.is_cuda else None
         args = (colors.data_ptr(), front.data_ptr() if front.numel() else None, int(front.numel()), int(round0))
         kw = dict(cround_dev=cround.data_ptr() if (track_rounds and cround is not None) else None,
-                  num_colors=num_colors, e1=e1, want_rounds=True, want_colors=want_colors)
+                  num_colors=num_colors, e1=e1, want_rounds=True, want_colors=want_colors, stream=stream)
         if lock is None:
             return dg.resume(*args, **kw)
         with lock:

@@ -53,9 +53,10 @@ int gc_graph_create(const int64_t* row_ptr, const int32_t* col, int64_t n, int64
 /* Same, from device pointers already resident in HBM: rp is copied, the rows are read in
    place and written rank-partitioned into the graph's own array (no copy of col).  The
    caller's buffers need to stay valid only for the duration of the call.  Ordering: the
-   library works on its own non-blocking stream, so the call first waits for all work on
-   the device (hipDeviceSynchronize): buffers still being written by kernels on any stream
-   (e.g. torch's) are complete before their first read.                                */
+   library works on its own non-blocking stream, so its first read is ordered after the
+   stream named with gc_set_input_stream (an event wait), or -- when none is named -- after
+   all work on the device (hipDeviceSynchronize): buffers still being written by kernels on
+   another stream (e.g. torch's) are complete before their first read.                  */
 int gc_graph_create_device(const int64_t* d_row_ptr, const int32_t* d_col, int64_t n, int64_t nnz,
                            uint32_t flags, gc_graph** out);
 /* Device-side synthetic generators (no host round trip):
@@ -307,6 +308,12 @@ const char* gc_last_error(void);
 /* Return every device / pinned block the library's allocator has parked for reuse (graph
    handles that are created and destroyed repeatedly get their buffers from that cache).  */
 int gc_release_cache(void);
+/* The stream (a hipStream_t, e.g. torch's current one) on which this thread's device inputs
+   to gc_graph_create_device / gc_color_resume are produced: those calls then order their
+   first read after it with an event instead of synchronising the whole device (which waits
+   for other threads' work too and is invalid during a stream capture).  enable = 0 restores
+   the device-wide synchronisation.  Per thread.                                         */
+int gc_set_input_stream(void* stream, int32_t enable);
 int gc_device_count(int32_t* count);
 int gc_set_device(int32_t device);
 

@@ -300,6 +300,16 @@ def test_partition_is_the_stable_three_class_split(kind):
             out_col = torch.empty_like(d_col)
             dg2.export_device(out_rp.data_ptr(), out_col.data_ptr())
             assert np.array_equal(out_col.cpu().numpy(), exp) and np.array_equal(out_rp.cpu().numpy(), rp)
+        # the CSR still being written on a side stream, no host wait: the creation is ordered
+        # after that stream by an event (gc_set_input_stream)
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            s_rp = torch.zeros_like(d_rp)
+            s_col = torch.zeros_like(d_col)
+            s_rp.copy_(d_rp)
+            s_col.copy_(d_col)
+        with DG.from_device(s_rp.data_ptr(), s_col.data_ptr(), len(rp) - 1, len(col), stream=side.cuda_stream) as dg3:
+            assert np.array_equal(dg3.export()[1], exp)
         # validation over tiles and segmented rows, host and device colours
         rng = np.random.default_rng(3)
         for ncol in (1, 3, 50):
