@@ -58,6 +58,7 @@ def analyze(trace, rec_path):
     print(f"{len(rounds)} rounds in the last colouring (records: {len(U)})")
     agg = collections.OrderedDict((c, collections.Counter()) for c in CLASSES)
     per_round = collections.OrderedDict((c, []) for c in CLASSES)
+    async_per_round = []
     for i, rnd in enumerate(rounds):
         # round i's records: U of round i (the last round lists U = 0)
         u = U[i] if i < len(U) else 0
@@ -79,12 +80,16 @@ def analyze(trace, rec_path):
                     a["adm_rest_us"] += d
             elif nm == "k_b_ev":
                 a["ev_us"] += d
+            elif nm == "k_b_async":  # the asynchronous fold (hub graphs): the round's passes in one launch
+                a["async_us"] += d
+                a["async_n"] += 1
+                async_per_round.append((i, u, d))
             else:
                 a["other_us"] += d
                 a["other:" + nm] += d
         per_round[cls].append(wall)
     hdr = f"{'U class':>16} {'rounds':>6} {'sumU':>10} {'passes':>7} {'wall ms':>8} {'adm1 ms':>8} {'adm+ ms':>8} " \
-          f"{'ev ms':>7} {'rest ms':>8} {'med round us':>12}"
+          f"{'ev ms':>7} {'async ms':>8} {'rest ms':>8} {'med round us':>12}"
     print(hdr)
     for c, a in agg.items():
         if not a["rounds"]:
@@ -92,9 +97,17 @@ def analyze(trace, rec_path):
         lab = f"[{c[0]}, {c[1] if c[1] < 1 << 40 else 'inf'})"
         print(f"{lab:>16} {a['rounds']:>6} {a['U']:>10} {a['passes']:>7} {a['wall_us'] / 1e3:>8.1f} "
               f"{a['adm_first_us'] / 1e3:>8.1f} {a['adm_rest_us'] / 1e3:>8.1f} {a['ev_us'] / 1e3:>7.1f} "
-              f"{a['other_us'] / 1e3:>8.1f} {statistics.median(per_round[c]):>12.1f}")
+              f"{a['async_us'] / 1e3:>8.1f} {a['other_us'] / 1e3:>8.1f} {statistics.median(per_round[c]):>12.1f}")
         top = sorted(((k[6:], v) for k, v in a.items() if k.startswith("other:")), key=lambda kv: -kv[1])[:5]
         print(" " * 18 + "rest: " + ", ".join(f"{k} {v / 1e3:.1f}" for k, v in top))
+    if async_per_round:
+        print("k_b_async per round (round, U, us): first 16 and every 25th")
+        sel = async_per_round[:16] + async_per_round[16::25]
+        print("  " + "  ".join(f"{i}:{u}:{d:.0f}" for i, u, d in sel))
+        ds = sorted(d for _, _, d in async_per_round)
+        q = lambda f: ds[min(len(ds) - 1, int(f * len(ds)))]
+        print(f"  k_b_async us: p10 {q(0.1):.0f} p50 {q(0.5):.0f} p90 {q(0.9):.0f} max {ds[-1]:.0f}; "
+              f"us per U item (U >= 1e4): {statistics.median([d / u for _, u, d in async_per_round if u >= 1e4] or [0]):.4f}")
 
 
 if __name__ == "__main__":

@@ -67,7 +67,7 @@ case ${1:-} in
   #    path (variants/bidle: -DGC_B_IDLE_ACQ=1): stale lines kept alive by the pollers?
   n) exec_steps=(env:GC_LIB_PATH=variants/bidle/libgcolor.so "py:tools/b_cliff_probe.py" env:GC_LIB_PATH=
                  env:AB_VARIANT=B "abl:rmat24:3:2:base=-,bidle=variants/bidle/libgcolor.so" env:AB_VARIANT=
-                 "abl:rmat24:4:2:base=-,aidle=variants/abidle/libgcolor.so") ;;
+                 "abl:rmat24:4:2:base=-,aidle=variants/abidle/libgcolor.so" brounds:rmat24) ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
