@@ -1635,12 +1635,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
             if (np == 0) break;
             if ((stop = gc_async_stop(c, par, t0, budget))) break;
             if (np == before) {
-                if (++idle > 2) {
-#ifdef GC_A_IDLE_ACQ  // (experiment: invalidate this XCD's non-coherent lines before polling again)
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-                    __builtin_amdgcn_s_sleep(2);
-                }
+                if (++idle > 2) __builtin_amdgcn_s_sleep(2);
             } else {
                 idle = 0;
             }
@@ -1695,12 +1690,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         if (nh == 0) break;
         if ((stop = gc_async_stop(c, par, t0, budget))) break;
         if (nh == before) {
-            if (++idle > 2) {
-#ifdef GC_A_IDLE_ACQ
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-                __builtin_amdgcn_s_sleep(2);
-            }
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
         } else {
             idle = 0;
         }

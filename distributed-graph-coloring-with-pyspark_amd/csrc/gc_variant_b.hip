@@ -520,6 +520,14 @@ __device__ __forceinline__ bool b_async_stop(DevCtl* c, ull t0, long long budget
     return __shfl(stop, 0, GC_WAVE) != 0;
 }
 
+#ifdef GC_B_PROF
+// (diagnostic build, -DGC_B_PROF: per round, the fold's slowest wave and its work; read by
+// gc_b_prof_dump at the end of the colouring, GC_B_PROF_OUT=path)
+#define GC_B_PROF_ROUNDS 4096
+#define GC_B_PROF_K 10
+__device__ ull gc_bprof[GC_B_PROF_ROUNDS][GC_B_PROF_K];
+#endif
+
 // a work item is v | kind << GC_BI_SHIFT (kind 0 admission, 2 eviction time): non-negative
 // for n < 2^29 (-1 marks an empty lane), so the host runs k_b_async only below that
 #define GC_BI_SHIFT 29
@@ -554,7 +562,7 @@ struct BAsyncLds {  // one wave's rows
 // one pass over the wave's light admission / eviction items l1[0, n1); the unsettled ones
 // are compacted to the front (an admitted vertex comes back as an eviction item); returns
 // their number
-__device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s) {
+__device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, ull* scanned) {
     const int lane = gc_lane();
     int nw = 0;
     for (int c0 = 0; c0 < n1; c0 += GC_WAVE) {
@@ -594,6 +602,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         const int incl = gc_wave_incl_scan(len);
         const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
+        *scanned += (ull)total;
         gc_wave_sync();
         b_chunk_edges(
             s.src, excl, total,
@@ -657,7 +666,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
 // lanes over its row from the cursor, GC_HUB_UNR entries each in flight): a refusing entry
 // settles it OUT, the first undecided entry is its new cursor, the end of the row admits it
 // (appended to l1 as an eviction item at *n1).  Returns the heavy items left.
-__device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, int* ev) {
+__device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, int* ev, ull* scanned) {
     const int lane = gc_lane();
     int nw = 0;
     for (int i = 0; i < n2; ++i) {
@@ -688,6 +697,7 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
                 if (mb && pend < 0) pend = pos + k * GC_WAVE + __builtin_ctzll(mb);
             }
             pos += GC_HUB_UNR * GC_WAVE;
+            *scanned += GC_HUB_UNR * GC_WAVE;
         }
         if (refused) {
             if (lane == 0) gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
@@ -757,23 +767,47 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
     gc_wave_sync();
     bool stop = false;
     int idle = 0;
+    ull lscan = 0, hscan = 0, npass = 0, htime = 0;
+    const int h0 = n2, items0 = n1 + n2;
     while (n1 + n2 > 0) {
         const int before = n1 + n2;
-        n1 = b_async_chunk_pass(g, B, l1, n1, ev, s_w[w]);
-        if (n2) n2 = b_async_heavy_pass(g, l2, n2, l1, &n1, ev);
+        ++npass;
+        n1 = b_async_chunk_pass(g, B, l1, n1, ev, s_w[w], &lscan);
+        if (n2) {
+#ifdef GC_B_PROF
+            const ull th = wall_clock64();
+#endif
+            n2 = b_async_heavy_pass(g, l2, n2, l1, &n1, ev, &hscan);
+#ifdef GC_B_PROF
+            htime += wall_clock64() - th;
+#endif
+        }
         if (n1 + n2 == 0) break;
         if ((stop = b_async_stop(c, t0, budget))) break;
         if (n1 + n2 == before) {
-            if (++idle > 2) {
-#ifdef GC_B_IDLE_ACQ  // (experiment: invalidate this XCD's non-coherent lines before polling again)
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-                __builtin_amdgcn_s_sleep(2);
-            }
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
         } else {
             idle = 0;
         }
     }
+#ifdef GC_B_PROF
+    if (lane == 0 && c->round < GC_B_PROF_ROUNDS) {
+        ull* r = gc_bprof[c->round];
+        const ull wall = wall_clock64() - t0;
+        atomicMax(r + 0, wall);
+        atomicMax(r + 1, htime);
+        atomicMax(r + 2, npass);
+        atomicAdd(r + 3, npass);
+        atomicAdd(r + 4, (ull)h0);
+        atomicMax(r + 5, (ull)items0);
+        atomicMax(r + 6, lscan + hscan);
+        atomicMax(r + 7, hscan);
+        atomicMax(r + 8, (wall << 24) | (npass < (1u << 24) ? npass : (1u << 24) - 1));
+        atomicMax(r + 9, (wall << 24) | ((htime >> 4) < (1u << 24) ? (htime >> 4) : (1u << 24) - 1));
+    }
+#else
+    (void)lscan; (void)hscan; (void)npass; (void)htime; (void)h0; (void)items0;
+#endif
     if (!stop) return;
     // hand the unsettled items to the host's passes (slot ws), by kind
     for (int i0 = 0; i0 < n1; i0 += GC_WAVE) {
@@ -994,6 +1028,24 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     if (colors_out) GC_HIP(hipMemcpyAsync(colors_out, g->color, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
     if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
     if ((rc = R.sync())) return rc;
+#ifdef GC_B_PROF
+    if (const char* pp = getenv("GC_B_PROF_OUT")) {  // append this colouring's per-round records
+        static ull hb[GC_B_PROF_ROUNDS][GC_B_PROF_K];
+        GC_HIP(hipMemcpyFromSymbol(hb, HIP_SYMBOL(gc_bprof), sizeof(hb)));
+        if (FILE* f = fopen(pp, "a")) {
+            fprintf(f, "# colouring: %zu rounds; per round: U wall_us heavy_us max_passes sum_passes heavy_items max_items "
+                    "max_scanned max_heavy_scanned slowest_passes slowest_heavy_us\n", recs.size());
+            for (size_t i = 0; i < recs.size() && i < GC_B_PROF_ROUNDS; ++i) {
+                const ull* r = hb[i];
+                fprintf(f, "%zu %lld %.1f %.1f %llu %llu %llu %llu %llu %llu %llu %.1f\n", i, recs[i].U, r[0] / 100.0,
+                        r[1] / 100.0, r[2], r[3], r[4], r[5], r[6], r[7], r[8] & 0xFFFFFF, (r[9] & 0xFFFFFF) * 16 / 100.0);
+            }
+            fclose(f);
+        }
+        static ull z[GC_B_PROF_ROUNDS][GC_B_PROF_K];
+        GC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(gc_bprof), z, sizeof(z)));
+    }
+#endif
     if (st) {
         kt.collect();
         float ms = 0.f;

@@ -68,6 +68,10 @@ case ${1:-} in
   n) exec_steps=(env:GC_LIB_PATH=variants/bidle/libgcolor.so "py:tools/b_cliff_probe.py" env:GC_LIB_PATH=
                  env:AB_VARIANT=B "abl:rmat24:3:2:base=-,bidle=variants/bidle/libgcolor.so" env:AB_VARIANT=
                  "abl:rmat24:4:2:base=-,aidle=variants/abidle/libgcolor.so" brounds:rmat24) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n" >&2; exit 2 ;;
+  # o: variant B's fold, per round: the slowest wave's time, passes and heavy-row time
+  #    (variants/bprof: -DGC_B_PROF=1) on R-MAT-24
+  o) exec_steps=(env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05o/bprof_rmat24.txt
+                 "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05o/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
