@@ -720,6 +720,180 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
     return nw;
 }
 
+// Resident form of a wave's fold, once its unsettled items fit one chunk (at most 64 light
+// items, no heavy one) and their entries fit the wave's LDS (GC_B_RES_CAP): each lane keeps its
+// item's words in registers and its pending (admission) or kept (eviction) entries in LDS, so
+// a pass is the entries' state gathers alone (k8[u]; ev[u] and k8[ev[u]] for an admitted u) --
+// a chunk pass first re-reads the list, the item's words and the entries from memory, and in
+// the deep rounds every hop of the fold's dependency chain waits for one such pass
+// (profiles/r05/o: ~4.5 us a pass, 100-300 passes a round).  The decisions are b_async_chunk_pass's.
+// Region of a lane: max(its entries now, the eviction range it may need once admitted).  The
+// stop check runs only on a pass without progress.  Returns -1 (not eligible: nothing
+// changed), 0 (every item settled) or the items left on a stop, written back in the global
+// form (l1, lcur, pend) for the hand-off.
+#ifndef GC_B_RES_CAP
+#define GC_B_RES_CAP 1536
+#endif
+__device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, int* pe, DevCtl* c,
+                                ull t0, long long budget, bool* stop, ull* npass) {
+    const int lane = gc_lane();
+    const int it0 = lane < n1 ? l1[lane] : -1;
+    int v = it0 >= 0 ? (it0 & GC_BI_MASK) : -1;
+    int kind = it0 >= 0 ? (it0 >> GC_BI_SHIFT) : -1;
+    unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte: only this wave writes it
+    const int d = v >= 0 ? g.deg[v] : 0;
+    const int lo = v >= 0 ? g.nlow[v] : 0;
+    const int lc = v >= 0 ? g.lcur[v] : 0;
+    const long long r0 = v >= 0 ? g.rp[v] : 0;
+    bool evcol = kind == 2 && lc == GC_B_EVCOL;
+    int np = (v >= 0 && !evcol) ? -lc - 1 : 0;
+    int evv = (kind == 2 && !evcol) ? ev[v] : -1;  // own eviction time (only this wave writes it)
+    const bool bad = kind == 0 && lc >= 0;          // first admission scan not done
+    const int need = kind == 0 ? max(np, d - lo) : (evcol ? d - lo : np);
+    const int incl = gc_wave_incl_scan(need);
+    const int off = incl - need;
+    if (__ballot(bad) || __shfl(incl, GC_WAVE - 1, GC_WAVE) > GC_B_RES_CAP) return -1;
+    // the entries into LDS (flat over the wave's lanes)
+    {
+        const int pin = gc_wave_incl_scan(np);
+        const int pex = pin - np;
+        const int ptot = __shfl(pin, GC_WAVE - 1, GC_WAVE);
+        s.src[lane] = B.pend + r0;
+        s.np[lane] = off;
+        gc_wave_sync();
+        for (int b0 = 0; b0 < ptot; b0 += GC_WAVE) {  // every lane runs gc_owner
+            const int e = b0 + lane;
+            const int o = gc_owner(pex, e < ptot ? e : 0);
+            const int x = e - __shfl(pex, o, GC_WAVE);
+            if (e < ptot) pe[s.np[o] + x] = s.src[o][x];
+        }
+        gc_wave_sync();
+    }
+    const unsigned c6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+    const int cv = v >= 0 ? b_cand(g, v, kv) : -1;
+    int n = __popcll(__ballot(v >= 0));
+    int idle = 0;
+    while (n > 0) {
+        ++*npass;
+        int watch = 0;  // eviction items: 1 still pending, 2 final, no scan
+        if (kind == 2 && !evcol) {
+            const unsigned st = gc_k8_state(gc_ald8(g.k8 + evv));
+            watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
+        }
+        int len = 0;
+        if (kind == 0 || (kind == 2 && !evcol && watch == 0)) {
+            len = np;
+            s.src[lane] = pe + off;
+        } else if (kind == 2 && evcol) {
+            len = d - lo;
+            s.src[lane] = g.col + r0 + lo;
+        }
+        s.dst[lane] = pe + off;
+        s.flag[lane] = 0;
+        s.np[lane] = 0;
+        s.minv[lane] = GC_B_INF;
+        s.v[lane] = v;
+        s.d[lane] = d;
+        s.c6[lane] = c6;
+        s.cv[lane] = cv;
+        s.kind[lane] = kind;
+        const int li = gc_wave_incl_scan(len);
+        const int le = li - len;
+        const int total = __shfl(li, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        b_chunk_edges(
+            s.src, le, total,
+            [&](int o, int um) {
+                const int u = um & 0x7FFFFFFF;
+                const ull k = (ull)gc_ald8(g.k8 + u);
+                return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
+            },
+            [&](int o, int um, ull du, int) {
+                const int u = um & 0x7FFFFFFF;
+                const unsigned ku = (unsigned)du & 0xFFu;
+                if (s.kind[o] == 0) {
+                    const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
+                    if (f) atomicOr(&s.flag[o], f);
+                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                } else {
+                    if (gc_k8_state(ku) == GC_JP_OUT) return;
+                    if (!((unsigned)um & GC_B_PMARK)) {
+                        if (u <= s.v[o] || (int)(du >> 32) <= s.d[o]) return;
+                        if (!b_same(g, u, ku, s.c6[o], s.cv[o])) return;
+                    }
+                    atomicMin(&s.minv[o], u);
+                    s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
+                }
+            });
+        gc_wave_sync();
+        bool keep = false;
+        if (kind == 0) {
+            const unsigned f = s.flag[lane];
+            if (f & 1u) {
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
+            } else if (f & 2u) {
+                np = s.np[lane];
+                keep = true;
+            } else {  // admitted: its eviction time next (the row's higher-rank part first)
+                kv = (kv & ~3u) | GC_JP_IN;
+                gc_ast8(g.k8 + v, kv);
+                kind = 2;
+                evcol = true;
+                np = 0;
+                keep = true;
+            }
+        } else if (kind == 2) {
+            if (watch == 1) {
+                keep = true;
+            } else if (watch == 0) {
+                const int e = s.minv[lane];
+                gc_asti(ev + v, e);
+                evv = e;
+                evcol = false;
+                np = s.np[lane];
+                keep = e != GC_B_INF && gc_k8_state(gc_ald8(g.k8 + e)) != GC_JP_IN;
+            }
+        }
+        if (!keep) {
+            v = -1;
+            kind = -1;
+        }
+        const int nn = __popcll(__ballot(keep));
+        gc_wave_sync();
+        if (nn == 0) return 0;
+        if (nn == n) {
+            if ((*stop = b_async_stop(c, t0, budget))) {
+                n = nn;
+                break;
+            }
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+        } else {
+            idle = 0;
+        }
+        n = nn;
+    }
+    // stopped: back to the global form -- cursor words, entries, the item list
+    if (v >= 0) g.lcur[v] = evcol ? GC_B_EVCOL : -np - 1;
+    {
+        const int pin = gc_wave_incl_scan(v >= 0 ? np : 0);
+        const int pex = pin - (v >= 0 ? np : 0);
+        const int ptot = __shfl(pin, GC_WAVE - 1, GC_WAVE);
+        s.dst[lane] = B.pend + r0;
+        s.np[lane] = off;
+        gc_wave_sync();
+        for (int b0 = 0; b0 < ptot; b0 += GC_WAVE) {
+            const int e = b0 + lane;
+            const int o = gc_owner(pex, e < ptot ? e : 0);
+            const int x = e - __shfl(pex, o, GC_WAVE);
+            if (e < ptot) s.dst[o][x] = pe[s.np[o] + x];
+        }
+    }
+    const ull km = __ballot(v >= 0);
+    if (v >= 0) l1[__popcll(km & gc_lanemask_lt())] = v | (kind << GC_BI_SHIFT);
+    gc_wave_sync();
+    return __popcll(km);
+}
+
 // pass `pass` of the round as one asynchronous launch: reads the three lists of slot
 // pass % 3, spills to slot (pass + 1) % 3, uses the arrays of slot (pass + 2) % 3 as the
 // waves' scratch and clears that slot's counts (as k_b_ev does)
@@ -732,6 +906,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
     if (c->halt) return;
     const int rs = pass % 3, ws = (pass + 1) % 3, zs = (pass + 2) % 3;
     __shared__ BAsyncLds s_w[GC_WAVES_PER_BLOCK];
+    __shared__ int s_pe[GC_WAVES_PER_BLOCK][GC_B_RES_CAP];
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const long long nA = (long long)*b_cnt(c, 0, rs), nH = (long long)*b_cnt(c, 1, rs), nE = (long long)*b_cnt(c, 2, rs);
@@ -767,6 +942,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
     gc_wave_sync();
     bool stop = false;
     int idle = 0;
+    int res_fail = GC_WAVE + 1;
+    const bool use_res = g.b_resident != 0;
     ull lscan = 0, hscan = 0, npass = 0, htime = 0;
     const int h0 = n2, items0 = n1 + n2;
     while (n1 + n2 > 0) {
@@ -788,6 +965,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
             if (++idle > 2) __builtin_amdgcn_s_sleep(2);
         } else {
             idle = 0;
+        }
+        if (use_res && n2 == 0 && n1 <= GC_WAVE && n1 < res_fail) {
+            const int r = b_async_resident(g, B, l1, n1, ev, s_w[w], s_pe[w], c, t0, budget, &stop, &npass);
+            if (r >= 0) {
+                n1 = r;
+                break;  // settled, or stopped with the items written back
+            }
+            res_fail = n1;  // retried once fewer items are left
         }
     }
 #ifdef GC_B_PROF
@@ -872,6 +1057,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     if ((rc = gc_hubs_prepare(g, R.d))) return rc;
     R.d.hub_w = 0;  // bitmaps only: the fold has no hub JP
     R.d.tail_hmax = GC_TAIL_HMAX;
+    // the asynchronous fold's resident form (b_async_resident); GC_B_RESIDENT=0 off
+    R.d.b_resident = getenv("GC_B_RESIDENT") ? atoi(getenv("GC_B_RESIDENT")) : 1;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
