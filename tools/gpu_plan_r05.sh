@@ -76,7 +76,7 @@ case ${1:-} in
   #    LDS): variant B parity (golden, oracle, C3 full size), the A/B against GC_B_RESIDENT=0, the
   #    per-round profile again
   p) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3" file:tests/test_gpu_parity.py
-                 env:AB_VARIANT=B ab:rmat24:4:base,nores=GC_B_RESIDENT:0 env:AB_VARIANT=
+                 env:AB_VARIANT=B ab:rmat24:4:base,nores=GC_B_RESIDENT:0,k1=GC_B_ASYNC_K:1 env:AB_VARIANT=
                  env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05p/bprof_rmat24.txt
                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05p/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
   *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p" >&2; exit 2 ;;
