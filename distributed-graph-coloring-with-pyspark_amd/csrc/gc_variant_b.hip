@@ -524,7 +524,7 @@ __device__ __forceinline__ bool b_async_stop(DevCtl* c, ull t0, long long budget
 // (diagnostic build, -DGC_B_PROF: per round, the fold's slowest wave and its work; read by
 // gc_b_prof_dump at the end of the colouring, GC_B_PROF_OUT=path)
 #define GC_B_PROF_ROUNDS 4096
-#define GC_B_PROF_K 10
+#define GC_B_PROF_K 12
 __device__ ull gc_bprof[GC_B_PROF_ROUNDS][GC_B_PROF_K];
 #endif
 
@@ -735,7 +735,7 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
 #define GC_B_RES_CAP 1536
 #endif
 __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, int* pe, DevCtl* c,
-                                ull t0, long long budget, bool* stop, ull* npass) {
+                                ull t0, long long budget, bool* stop, ull* npass, ull* scanned) {
     const int lane = gc_lane();
     const int it0 = lane < n1 ? l1[lane] : -1;
     int v = it0 >= 0 ? (it0 & GC_BI_MASK) : -1;
@@ -800,6 +800,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         const int li = gc_wave_incl_scan(len);
         const int le = li - len;
         const int total = __shfl(li, GC_WAVE - 1, GC_WAVE);
+        *scanned += (ull)total;
         gc_wave_sync();
         b_chunk_edges(
             s.src, le, total,
@@ -967,7 +968,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
             idle = 0;
         }
         if (use_res && n2 == 0 && n1 <= GC_WAVE && n1 < res_fail) {
-            const int r = b_async_resident(g, B, l1, n1, ev, s_w[w], s_pe[w], c, t0, budget, &stop, &npass);
+            const int r = b_async_resident(g, B, l1, n1, ev, s_w[w], s_pe[w], c, t0, budget, &stop, &npass, &lscan);
             if (r >= 0) {
                 n1 = r;
                 break;  // settled, or stopped with the items written back
@@ -989,6 +990,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
         atomicMax(r + 7, hscan);
         atomicMax(r + 8, (wall << 24) | (npass < (1u << 24) ? npass : (1u << 24) - 1));
         atomicMax(r + 9, (wall << 24) | ((htime >> 4) < (1u << 24) ? (htime >> 4) : (1u << 24) - 1));
+        atomicAdd(r + 10, lscan + hscan);
+        atomicAdd(r + 11, wall);
     }
 #else
     (void)lscan; (void)hscan; (void)npass; (void)htime; (void)h0; (void)items0;
@@ -1221,11 +1224,12 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         GC_HIP(hipMemcpyFromSymbol(hb, HIP_SYMBOL(gc_bprof), sizeof(hb)));
         if (FILE* f = fopen(pp, "a")) {
             fprintf(f, "# colouring: %zu rounds; per round: U wall_us heavy_us max_passes sum_passes heavy_items max_items "
-                    "max_scanned max_heavy_scanned slowest_passes slowest_heavy_us\n", recs.size());
+                    "max_scanned max_heavy_scanned slowest_passes slowest_heavy_us sum_scanned sum_wall_us\n", recs.size());
             for (size_t i = 0; i < recs.size() && i < GC_B_PROF_ROUNDS; ++i) {
                 const ull* r = hb[i];
-                fprintf(f, "%zu %lld %.1f %.1f %llu %llu %llu %llu %llu %llu %llu %.1f\n", i, recs[i].U, r[0] / 100.0,
-                        r[1] / 100.0, r[2], r[3], r[4], r[5], r[6], r[7], r[8] & 0xFFFFFF, (r[9] & 0xFFFFFF) * 16 / 100.0);
+                fprintf(f, "%zu %lld %.1f %.1f %llu %llu %llu %llu %llu %llu %llu %.1f %llu %.1f\n", i, recs[i].U,
+                        r[0] / 100.0, r[1] / 100.0, r[2], r[3], r[4], r[5], r[6], r[7], r[8] & 0xFFFFFF,
+                        (r[9] & 0xFFFFFF) * 16 / 100.0, r[10], r[11] / 100.0);
             }
             fclose(f);
         }
