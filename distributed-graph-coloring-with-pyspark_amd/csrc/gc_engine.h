@@ -87,6 +87,7 @@ struct gc_graph {
     bool bpart = false;        // low parts also split by degree (variant B: equal-degree entries last, neq counts them)
     int* neq = nullptr;
     int* bpend = nullptr;      // variant B's pending entries (nnz ints, gc_color_variant_b allocates it)
+    int* bwatch = nullptr;     // variant B: each undecided vertex's watched pending entry (n ints, likewise)
     int* hpl = nullptr;        // hubs-off heavy JP pending lists (gc_alloc_heavy_pending), nnz + n ints
     int* hplc = nullptr;
     uint64_t part_seed = 0;

@@ -99,6 +99,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_fail0(GDev g, GLists L) {
 struct BLists {
     int* l[3][3];  // [kind][slot]
     int* pend;     // nnz ints: each listed light vertex's still-pending entries, at rp[v] (see below)
+    int* watch;    // n ints: an undecided vertex's smallest pending entry at its last scan (asynchronous fold)
 };
 // Pending entries (round 4).  A flag that reads 0 is final (a later arrival, a refused or
 // other-candidate vertex, an eviction before v), so after its first scan a light vertex only
@@ -562,7 +563,13 @@ struct BAsyncLds {  // one wave's rows
 // one pass over the wave's light admission / eviction items l1[0, n1); the unsettled ones
 // are compacted to the front (an admitted vertex comes back as an eviction item); returns
 // their number
-__device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, ull* scanned) {
+// Watched entries (g.b_watch = R > 0): an admission item's full rescan of its pending entries
+// waits until the smallest of them (B.watch[v], the entry the fold most likely settles first)
+// settles, or every R-th pass of the wave -- between those, a pass checks that one entry.
+// Refusals by other entries are only seen later; the decisions are the same.
+__device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, ull* scanned,
+                                  ull npass) {
+    const bool full_pass = g.b_watch <= 0 || npass % (ull)g.b_watch == 0;
     const int lane = gc_lane();
     int nw = 0;
     for (int c0 = 0; c0 < n1; c0 += GC_WAVE) {
@@ -578,8 +585,13 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + ev[v]));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
+        bool held = false;  // admission item whose watched entry is still pending: no rescan
+        if (kind == 0 && lc < 0 && !full_pass) {
+            const int wu = B.watch[v];
+            held = wu >= 0 && wu < g.n && b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), gc_k8_cand(kv), b_cand(g, v, kv), ev) == 2u;
+        }
         int len = 0;
-        if (kind == 0) {
+        if (kind == 0 && !held) {
             len = lc >= 0 ? d - lc : -lc - 1;
             s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0;
         } else if (kind == 2 && lc == GC_B_EVCOL) {
@@ -617,7 +629,10 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
                 if (s.kind[o] == 0) {  // admission (k_b_adm)
                     const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
                     if (f) atomicOr(&s.flag[o], f);
-                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                    if (f == 2u) {
+                        s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                        atomicMin(&s.minv[o], u);
+                    }
                 } else {  // eviction time (k_b_ev)
                     if (gc_k8_state(ku) == GC_JP_OUT) return;
                     if (!((unsigned)um & GC_B_PMARK)) {
@@ -630,12 +645,15 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             });
         gc_wave_sync();
         int keep = -1;  // the item that stays (-1: settled)
-        if (kind == 0) {
+        if (kind == 0 && held) {
+            keep = it;
+        } else if (kind == 0) {
             const unsigned f = s.flag[lane];
             if (f & 1u) {
                 gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
             } else if (f & 2u) {
                 g.lcur[v] = -s.np[lane] - 1;
+                if (g.b_watch > 0) B.watch[v] = s.minv[lane];
                 keep = it;
             } else {
                 g.lcur[v] = GC_B_EVCOL;
@@ -773,15 +791,19 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
     const int cv = v >= 0 ? b_cand(g, v, kv) : -1;
     int n = __popcll(__ballot(v >= 0));
     int idle = 0;
+    int wu = (kind == 0 && g.b_watch > 0) ? B.watch[v] : -1;  // admission items: the watched entry
     while (n > 0) {
         ++*npass;
+        bool held = false;
+        if (kind == 0 && wu >= 0 && wu < g.n && g.b_watch > 0 && *npass % (ull)g.b_watch != 0)
+            held = b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), c6, cv, ev) == 2u;
         int watch = 0;  // eviction items: 1 still pending, 2 final, no scan
         if (kind == 2 && !evcol) {
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + evv));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
         int len = 0;
-        if (kind == 0 || (kind == 2 && !evcol && watch == 0)) {
+        if ((kind == 0 && !held) || (kind == 2 && !evcol && watch == 0)) {
             len = np;
             s.src[lane] = pe + off;
         } else if (kind == 2 && evcol) {
@@ -815,7 +837,10 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                 if (s.kind[o] == 0) {
                     const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
                     if (f) atomicOr(&s.flag[o], f);
-                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                    if (f == 2u) {
+                        s.dst[o][atomicAdd(&s.np[o], 1)] = u;
+                        atomicMin(&s.minv[o], u);
+                    }
                 } else {
                     if (gc_k8_state(ku) == GC_JP_OUT) return;
                     if (!((unsigned)um & GC_B_PMARK)) {
@@ -828,12 +853,15 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
             });
         gc_wave_sync();
         bool keep = false;
-        if (kind == 0) {
+        if (kind == 0 && held) {
+            keep = true;
+        } else if (kind == 0) {
             const unsigned f = s.flag[lane];
             if (f & 1u) {
                 gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
             } else if (f & 2u) {
                 np = s.np[lane];
+                wu = s.minv[lane];
                 keep = true;
             } else {  // admitted: its eviction time next (the row's higher-rank part first)
                 kv = (kv & ~3u) | GC_JP_IN;
@@ -873,8 +901,9 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         }
         n = nn;
     }
-    // stopped: back to the global form -- cursor words, entries, the item list
+    // stopped: back to the global form -- cursor words, watched entries, entries, the item list
     if (v >= 0) g.lcur[v] = evcol ? GC_B_EVCOL : -np - 1;
+    if (kind == 0 && g.b_watch > 0) B.watch[v] = wu;
     {
         const int pin = gc_wave_incl_scan(v >= 0 ? np : 0);
         const int pex = pin - (v >= 0 ? np : 0);
@@ -950,7 +979,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
     while (n1 + n2 > 0) {
         const int before = n1 + n2;
         ++npass;
-        n1 = b_async_chunk_pass(g, B, l1, n1, ev, s_w[w], &lscan);
+        n1 = b_async_chunk_pass(g, B, l1, n1, ev, s_w[w], &lscan, npass);
         if (n2) {
 #ifdef GC_B_PROF
             const ull th = wall_clock64();
@@ -1062,6 +1091,9 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     R.d.tail_hmax = GC_TAIL_HMAX;
     // the asynchronous fold's resident form (b_async_resident); GC_B_RESIDENT=0 off
     R.d.b_resident = getenv("GC_B_RESIDENT") ? atoi(getenv("GC_B_RESIDENT")) : 1;
+    // watched entries (b_async_chunk_pass): a full admission rescan every GC_B_WATCH-th pass at most
+    // otherwise; 0 off
+    R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 8;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;
@@ -1125,6 +1157,11 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     for (int k = 0; k < 9; ++k) B.l[k / 3][k % 3] = wl[k];
     if (!g->bpend && g->nnz > 0) GC_HIP(gc_dmalloc((void**)&g->bpend, sizeof(int) * (size_t)g->nnz));
     B.pend = g->bpend;
+    if (!g->bwatch && g->n > 0) {
+        GC_HIP(gc_dmalloc((void**)&g->bwatch, sizeof(int) * (size_t)g->n));
+        GC_HIP(hipMemsetAsync(g->bwatch, 0xFF, sizeof(int) * (size_t)g->n, s));  // -1: none
+    }
+    B.watch = g->bwatch;
     std::vector<RoundRec> recs;
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;

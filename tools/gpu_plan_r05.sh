@@ -79,6 +79,13 @@ case ${1:-} in
                  env:AB_VARIANT=B ab:rmat24:4:base,nores=GC_B_RESIDENT:0,k1=GC_B_ASYNC_K:1 env:AB_VARIANT=
                  env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05p/bprof_rmat24.txt
                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05p/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p" >&2; exit 2 ;;
+  # q: watched admission entries (a full rescan only when the smallest pending entry settles, or
+  #    every GC_B_WATCH-th pass; profiles/r05/p: 21.8 G entries scanned per R-MAT-24 colouring):
+  #    parity, the A/B over GC_B_WATCH, the per-round profile
+  q) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_parity.py
+                 env:AB_VARIANT=B ab:rmat24:4:base,w0=GC_B_WATCH:0,w4=GC_B_WATCH:4,w32=GC_B_WATCH:32 env:AB_VARIANT=
+                 env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05q/bprof_rmat24.txt
+                 "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05q/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
