@@ -86,6 +86,7 @@ struct gc_graph {
     uint64_t hub_seed = 0;
     bool bpart = false;        // low parts also split by degree (variant B: equal-degree entries last, neq counts them)
     int* neq = nullptr;
+    int* nhe = nullptr;        // per row: its entries of higher degree and earlier position (variant B's admission range end, gc_prep.hip)
     int* bpend = nullptr;      // variant B's pending entries (nnz ints, gc_color_variant_b allocates it)
     int* bwatch = nullptr;     // variant B: each undecided vertex's watched pending entry (n ints, likewise)
     int* hpl = nullptr;        // hubs-off heavy JP pending lists (gc_alloc_heavy_pending), nnz + n ints

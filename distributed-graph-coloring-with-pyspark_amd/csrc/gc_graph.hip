@@ -184,7 +184,7 @@ void gc_free_all(gc_graph* g) {
     }
     void* ptrs[] = {g->rp, g->col, g->deg, g->color, g->cround, g->cand, g->c8, g->c4, g->k8, g->nlow, g->inF, g->mark, g->F[0],
                     g->F[1], g->heavy, g->wide, g->undL[0], g->undL[1], g->undL[2], g->undH[0], g->undH[1],
-                    g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->lcur, g->neq, g->bpend, g->bwatch, g->hpl, g->hplc, g->bstat, g->accs, g->bigw, g->rec, g->fsum, g->ctl};
+                    g->undH[2], g->seeds[0], g->seeds[1], g->ulist, g->parent, g->best, g->vcolors, g->lcur, g->neq, g->nhe, g->bpend, g->bwatch, g->hpl, g->hplc, g->bstat, g->accs, g->bigw, g->rec, g->fsum, g->ctl};
     for (void* p : ptrs)
         if (p) gc_dfree(p);
     if (g->hctl) gc_dfree(g->hctl);
@@ -234,6 +234,7 @@ int gc_alloc_graph_common(gc_graph* g, const int* src) {
     const size_t n1 = (size_t)std::max<long long>(g->n, 1);
     GC_HIP(gc_dmalloc((void**)&g->nlow, sizeof(int) * n1));
     GC_HIP(gc_dmalloc((void**)&g->neq, sizeof(int) * n1));
+    GC_HIP(gc_dmalloc((void**)&g->nhe, sizeof(int) * n1));
     GC_HIP(gc_dmalloc((void**)&g->kb, n1));
     GC_HIP(hipMemsetAsync(g->ctl, 0, sizeof(DevCtl), s));
     if (g->n > 0)

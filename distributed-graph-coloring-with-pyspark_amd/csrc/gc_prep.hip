@@ -142,10 +142,13 @@ __device__ __forceinline__ unsigned f16(ull p, int c) { return (unsigned)((p >> 
 __device__ __forceinline__ ull pack3(unsigned a, unsigned b, unsigned c) {
     return (ull)a | ((ull)b << 16) | ((ull)c << 32);
 }
+__device__ __forceinline__ ull pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
+    return pack3(a, b, c) | ((ull)d << 48);
+}
 // counts of this thread's entries [0, x) per class, from its 16-bit class masks
-__device__ __forceinline__ ull own_before(unsigned m0, unsigned m1, unsigned m2, int x) {
+__device__ __forceinline__ ull own_before(unsigned m0, unsigned m1, unsigned m2, int x, unsigned m3 = 0u) {
     const unsigned lt = x >= 32 ? 0xFFFFFFFFu : ((1u << x) - 1u);
-    return pack3(__popc(m0 & lt), __popc(m1 & lt), __popc(m2 & lt));
+    return pack4(__popc(m0 & lt), __popc(m1 & lt), __popc(m2 & lt), __popc(m3 & lt));
 }
 
 // Tile rows into LDS: offsets relative to the first entry; returns R (rows) and sets *e_beg,
@@ -239,7 +242,7 @@ __device__ __forceinline__ int thread_entries(const Lds& S, int R, int NE, int* 
 // it; rows starting at or past NE get the total.  Then base[R] = total.
 template <class Lds>
 __device__ __forceinline__ void record_bases(Lds& S, int R, int NE, int nv, ull prefix, ull total, unsigned m0,
-                                             unsigned m1, unsigned m2) {
+                                             unsigned m1, unsigned m2, unsigned m3 = 0u) {
     const int j0 = threadIdx.x * GC_PER;
     if (nv > 0) {
         int lo = 0, hi = R;  // first r with off[r] >= j0
@@ -248,7 +251,7 @@ __device__ __forceinline__ void record_bases(Lds& S, int R, int NE, int nv, ull 
             if (S.off[mid] < j0) lo = mid + 1;
             else hi = mid;
         }
-        for (int r = lo; r < R && S.off[r] < j0 + nv; ++r) S.base[r] = prefix + own_before(m0, m1, m2, S.off[r] - j0);
+        for (int r = lo; r < R && S.off[r] < j0 + nv; ++r) S.base[r] = prefix + own_before(m0, m1, m2, S.off[r] - j0, m3);
     }
     for (int r = threadIdx.x; r <= R; r += blockDim.x)
         if (S.off[r] >= NE) S.base[r] = total;
@@ -265,6 +268,7 @@ struct PartArgs {
     const unsigned char* kb;
     int* nlow;
     int* neq;
+    int* nhe;
     ull seed;
     ull* bad;
     ull* seg_aux;       // per segment: packed class counts
@@ -283,20 +287,27 @@ __device__ __forceinline__ unsigned owner_key(const PartArgs& a, int prio, int v
 }
 
 // classes of this thread's entries against their owners' keys: 0 lower key, 1 equal key and
-// earlier position, 2 the rest (higher rank, self-loops, out-of-range entries)
+// earlier position, 2 higher key and earlier position, 3 the rest (equal key and later
+// position, higher key and later position, self-loops, out-of-range entries).  Classes 1 + 2
+// are the entries an arrival of the owner can be refused by in variant B's fold (earlier,
+// degree >= its own), class 3 holds the ones it can be evicted by (later, higher degree).
+// The seeded-priority partition (PRIO) has classes 0 and 3 only.
 template <int PRIO>
 __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u, const unsigned* kv, const int* v,
-                                         unsigned* m0, unsigned* m1, unsigned* m2, ull* nbad, unsigned* mh) {
-    int cls[GC_PER];
+                                         unsigned* m0, unsigned* m1, unsigned* m2, unsigned* m3, ull* nbad,
+                                         unsigned* mh) {
+    // the class masks are built directly (no per-entry class array: registers, occupancy)
+    unsigned a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     *mh = 0;
     if (PRIO) {
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
-            cls[k] = 3;
             if (k < nv) {
-                if ((unsigned)u[k] >= (unsigned)a.T.n) { cls[k] = 2; ++*nbad; continue; }
+                const unsigned bit = 1u << k;
+                if ((unsigned)u[k] >= (unsigned)a.T.n) { a3 |= bit; ++*nbad; continue; }
                 const unsigned ku = gc_prio_hash(a.seed, u[k]);
-                cls[k] = gc_rank_lt_key(ku, u[k], kv[k], v[k]) ? 0 : 2;
+                if (gc_rank_lt_key(ku, u[k], kv[k], v[k])) a0 |= bit;
+                else a3 |= bit;
             }
         }
     } else {
@@ -316,18 +327,26 @@ __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u
         const bool hf = a.hflag != nullptr;
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
-            cls[k] = 3;
             if (k < nv) {
-                if ((unsigned)u[k] >= (unsigned)a.T.n) { cls[k] = 2; ++*nbad; continue; }
+                const unsigned bit = 1u << k;
+                if ((unsigned)u[k] >= (unsigned)a.T.n) { a3 |= bit; ++*nbad; continue; }
                 const unsigned kv8 = gc_deg_code((long long)kv[k]);
-                if (kb8[k] != kv8) cls[k] = kb8[k] < kv8 ? 0 : 2;
-                else if (kv8 < GC_DEG_CODE_EXACT) cls[k] = u[k] < v[k] ? 1 : 2;
-                else fullm |= 1u << k;
+                const bool early = u[k] < v[k];
+                if (kb8[k] != kv8) {
+                    if (kb8[k] < kv8) a0 |= bit;
+                    else if (early) a2 |= bit;
+                    else a3 |= bit;
+                } else if (kv8 < GC_DEG_CODE_EXACT) {
+                    if (early) a1 |= bit;
+                    else a3 |= bit;
+                } else {
+                    fullm |= bit;
+                }
                 // hub entries (deg(u) > hub_t) from the same byte key: exact except in the
                 // code's bucket when it also holds degrees <= hub_t (R-MAT: few entries)
                 if (hf && kb8[k] >= hc) {
-                    if (kb8[k] > hc || !a.hub_amb) h |= 1u << k;
-                    else hamb |= 1u << k;
+                    if (kb8[k] > hc || !a.hub_amb) h |= bit;
+                    else hamb |= bit;
                 }
             }
         }
@@ -337,22 +356,22 @@ __device__ __forceinline__ void classify(const PartArgs& a, int nv, const int* u
             for (int k = 0; k < GC_PER; ++k) du[k] = ((fullm | hamb) >> k) & 1u ? (unsigned)a.deg[u[k]] : 0u;
 #pragma unroll
             for (int k = 0; k < GC_PER; ++k) {
-                if ((fullm >> k) & 1u) cls[k] = du[k] < kv[k] ? 0 : (du[k] > kv[k] ? 2 : (u[k] < v[k] ? 1 : 2));
-                if (((hamb >> k) & 1u) && du[k] > (unsigned)a.hub_t) h |= 1u << k;
+                const unsigned bit = 1u << k;
+                if (fullm & bit) {
+                    if (du[k] < kv[k]) a0 |= bit;
+                    else if (u[k] >= v[k]) a3 |= bit;
+                    else if (du[k] > kv[k]) a2 |= bit;
+                    else a1 |= bit;
+                }
+                if ((hamb & bit) && du[k] > (unsigned)a.hub_t) h |= bit;
             }
         }
         *mh = h;
     }
-    unsigned a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll
-    for (int k = 0; k < GC_PER; ++k) {
-        a0 |= (cls[k] == 0 ? 1u : 0u) << k;
-        a1 |= (cls[k] == 1 ? 1u : 0u) << k;
-        a2 |= (cls[k] == 2 ? 1u : 0u) << k;
-    }
     *m0 = a0;
     *m1 = a1;
     *m2 = a2;
+    *m3 = a3;
 }
 
 template <int PRIO>
@@ -374,24 +393,24 @@ __device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad
         kv[k] = S.key[rk[k]];
         vv[k] = r0 + rk[k];
     }
-    unsigned m0, m1, m2, mh;
-    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad, &mh);
-    const ull mine = pack3(__popc(m0), __popc(m1), __popc(m2));
+    unsigned m0, m1, m2, m3, mh;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, &m3, nbad, &mh);
+    const ull mine = pack4(__popc(m0), __popc(m1), __popc(m2), __popc(m3));
     ull total;
     const ull prefix = block_excl_scan(mine, S.w, &total);  // (its barriers: every S.buf read is done)
-    record_bases(S, R, NE, nv, prefix, total, m0, m1, m2);
+    record_bases(S, R, NE, nv, prefix, total, m0, m1, m2, m3);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < GC_PER; ++k) {
         if (k >= nv) break;
         const int r = rk[k];
         const ull b = S.base[r], b1 = S.base[r + 1];
-        const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1);
+        const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1), c2 = f16(b1, 2) - f16(b, 2);
         const unsigned bit = 1u << k;
-        const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : 2);
-        const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
+        const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : ((m2 & bit) ? 2 : 3));
+        const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : (c == 2 ? m2 : m3));
         const unsigned rank = f16(prefix, c) + __popc(mc & (bit - 1u)) - f16(b, c);
-        const unsigned start = c == 0 ? 0u : (c == 1 ? c0 : c0 + c1);
+        const unsigned start = c == 0 ? 0u : (c == 1 ? c0 : (c == 2 ? c0 + c1 : c0 + c1 + c2));
         // (a hub entry carries its flag in bit 31: vertex ids are < 2^31)
         S.buf[S.off[r] + (int)(start + rank)] = (int)((unsigned)u[k] | (((mh >> k) & 1u) << 31));
     }
@@ -411,6 +430,7 @@ __device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad
         const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1);
         a.nlow[r0 + r] = (int)(c0 + c1);
         if (a.neq) a.neq[r0 + r] = (int)c1;
+        if (a.nhe) a.nhe[r0 + r] = (int)(f16(b1, 2) - f16(b, 2));
     }
 }
 
@@ -435,16 +455,17 @@ __device__ void part_seg1(const PartArgs& a, TileLdsP& S, long long s, ull* nbad
         vv[k] = v;
         kv[k] = key;
     }
-    unsigned m0, m1, m2, mh;
-    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, nbad, &mh);
-    unsigned cls = 0;
+    unsigned m0, m1, m2, m3, mh;
+    classify<PRIO>(a, nv, u, kv, vv, &m0, &m1, &m2, &m3, nbad, &mh);
+    unsigned cls = 0;  // 2 bits per entry: its class
 #pragma unroll
-    for (int k = 0; k < GC_PER; ++k) cls |= (((m1 >> k) & 1u) | (((m2 >> k) & 1u) << 1)) << (2 * k);
+    for (int k = 0; k < GC_PER; ++k)
+        cls |= (((m1 >> k) & 1u) | (((m2 >> k) & 1u) << 1) | (((m3 >> k) & 1u) * 3u)) << (2 * k);
 #if GC_PART_HUBFLAG
     cls |= mh << 16;
 #endif
     a.seg_cls[s * GC_BLOCK + threadIdx.x] = cls;
-    const ull tot = block_sum(pack3(__popc(m0), __popc(m1), __popc(m2)), S.w);
+    const ull tot = block_sum(pack4(__popc(m0), __popc(m1), __popc(m2), __popc(m3)), S.w);
     if (threadIdx.x == 0) a.seg_aux[s] = tot;
 }
 
@@ -464,16 +485,18 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part1(PartArgs a) {
 
 // sums over segments [f, l) of a row's packed counts, per class (one wave, lane-strided)
 __device__ __forceinline__ void seg_sums(const ull* aux, long long f, long long l, ull* c) {
-    ull a0 = 0, a1 = 0, a2 = 0;
+    ull a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     for (long long i = f + gc_lane(); i < l; i += GC_WAVE) {
         const ull p = aux[i];
         a0 += f16(p, 0);
         a1 += f16(p, 1);
         a2 += f16(p, 2);
+        a3 += f16(p, 3);
     }
     c[0] = gc_wave_sum(a0);
     c[1] = gc_wave_sum(a1);
     c[2] = gc_wave_sum(a2);
+    c[3] = gc_wave_sum(a3);
 }
 
 // second pass of the heavy rows: every segment places its entries after the row's earlier
@@ -481,7 +504,7 @@ __device__ __forceinline__ void seg_sums(const ull* aux, long long f, long long 
 __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
     __shared__ int buf[GC_SEG];
     __shared__ ull s_w[GC_WAVES_PER_BLOCK];
-    __shared__ ull s_pre[3], s_tot[3];
+    __shared__ ull s_pre[4], s_tot[4];
     const long long ns = nseg_of(a.T);
     for (long long s = blockIdx.x; s < ns; s += gridDim.x) {
         const int v = a.T.seg_row[s], j = a.T.seg_j[s];
@@ -490,11 +513,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
         const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
         const long long first = s - j, nsr = (d + GC_SEG - 1) / GC_SEG;
         if (threadIdx.x < GC_WAVE) {
-            ull p[3], t[3];
+            ull p[4], t[4];
             seg_sums(a.seg_aux, first, s, p);
             seg_sums(a.seg_aux, first, first + nsr, t);
             if (threadIdx.x == 0)
-                for (int c = 0; c < 3; ++c) {
+                for (int c = 0; c < 4; ++c) {
                     s_pre[c] = p[c];
                     s_tot[c] = t[c];
                 }
@@ -511,7 +534,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
         const unsigned mh = 0u;
 #endif
         int u[GC_PER];
-        unsigned m0 = 0, m1 = 0, m2 = 0;
+        unsigned m0 = 0, m1 = 0, m2 = 0, m3 = 0;
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
             u[k] = k < nv ? buf[j0 + k] : 0;
@@ -520,30 +543,33 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
                 m0 |= (c == 0 ? 1u : 0u) << k;
                 m1 |= (c == 1 ? 1u : 0u) << k;
                 m2 |= (c == 2 ? 1u : 0u) << k;
+                m3 |= (c == 3 ? 1u : 0u) << k;
             }
         }
         ull segtot;
-        const ull prefix = block_excl_scan(pack3(__popc(m0), __popc(m1), __popc(m2)), s_w, &segtot);
-        const unsigned L0 = f16(segtot, 0), L1 = f16(segtot, 1);
+        const ull prefix = block_excl_scan(pack4(__popc(m0), __popc(m1), __popc(m2), __popc(m3)), s_w, &segtot);
+        const unsigned L0 = f16(segtot, 0), L1 = f16(segtot, 1), L2 = f16(segtot, 2);
         // compact the segment in LDS by class (u is in registers; block_excl_scan's barriers
         // ordered every read of buf before these writes)
 #pragma unroll
         for (int k = 0; k < GC_PER; ++k) {
             if (k >= nv) break;
             const unsigned bit = 1u << k;
-            const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : 2);
-            const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : m2);
-            const unsigned sec = c == 0 ? 0u : (c == 1 ? L0 : L0 + L1);
+            const int c = (m0 & bit) ? 0 : ((m1 & bit) ? 1 : ((m2 & bit) ? 2 : 3));
+            const unsigned mc = c == 0 ? m0 : (c == 1 ? m1 : (c == 2 ? m2 : m3));
+            const unsigned sec = c == 0 ? 0u : (c == 1 ? L0 : (c == 2 ? L0 + L1 : L0 + L1 + L2));
             buf[sec + f16(prefix, c) + __popc(mc & (bit - 1u))] = (int)((unsigned)u[k] | (((mh >> k) & 1u) << 31));
         }
         __syncthreads();
-        const long long T0 = (long long)s_tot[0], T1 = (long long)s_tot[1];
-        const long long P0 = (long long)s_pre[0], P1 = (long long)s_pre[1], P2 = (long long)s_pre[2];
+        const long long T0 = (long long)s_tot[0], T1 = (long long)s_tot[1], T2 = (long long)s_tot[2];
+        const long long P0 = (long long)s_pre[0], P1 = (long long)s_pre[1], P2 = (long long)s_pre[2],
+                        P3 = (long long)s_pre[3];
         for (int i = threadIdx.x; i < len; i += blockDim.x) {
             long long pos;
             if (i < (int)L0) pos = P0 + i;
             else if (i < (int)(L0 + L1)) pos = T0 + P1 + (i - (int)L0);
-            else pos = T0 + T1 + P2 + (i - (int)(L0 + L1));
+            else if (i < (int)(L0 + L1 + L2)) pos = T0 + T1 + P2 + (i - (int)(L0 + L1));
+            else pos = T0 + T1 + T2 + P3 + (i - (int)(L0 + L1 + L2));
             const unsigned x = (unsigned)buf[i];
             if (a.hflag) {
                 a.dst[rs + pos] = (int)(x & 0x7FFFFFFFu);
@@ -555,6 +581,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_part2(PartArgs a) {
         if (j == 0 && threadIdx.x == 0) {
             a.nlow[v] = (int)(T0 + T1);
             if (a.neq) a.neq[v] = (int)T1;
+            if (a.nhe) a.nhe[v] = (int)T2;
         }
         __syncthreads();
     }
@@ -942,6 +969,7 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
         if (g->n) {
             GC_HIP(hipMemsetAsync(g->nlow, 0, sizeof(int) * (size_t)g->n, g->stream));
             if (g->neq) GC_HIP(hipMemsetAsync(g->neq, 0, sizeof(int) * (size_t)g->n, g->stream));
+            if (g->nhe) GC_HIP(hipMemsetAsync(g->nhe, 0, sizeof(int) * (size_t)g->n, g->stream));
         }
         return GC_OK;
     }
@@ -955,6 +983,7 @@ int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed,
     a.kb = g->kb;
     a.nlow = g->nlow;
     a.neq = g->neq;
+    a.nhe = g->nhe;
     a.seed = (ull)seed;
     a.bad = bad;
     a.seg_aux = g->seg_aux;

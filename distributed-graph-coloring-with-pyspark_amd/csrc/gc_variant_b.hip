@@ -100,7 +100,15 @@ struct BLists {
     int* l[3][3];  // [kind][slot]
     int* pend;     // nnz ints: each listed light vertex's still-pending entries, at rp[v] (see below)
     int* watch;    // n ints: an undecided vertex's smallest pending entry at its last scan (asynchronous fold)
+    const int* nhe;  // n ints: the row's higher-degree earlier entries (gc_prep.hip's class 2)
 };
+// Row layout (the (deg, pos) rank partition, gc_prep.hip): [lower degree | equal degree and
+// earlier | higher degree and earlier | the rest (later positions of equal or higher degree)].
+// An arrival of v can only be refused by an earlier u with deg(u) >= deg(v): the admission
+// range [nlow[v] - neq[v], nlow[v] + nhe[v]).  v can only be evicted by a later u with
+// deg(u) > deg(v): the eviction range [nlow[v] + nhe[v], deg(v)) (its equal-degree entries
+// are skipped by their degree).
+__device__ __forceinline__ int b_adm_end(const GDev& g, const BLists& B, int v) { return g.nlow[v] + B.nhe[v]; }
 // Pending entries (round 4).  A flag that reads 0 is final (a later arrival, a refused or
 // other-candidate vertex, an eviction before v), so after its first scan a light vertex only
 // ever needs the entries that were still pending: each scan writes them, compacted, to
@@ -140,10 +148,7 @@ __device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl,
     }
 }
 
-// Row layout (the (deg, pos) rank partition, gc_prep.hip): [lower degree | equal degree,
-// earlier | higher rank].  The admission of v can only be blocked by an earlier u with
-// deg(u) >= deg(v): the entries from nlow[v] - neq[v] on.  An evictor of u has a higher
-// degree: the entries from nlow[u] on.
+// (Row layout and the two ranges: b_adm_end above.)
 // Round start: every proposer is undecided; its admission range starts at the equal-degree
 // entries; eviction times unknown (-1).
 __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B, int* ev, const int* neq) {
@@ -164,7 +169,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B,
             const int bc = g.nlow[v] - neq[v];
             g.lcur[v] = bc;
             ev[v] = -1;
-            heavy = g.deg[v] - bc > GC_B_HEAVY;
+            heavy = b_adm_end(g, B, v) - bc > GC_B_HEAVY;
         }
         gc_wave_append(heavy, v, B.l[1][0], b_cnt(c, 1, 0));
         gc_stage_push(st, v >= 0 && !heavy, v, B.l[0][0], b_cnt(c, 0, 0));
@@ -213,8 +218,8 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
         int len = 0;
-        if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's higher-rank part
-            const int lo = g.nlow[v];
+        if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's eviction range
+            const int lo = b_adm_end(g, B, v);
             len = d - lo;
             s_src[w][lane] = g.col + r0 + lo;
         } else if (v >= 0 && watch == 0) {  // the kept potential evictors
@@ -294,7 +299,7 @@ __device__ __forceinline__ void b_adm_decide(GDev& g, BLists& B, DevCtl* c, int 
     } else if (f & 2u) {
         const int bc = g.lcur[v] + first;
         g.lcur[v] = bc;
-        *dst_kind = g.deg[v] - bc > GC_B_HEAVY ? 1 : 0;
+        *dst_kind = b_adm_end(g, B, v) - bc > GC_B_HEAVY ? 1 : 0;
     } else {
         g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
         g.lcur[v] = GC_B_EVCOL;
@@ -318,7 +323,7 @@ __device__ void b_adm_heavy(GDev& g, BLists& B, const int* ev, int pass, int bid
         const unsigned c6 = gc_k8_cand(kv);
         const int cv = b_cand(g, v, kv);
         const int bc = g.lcur[v];
-        const long long s0 = g.rp[v] + bc, s1 = g.rp[v] + g.deg[v];
+        const long long s0 = g.rp[v] + bc, s1 = g.rp[v] + b_adm_end(g, B, v);
         if (threadIdx.x == 0) {
             s_flag = 0u;
             s_first = 0x7FFFFFFF;
@@ -388,7 +393,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
         const long long r0 = v >= 0 ? g.rp[v] : 0;
         int len = 0;
         if (v >= 0 && lc >= 0) {  // first light scan: the row from the cursor
-            len = g.deg[v] - lc;
+            len = b_adm_end(g, B, v) - lc;
             s_src[w][lane] = g.col + r0 + lc;
         } else if (v >= 0) {  // the still-pending entries
             len = -lc - 1;
@@ -592,10 +597,10 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         }
         int len = 0;
         if (kind == 0 && !held) {
-            len = lc >= 0 ? d - lc : -lc - 1;
+            len = lc >= 0 ? b_adm_end(g, B, v) - lc : -lc - 1;
             s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0;
         } else if (kind == 2 && lc == GC_B_EVCOL) {
-            const int lo = g.nlow[v];
+            const int lo = b_adm_end(g, B, v);
             len = d - lo;
             s.src[lane] = g.col + r0 + lo;
         } else if (kind == 2 && watch == 0) {
@@ -684,7 +689,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
 // lanes over its row from the cursor, GC_HUB_UNR entries each in flight): a refusing entry
 // settles it OUT, the first undecided entry is its new cursor, the end of the row admits it
 // (appended to l1 as an eviction item at *n1).  Returns the heavy items left.
-__device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, int* ev, ull* scanned) {
+__device__ int b_async_heavy_pass(GDev& g, const BLists& B, int* l2, int n2, int* l1, int* n1, int* ev, ull* scanned) {
     const int lane = gc_lane();
     int nw = 0;
     for (int i = 0; i < n2; ++i) {
@@ -692,7 +697,7 @@ __device__ int b_async_heavy_pass(GDev& g, int* l2, int n2, int* l1, int* n1, in
         const unsigned kv = g.k8[v];
         const unsigned c6 = gc_k8_cand(kv);
         const int cv = b_cand(g, v, kv);
-        const int d = g.deg[v];
+        const int d = b_adm_end(g, B, v);  // the admission range's end
         const long long base = g.rp[v];
         int pos = g.lcur[v];
         bool refused = false;
@@ -760,7 +765,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
     int kind = it0 >= 0 ? (it0 >> GC_BI_SHIFT) : -1;
     unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte: only this wave writes it
     const int d = v >= 0 ? g.deg[v] : 0;
-    const int lo = v >= 0 ? g.nlow[v] : 0;
+    const int lo = v >= 0 ? b_adm_end(g, B, v) : 0;  // the eviction range's start
     const int lc = v >= 0 ? g.lcur[v] : 0;
     const long long r0 = v >= 0 ? g.rp[v] : 0;
     bool evcol = kind == 2 && lc == GC_B_EVCOL;
@@ -984,7 +989,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev,
 #ifdef GC_B_PROF
             const ull th = wall_clock64();
 #endif
-            n2 = b_async_heavy_pass(g, l2, n2, l1, &n1, ev, &hscan);
+            n2 = b_async_heavy_pass(g, B, l2, n2, l1, &n1, ev, &hscan);
 #ifdef GC_B_PROF
             htime += wall_clock64() - th;
 #endif
@@ -1074,7 +1079,7 @@ struct RunB {
 // part by degree and counts the equal-degree entries (neq); variant A never looks inside a
 // low part, so the layout serves both variants.
 static int ensure_bpart(gc_graph* g) {
-    if (g->part_prio != GC_PRIORITY_REF || !g->bpart || !g->neq) {
+    if (g->part_prio != GC_PRIORITY_REF || !g->bpart || !g->neq || !g->nhe) {
         gc_set_error("variant B needs the (deg, pos) row partition");
         return GC_EINVAL;
     }
@@ -1162,6 +1167,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         GC_HIP(hipMemsetAsync(g->bwatch, 0xFF, sizeof(int) * (size_t)g->n, s));  // -1: none
     }
     B.watch = g->bwatch;
+    B.nhe = g->nhe;
     std::vector<RoundRec> recs;
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;

@@ -242,14 +242,16 @@ def _check_partition(dg):
 
 def _expected_layout(rp, col):
     """The rank partition as gc_prep.hip states it, restated on the host: every row stably
-    split into [lower degree | equal degree, earlier position | higher rank] (coloring.py:64's
-    (deg, pos) order; the middle class is variant B's equal-degree block)."""
+    split into [lower degree | equal degree, earlier position | higher degree, earlier position
+    | the rest] (coloring.py:64's (deg, pos) order: the first two classes are the lower ranks;
+    the middle two are variant B's admission range, the last its eviction range)."""
     deg = np.diff(rp)
     n = len(rp) - 1
     src = np.repeat(np.arange(n, dtype=np.int64), deg)
     du, dv = deg[col], deg[src]
-    cls = np.where(du < dv, 0, np.where((du == dv) & (col < src), 1, 2))
-    order = np.argsort(src * 3 + cls, kind="stable")
+    early = col < src
+    cls = np.where(du < dv, 0, np.where(early & (du == dv), 1, np.where(early, 2, 3)))
+    order = np.argsort(src * 4 + cls, kind="stable")
     nlow = np.bincount(src, weights=(cls < 2), minlength=n).astype(np.int64)
     neq = np.bincount(src, weights=(cls == 1), minlength=n).astype(np.int64)
     return col[order], nlow, neq

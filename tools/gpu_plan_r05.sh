@@ -86,6 +86,15 @@ case ${1:-} in
                  env:AB_VARIANT=B ab:rmat24:4:base,w0=GC_B_WATCH:0,w4=GC_B_WATCH:4,w32=GC_B_WATCH:32 env:AB_VARIANT=
                  env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05q/bprof_rmat24.txt
                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05q/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q" >&2; exit 2 ;;
+  # r: the rank partition's fourth class (higher degree split by position: variant B's admission
+  #    range is the earlier entries, its eviction range the later ones -- about half of each
+  #    scan, R-MAT-20 oracle count): every GPU test, variant B's A/B against the previous
+  #    build (variants/r05q), variant A's step, the per-round profile
+  r) exec_steps=(file:tests/test_gpu_parity.py file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3" tests
+                 env:AB_VARIANT=B "abl:rmat24:3:2:base=-,prev=variants/r05q/libgcolor.so" env:AB_VARIANT=
+                 "abl:rmat24:3:2:base=-,prev=variants/r05q/libgcolor.so"
+                 env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05r/bprof_rmat24.txt
+                 "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05r/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
