@@ -95,6 +95,11 @@ case ${1:-} in
                  "abl:rmat24:3:2:base=-,prev=variants/r05q/libgcolor.so"
                  env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05r/bprof_rmat24.txt
                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05r/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r" >&2; exit 2 ;;
+  # s: variant B's fold knobs on the split partition: the watch period, the resident form, the
+  #    grid (4 / 6 per CU)
+  s) exec_steps=(env:AB_VARIANT=B
+                 ab:rmat24:4:base,w16=GC_B_WATCH:16,w32=GC_B_WATCH:32,w64=GC_B_WATCH:64,nores=GC_B_RESIDENT:0,bpc6=GC_B_ASYNC_BPC:6
+                 ab:rmat26:2:base,w32=GC_B_WATCH:32,bpc6=GC_B_ASYNC_BPC:6 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
