@@ -100,6 +100,9 @@ case ${1:-} in
   s) exec_steps=(env:AB_VARIANT=B
                  ab:rmat24:4:base,w16=GC_B_WATCH:16,w32=GC_B_WATCH:32,w64=GC_B_WATCH:64,nores=GC_B_RESIDENT:0,bpc6=GC_B_ASYNC_BPC:6
                  ab:rmat26:2:base,w32=GC_B_WATCH:32,bpc6=GC_B_ASYNC_BPC:6 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s" >&2; exit 2 ;;
+  # t: variant B with pushed forbidden-colour bitmaps for more vertices (every uncoloured vertex
+  #    proposes every round: rows of degree 64-512 are re-read ~13 times, R-MAT-20 oracle count)
+  t) exec_steps=(env:AB_VARIANT=B ab:rmat24:3:base,t256=GC_HUB_T:256,t128=GC_HUB_T:128,t64=GC_HUB_T:64 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
