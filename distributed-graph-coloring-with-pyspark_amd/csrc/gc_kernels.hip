@@ -1402,9 +1402,14 @@ struct GcAsyncLds {  // one wave's rows
 // gc_jp_sweep); the still-undecided ones are compacted to the front of lst (a chunk is
 // read into registers before any of it is rewritten, and survivors only move down).
 // Returns their number; `decided` counts the rest.
-__device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull& decided) {
+// Held lights (g.a_watch = R > 0, GC_A_WATCH): between full passes (every R-th), a light whose
+// cursor entry -- its first pending entry at the last scan -- is still undecided with its
+// candidate is kept without rescanning the rest of its range (an IN entry further on is seen
+// at the next full pass; the decisions are the same).
+__device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull& decided, int pass) {
     const int lane = gc_lane();
     const unsigned char* k8 = g.k8;
+    const bool full_pass = g.a_watch <= 0 || pass % g.a_watch == 0;
     int nw = 0;
     for (int c0 = 0; c0 < np; c0 += GC_WAVE) {
         const int idx = c0 + lane;
@@ -1414,13 +1419,19 @@ __device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull
         const int nl = v >= 0 ? g.nlow[v] : 0;
         const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0xFFu;  // own byte: only this wave changes it
         const long long rs = v >= 0 ? g.rp[v] : 0;
-        const int dl = v >= 0 ? nl - lc : 0;
         const unsigned cv6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
-        s.flag[lane] = 0;
-        s.first[lane] = 0x7FFFFFFF;
+        const int cvv = (v >= 0 && cv6 == GC_K8_BIG) ? g.cand[v] : (int)cv6;
+        bool held = false;
+        if (!full_pass && v >= 0 && lc < nl) {
+            const int u0 = g.col[rs + lc];
+            held = gc_jp_flag(g, u0, gc_ald8(k8 + u0), cv6, cvv) == 2u;
+        }
+        const int dl = (v >= 0 && !held) ? nl - lc : 0;
+        s.flag[lane] = held ? 2u : 0u;
+        s.first[lane] = held ? 0 : 0x7FFFFFFF;
         s.start[lane] = rs + lc;
         s.c6[lane] = cv6;
-        s.cv[lane] = (v >= 0 && cv6 == GC_K8_BIG) ? g.cand[v] : (int)cv6;
+        s.cv[lane] = cvv;
         const int incl = gc_wave_incl_scan(dl);
         const int excl = incl - dl;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -1628,10 +1639,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         int np = (int)(lb - la);
         int* lst = L.undL[in] + la;
         ull decided = 0;
-        int idle = 0;
+        int idle = 0, lpass = 0;
         while (np > 0) {
             const int before = np;
-            np = gc_async_light_pass(g, lst, np, s_w[w], decided);
+            np = gc_async_light_pass(g, lst, np, s_w[w], decided, ++lpass);
             if (np == 0) break;
             if ((stop = gc_async_stop(c, par, t0, budget))) break;
             if (np == before) {

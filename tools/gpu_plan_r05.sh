@@ -103,6 +103,10 @@ case ${1:-} in
   # t: variant B with pushed forbidden-colour bitmaps for more vertices (every uncoloured vertex
   #    proposes every round: rows of degree 64-512 are re-read ~13 times, R-MAT-20 oracle count)
   t) exec_steps=(env:AB_VARIANT=B ab:rmat24:3:base,t256=GC_HUB_T:256,t128=GC_HUB_T:128,t64=GC_HUB_T:64 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t" >&2; exit 2 ;;
+  # u: variant A's asynchronous JP with held lights (GC_A_WATCH): parity with it on, the A/Bs
+  u) exec_steps=(env:GC_A_WATCH=8 file:tests/test_gpu_parity.py file:tests/test_gpu_hubs.py "file:tests/test_gpu_fullsize.py:c3 and A"
+                 env:GC_A_WATCH= ab:rmat24:4:base,aw4=GC_A_WATCH:4,aw8=GC_A_WATCH:8,aw32=GC_A_WATCH:32
+                 ab:rmat26:3:base,aw8=GC_A_WATCH:8,aw32=GC_A_WATCH:32) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
