@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 
 #include "gc_engine.h"
 
@@ -140,8 +141,18 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
     if (!g || !out) { gc_set_error("gc_shard_create: null argument"); return GC_EINVAL; }
     if (lo < 0 || hi < lo || hi > g->n) { gc_set_error("gc_shard_create: bad range [%lld, %lld)", (long long)lo, (long long)hi); return GC_EINVAL; }
     GC_HIP(hipSetDevice(g->device));
+    // GC_PREP_TIMING=1: host-side phase times on stderr (each phase ends in a synchronisation)
+    const bool timing = getenv("GC_PREP_TIMING") != nullptr;
+    auto tmark = [&, t = std::chrono::steady_clock::now()](const char* what) mutable {
+        if (!timing) return;
+        hipDeviceSynchronize();
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[gc shard] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    };
     int rc0 = gc_set_priority(g, GC_PRIORITY_REF, 0);  // shards run the reference's (deg, pos) rank
     if (rc0) return rc0;
+    tmark("priority");
     gc_shard* sh = new gc_shard();
     gc_graph& v = sh->v;
     v.device = g->device;
@@ -168,10 +179,13 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
         return GC_ENOMEM;
     }
     int rc = (g->flags & GC_GRAPH_SYMMETRIC) ? gc_build_in_csr_sym(&v, lo, hi) : gc_build_in_csr(&v, lo, hi);
+    tmark("in-rows");
     if (!rc) rc = gc_alloc_run_state(&v);
+    tmark("run state");
     if (!rc) {  // hub lists on the parent (once), a bitmap replica (+ hub JP state) for this shard
         GDev pd = gc_view(g);
         rc = gc_hubs_prepare(g, pd);
+        tmark("hub index");
         const char* env = getenv("GC_SHARD_HUBS");
         const bool want_repl = !(env && *env && atoi(env) == 0);
         if (!rc && g->nhub > 0 && want_repl && g->hub_t >= 0) {  // every deg > hub_t vertex is a hub
@@ -188,6 +202,7 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
             rc = shard_alloc_hubs(sh);
         }
     }
+    tmark("hub replica");
     // without replicated hubs the shards resolve heavy vertices by row scans
     if (!rc && !sh->repl && g->maxdeg > GC_HEAVY_T) rc = gc_alloc_heavy_pending(&v);
     if (rc) {

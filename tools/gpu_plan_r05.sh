@@ -107,6 +107,10 @@ case ${1:-} in
   u) exec_steps=(env:GC_A_WATCH=8 file:tests/test_gpu_parity.py file:tests/test_gpu_hubs.py "file:tests/test_gpu_fullsize.py:c3 and A"
                  env:GC_A_WATCH= ab:rmat24:4:base,aw4=GC_A_WATCH:4,aw8=GC_A_WATCH:8,aw32=GC_A_WATCH:32
                  ab:rmat26:3:base,aw8=GC_A_WATCH:8,aw32=GC_A_WATCH:32) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u" >&2; exit 2 ;;
+  # v: where the N > 1 step's creation goes (R-MAT-28 one-rank RCCL: create 2046 ms against 159 at
+  #    N = 1): gc_shard_create's phases and the allocator's large blocks
+  v) exec_steps=(env:GC_PREP_TIMING=1 env:GC_ALLOC_TRACE=1 "bench:rmat28:--sharded,--steps,1,--warmup,1"
+                 "bench:rmat26:--sharded,--steps,1,--warmup,1" env:GC_PREP_TIMING= env:GC_ALLOC_TRACE=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
