@@ -183,6 +183,7 @@ int gc_order_after_inputs(hipStream_t s);
 int gc_alloc_graph_common(gc_graph* g, const int* src);  // deg, maxdeg, rank partition of src, transpose (gc_graph.hip)
 int gc_build_in_csr(gc_graph* g, long long lo, long long hi);  // in-neighbour CSR of rows [lo, hi)
 int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi);  // the same, symmetric graphs (no atomics)
+int gc_filter_rows_sym(gc_graph* g, gc_graph* v, long long lo, long long hi);  // the same over g's tiling (gc_prep.hip)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
 int gc_hubs_prepare(gc_graph* g, GDev& d);
 int gc_alloc_heavy_pending(gc_graph* g);  // gc_engine.hip: the hubs-off heavy JP's pending lists, on first use  // gc_hubs.hip: build (once) + reset; fills d's hub fields

@@ -878,6 +878,127 @@ int scan_ll(const long long* in, long long* out, long long count, hipStream_t s)
     return GC_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// A shard's in-rows of a symmetric graph (gc_shard_create): for every row v, its entries in
+// the shard's vertex range [lo, hi), in row order (trp / tcol).  Entry-parallel over the tiles
+// and the heavy rows' segments, like the rank partition: round 4's wave-per-row kernels took
+// 1.73 s on R-MAT-28 (a row per wave, the heaviest rows one wave each; profiles/r05/v).
+// ------------------------------------------------------------------------------------
+// pass 1: per-row counts (tiles: plain stores; heavy rows: per-segment counts, summed)
+__global__ void __launch_bounds__(GC_BLOCK) k_filt_count(Tiles T, const int* col, int lo, int hi, long long* cnt,
+                                                         ull* segc) {
+    __shared__ TileLdsP S;
+    const long long nt = T.ntiles, ns = nseg_of(T);
+    for (long long q = blockIdx.x; q < nt + ns; q += gridDim.x) {
+        if (q < nt) {
+            int r0, NE;
+            long long eb;
+            bool hl;
+            const int R = tile_rows(T, q, S, &r0, &eb, &NE, &hl);
+            if (R == 0) continue;
+            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = col[eb + i];
+            __syncthreads();
+            int u[GC_PER], rk[GC_PER];
+            const int nv = thread_entries(S, R, NE, u, rk);
+            unsigned m = 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) m |= (k < nv && u[k] >= lo && u[k] < hi ? 1u : 0u) << k;
+            ull total;
+            const ull prefix = block_excl_scan((ull)__popc(m), S.w, &total);
+            record_bases(S, R, NE, nv, prefix, total, m, 0u, 0u);
+            __syncthreads();
+            for (int r = threadIdx.x; r < R; r += blockDim.x) {
+                if (hl && r == R - 1) continue;  // the heavy row: its segments
+                cnt[r0 + r] = (long long)(f16(S.base[r + 1], 0) - f16(S.base[r], 0));
+            }
+        } else {
+            const long long sg = q - nt;
+            const int v = T.seg_row[sg], j = T.seg_j[sg];
+            const long long rs = T.rp[v], d = T.rp[v + 1] - rs;
+            const long long e0 = rs + (long long)j * GC_SEG;
+            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            ull c = 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                const int i = threadIdx.x + k * GC_BLOCK;
+                const int x = i < len ? col[e0 + i] : -1;
+                c += (x >= lo && x < hi) ? 1ull : 0ull;
+            }
+            const ull tot = block_sum(c, S.w);
+            if (threadIdx.x == 0) {
+                segc[sg] = tot;
+                if (tot) atomicAdd(reinterpret_cast<ull*>(cnt + v), tot);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// pass 2: the entries in range to tcol[trp[v] ...], in row order
+__global__ void __launch_bounds__(GC_BLOCK) k_filt_fill(Tiles T, const int* col, int lo, int hi, const long long* trp,
+                                                        int* tcol, const ull* segc) {
+    __shared__ TileLdsP S;
+    __shared__ ull s_pre;
+    const long long nt = T.ntiles, ns = nseg_of(T);
+    for (long long q = blockIdx.x; q < nt + ns; q += gridDim.x) {
+        if (q < nt) {
+            int r0, NE;
+            long long eb;
+            bool hl;
+            const int R = tile_rows(T, q, S, &r0, &eb, &NE, &hl);
+            if (R == 0) continue;
+            for (int i = threadIdx.x; i < NE; i += blockDim.x) S.buf[i] = col[eb + i];
+            __syncthreads();
+            int u[GC_PER], rk[GC_PER];
+            const int nv = thread_entries(S, R, NE, u, rk);
+            unsigned m = 0;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) m |= (k < nv && u[k] >= lo && u[k] < hi ? 1u : 0u) << k;
+            ull total;
+            const ull prefix = block_excl_scan((ull)__popc(m), S.w, &total);
+            record_bases(S, R, NE, nv, prefix, total, m, 0u, 0u);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                const unsigned bit = 1u << k;
+                if (!(m & bit)) continue;
+                const int r = rk[k];
+                const unsigned rank = (unsigned)prefix + __popc(m & (bit - 1u)) - f16(S.base[r], 0);
+                tcol[trp[r0 + r] + rank] = u[k];
+            }
+        } else {
+            const long long sg = q - nt;
+            const int v = T.seg_row[sg], j = T.seg_j[sg];
+            const long long rs = T.rp[v], d = T.rp[v + 1] - rs;
+            const long long e0 = rs + (long long)j * GC_SEG;
+            const int len = (int)std::min<long long>(GC_SEG, d - (long long)j * GC_SEG);
+            if (threadIdx.x < GC_WAVE) {  // the row's earlier segments' entries in range
+                ull a = 0;
+                for (long long i = sg - j + threadIdx.x; i < sg; i += GC_WAVE) a += segc[i];
+                a = gc_wave_sum(a);
+                if (threadIdx.x == 0) s_pre = a;
+            }
+            for (int i = threadIdx.x; i < len; i += blockDim.x) S.buf[i] = col[e0 + i];
+            __syncthreads();
+            const int j0 = threadIdx.x * GC_PER;  // this thread's consecutive entries: row order
+            unsigned m = 0;
+            int u[GC_PER];
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k) {
+                u[k] = j0 + k < len ? S.buf[j0 + k] : -1;
+                m |= (u[k] >= lo && u[k] < hi ? 1u : 0u) << k;
+            }
+            ull total;
+            const ull prefix = block_excl_scan((ull)__popc(m), S.w, &total);
+            const long long base = trp[v] + (long long)s_pre + (long long)prefix;
+#pragma unroll
+            for (int k = 0; k < GC_PER; ++k)
+                if (m & (1u << k)) tcol[base + __popc(m & ((1u << k) - 1u))] = u[k];
+        }
+        __syncthreads();
+    }
+}
+
 int small_grid(long long items) {
     return (int)std::max<long long>(1, std::min<long long>((items + GC_BLOCK - 1) / GC_BLOCK, 8192));
 }
@@ -962,6 +1083,55 @@ int gc_build_tiling(gc_graph* g) {
 }
 
 bool gc_partition_hubflags_supported() { return GC_PART_HUBFLAG; }
+
+// v's in-rows (v->trp, v->tcol) for the vertex range [lo, hi) of the symmetric graph g whose
+// rows v borrows (k_filt_count / k_filt_fill over g's tiling), on v's stream
+int gc_filter_rows_sym(gc_graph* g, gc_graph* v, long long lo, long long hi) {
+    const hipStream_t s = v->stream;
+    const long long n = g->n;
+    GC_HIP(gc_dmalloc((void**)&v->trp, sizeof(long long) * (size_t)(n + 1)));
+    if (n == 0 || g->nnz == 0) {
+        GC_HIP(hipMemsetAsync(v->trp, 0, sizeof(long long) * (size_t)(n + 1), s));
+        GC_HIP(gc_dmalloc((void**)&v->tcol, sizeof(int)));
+        GC_HIP(hipStreamSynchronize(s));
+        return GC_OK;
+    }
+    int rc = gc_build_tiling(g);
+    if (rc) return rc;
+    const Tiles T = tiles_of(g);
+    long long* cnt = nullptr;
+    ull* segc = nullptr;
+    GC_HIP(gc_dmalloc((void**)&cnt, sizeof(long long) * (size_t)(n + 1)));
+    if (gc_dmalloc((void**)&segc, sizeof(ull) * (size_t)std::max<long long>(g->nseg_cap, 1)) != hipSuccess) {
+        gc_dfree(cnt);
+        gc_set_error("gc_filter_rows_sym: device allocation failed");
+        return GC_ENOMEM;
+    }
+    GC_HIP(hipMemsetAsync(cnt, 0, sizeof(long long) * (size_t)(n + 1), s));
+    const int grid = prep_grid(g);
+    hipLaunchKernelGGL(k_filt_count, dim3(grid), dim3(GC_BLOCK), 0, s, T, (const int*)g->col, (int)lo, (int)hi, cnt,
+                       segc);
+    rc = scan_ll(cnt, v->trp, n + 1, s);
+    gc_dfree(cnt);
+    long long e = 0;
+    if (!rc) rc = gc_read_dev(s, &e, (const long long*)v->trp + n, 1);
+    if (!rc && gc_dmalloc((void**)&v->tcol, sizeof(int) * (size_t)std::max<long long>(e, 1)) != hipSuccess) {
+        gc_set_error("gc_filter_rows_sym: allocation of %lld in-entries failed", e);
+        rc = GC_ENOMEM;
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(k_filt_fill, dim3(grid), dim3(GC_BLOCK), 0, s, T, (const int*)g->col, (int)lo, (int)hi,
+                           (const long long*)v->trp, v->tcol, (const ull*)segc);
+        const hipError_t le = hipGetLastError(), se = hipStreamSynchronize(s);
+        if (le != hipSuccess || se != hipSuccess) {
+            gc_set_error("gc_filter_rows_sym: %s", hipGetErrorString(le != hipSuccess ? le : se));
+            rc = GC_EHIP;
+        }
+    }
+    hipStreamSynchronize(s);
+    gc_dfree(segc);
+    return rc;
+}
 
 int gc_partition(gc_graph* g, const int* src, int* dst, int prio, uint64_t seed, ull* bad, unsigned char* hubflag,
                  int hub_t) {

@@ -178,7 +178,12 @@ extern "C" int gc_shard_create(gc_graph* g, int64_t lo, int64_t hi, gc_shard** o
         delete sh;
         return GC_ENOMEM;
     }
-    int rc = (g->flags & GC_GRAPH_SYMMETRIC) ? gc_build_in_csr_sym(&v, lo, hi) : gc_build_in_csr(&v, lo, hi);
+    // symmetric graphs: the rows' entries in [lo, hi), entry-parallel over the parent's tiling
+    // (GC_SHARD_INROWS=wave: round 4's row-per-wave kernels)
+    const char* ir = getenv("GC_SHARD_INROWS");
+    int rc = !(g->flags & GC_GRAPH_SYMMETRIC) ? gc_build_in_csr(&v, lo, hi)
+             : (ir && strcmp(ir, "wave") == 0)  ? gc_build_in_csr_sym(&v, lo, hi)
+                                                : gc_filter_rows_sym(g, &v, lo, hi);
     tmark("in-rows");
     if (!rc) rc = gc_alloc_run_state(&v);
     tmark("run state");

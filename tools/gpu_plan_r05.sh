@@ -111,6 +111,12 @@ case ${1:-} in
   #    N = 1): gc_shard_create's phases and the allocator's large blocks
   v) exec_steps=(env:GC_PREP_TIMING=1 env:GC_ALLOC_TRACE=1 "bench:rmat28:--sharded,--steps,1,--warmup,1"
                  "bench:rmat26:--sharded,--steps,1,--warmup,1" env:GC_PREP_TIMING= env:GC_ALLOC_TRACE=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v" >&2; exit 2 ;;
+  # w: a shard's in-rows entry-parallel over the tiling (k_filt_count / k_filt_fill): the shard,
+  #    resume and multi-GPU bench tests, then session v's creation phases again
+  w) exec_steps=(file:tests/test_shard_gpu.py file:tests/test_gpu_resume.py file:tests/test_bench_gpu.py
+                 "file:tests/test_gpu_fullsize.py:rmat27" file:tests/test_xl_gpu.py
+                 env:GC_PREP_TIMING=1 "bench:rmat28:--sharded,--steps,1,--warmup,1"
+                 "bench:rmat26:--sharded,--steps,1,--warmup,1" env:GC_PREP_TIMING=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
