@@ -118,18 +118,24 @@ hipError_t alloc(void** p, size_t bytes, bool host) {
 hipError_t gc_dmalloc(void** p, size_t bytes) { return alloc(p, bytes, false); }
 hipError_t gc_hmalloc(void** p, size_t bytes) { return alloc(p, bytes, true); }
 
-// Parked bytes beyond this are freed at once: half the device's memory, at least 64 GB.
-// Round 4's fixed 64 GB was below one R-MAT-28 handle's buffers (~110 GB: the partitioned
-// CSR, the hub transpose and its hlow copies, the work lists), so every step's destroy freed
-// ~40 GB with hipFree -- which returns at once -- and the next large hipMalloc waited ~3 s
-// for that release (GC_ALLOC_TRACE=1, profiles/r05/a: "malloc 1024 MB 3123 ms"), one step in
-// two or three: R-MAT-28's bench step 2.93 s against 1.77 s without the stall.
+// Parked bytes beyond this are freed at once: the device's memory less 48 GB (at least 64 GB;
+// GC_ALLOC_IDLE_CAP_GB sets it).  A parked block is only idle memory of this process: an
+// allocation of ours that fails gives the whole cache back and retries.  Round 4's fixed 64 GB
+// was below one R-MAT-28 handle's buffers (~110 GB: the partitioned CSR, the hub transpose and
+// its hlow copies, the work lists), so every step's destroy freed ~40 GB with hipFree -- which
+// returns at once -- and the next large hipMalloc waited ~3 s for that memory (GC_ALLOC_TRACE=1,
+// profiles/r05/a: "malloc 1024 MB 3123 ms"): R-MAT-28's bench step 2.93 s against 1.77 s
+// without it.  Half of the memory (round 5's first cap) fixed the one-GPU step but not the
+// multi-GPU one, whose shard state adds its in-rows and replicas (~1.75 s stalls a step,
+// profiles/r05/w).
 static size_t idle_cap() {
     static size_t cap = 0;
     if (!cap) {
         size_t freeb = 0, total = 0;
-        const size_t floor = (size_t)64 << 30;
-        cap = (hipMemGetInfo(&freeb, &total) == hipSuccess && total / 2 > floor) ? total / 2 : floor;
+        const size_t floor = (size_t)64 << 30, reserve = (size_t)48 << 30;
+        const char* env = getenv("GC_ALLOC_IDLE_CAP_GB");
+        if (env && atoll(env) > 0) cap = (size_t)atoll(env) << 30;
+        else cap = (hipMemGetInfo(&freeb, &total) == hipSuccess && total > floor + reserve) ? total - reserve : floor;
     }
     return cap;
 }

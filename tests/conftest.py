@@ -19,6 +19,9 @@ GOLDEN = os.path.join(REPO, "tests", "golden", "cases")
 for p in (REPO, PKG_DIR):
     if p not in sys.path:
         sys.path.insert(0, p)
+# the tests share the device with torch's own allocations (resident CSRs, shard buffers): the
+# library parks at most half of it between calls (the bench's default is all but 48 GB)
+os.environ.setdefault("GC_ALLOC_IDLE_CAP_GB", "144")
 
 
 def pytest_configure(config):

@@ -117,6 +117,13 @@ case ${1:-} in
                  "file:tests/test_gpu_fullsize.py:rmat27" file:tests/test_xl_gpu.py
                  env:GC_PREP_TIMING=1 "bench:rmat28:--sharded,--steps,1,--warmup,1"
                  "bench:rmat26:--sharded,--steps,1,--warmup,1" env:GC_PREP_TIMING=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w" >&2; exit 2 ;;
+  # x: the allocator parking all but 48 GB (the multi-GPU step's stalls), R-MAT-28 / 26 sharded
+  #    and one-GPU, and the gloo two-rank rehearsal on R-MAT-26
+  x) exec_steps=(env:GC_PREP_TIMING=1 env:GC_ALLOC_TRACE=1 "bench:rmat28:--sharded,--steps,2,--warmup,1"
+                 env:GC_PREP_TIMING= env:GC_ALLOC_TRACE= "bench:rmat26:--sharded,--steps,2,--warmup,1"
+                 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
+                 env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0 "bench:rmat26:--gpus,2,--steps,1,--warmup,1"
+                 env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
