@@ -52,7 +52,8 @@ case ${1:-} in
   # k: the rocprofv3 summaries of THIS build (kernel trace + FETCH / WRITE passes -> profiles/pmc),
   #    the five single-GPU workloads the bench lines read them for
   k) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
-  k2) exec_steps=("profile:mesh512:--steps,3" "profile:uniform10M") ;;
+  k2) exec_steps=(profile:mesh512 profile:uniform10M) ;;
+  k3) exec_steps=(profile:mesh512) ;;
   # l: the N > 1 step rehearsed at scale: bench.py --gpus 2 (it starts the two ranks itself) on
   #    R-MAT-26, both ranks on this box's one GPU over gloo
   l) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
