@@ -3171,6 +3171,10 @@ void gcl_shard_own_front(const GDev& g, const GLists& L, long long lo, long long
                          hipStream_t s) {
     GC_LAUNCH(k_shard_own_front, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, g, L, lo, hi, out, out_cnt);
 }
+// the control block into a host-mapped snapshot slot (variant B's per-round wait: a kernel's
+// vector stores instead of a copy-engine blit)
+__global__ void k_snap_ctl(DevCtl* c, DevCtl* snap) { gc_snap_copy(c, snap); }
+void gcl_snap(DevCtl* ctl, DevCtl* snap, hipStream_t s) { GC_LAUNCH(k_snap_ctl, dim3(1), dim3(GC_BLOCK), 0, s, ctl, snap); }
 void gcl_finalize(const GDev& g, int grid, hipStream_t s) {
     GC_LAUNCH(k_finalize, dim3(grid), dim3(GC_BLOCK), 0, s, g);
 }

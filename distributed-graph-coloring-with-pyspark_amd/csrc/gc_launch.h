@@ -164,6 +164,7 @@ void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStrea
 // replicated hubs after a slice seam: the other ranks' light winners flag their hubs
 void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
+void gcl_snap(DevCtl* ctl, DevCtl* snap, hipStream_t s);
 // gc_color_resume: the round-start state from colours + frontier (big: scratch list + its count)
 void gcl_resume(const GDev& g, const GLists& L, const int* colors, const int* cround, const int* front, long long nf,
                 int* big, ull* big_cnt, hipStream_t s);

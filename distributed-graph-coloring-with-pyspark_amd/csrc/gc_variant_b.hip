@@ -69,6 +69,7 @@ __global__ void k_b_reset(GDev g, long long round) {
     c->fsort_all = 1;
     for (int k = 0; k < 3; ++k) c->und_cnt[k] = 0;
     for (int k = 0; k < 9; ++k) c->bcnt[k] = 0;
+    c->async_abort[0] = 0;  // the round's asynchronous fold starts un-aborted
 }
 
 // bounded attempt with k = 0: only proposers WITH a coloured neighbour fail
@@ -1061,10 +1062,21 @@ struct RunB {
     GDev d;
     GLists L;
     hipStream_t s;
+    // the round's wait: a one-workgroup kernel writes the control block into the pinned
+    // snapshot slot (GC_SNAP_COPY=1: a copy-engine blit, as before), then an event wait
+    const bool snap_copy = getenv("GC_SNAP_COPY") && atoi(getenv("GC_SNAP_COPY")) > 0;
     int sync() {
         GC_HIP(hipGetLastError());
-        GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
-        GC_HIP(hipStreamSynchronize(s));
+        if (snap_copy || !g->hsnap_dev) {
+            GC_HIP(hipMemcpyAsync(g->hctl, g->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
+            GC_HIP(hipStreamSynchronize(s));
+            return GC_OK;
+        }
+        gcl_snap(g->ctl, g->hsnap_dev, s);
+        GC_HIP(hipGetLastError());
+        GC_HIP(hipEventRecord(g->evsnap[0], s));
+        GC_HIP(hipEventSynchronize(g->evsnap[0]));
+        memcpy(g->hctl, g->hsnap, sizeof(DevCtl));
         return GC_OK;
     }
     int zero(ull* p) {
@@ -1211,7 +1223,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         };
         if (b_async_grid > 0) {  // the first passes on the full grid, then the rest as one asynchronous launch
             enqueue_passes(b_async_k);
-            GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
+            if (b_async_k > 0) GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
             GC_LAUNCH(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3),
                                b_async_budget);
             ++passes;

@@ -125,6 +125,10 @@ case ${1:-} in
                  "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
                  env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0 "bench:rmat26:--gpus,2,--steps,1,--warmup,1"
                  env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x" >&2; exit 2 ;;
+  # y: variant B's round wait through a kernel-written snapshot (no copy-engine blit, no memset a
+  #    round): parity, the A/B against GC_SNAP_COPY=1
+  y) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B"
+                 env:AB_VARIANT=B ab:rmat24:4:base,blit=GC_SNAP_COPY:1 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|y" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
