@@ -124,9 +124,14 @@ __device__ __forceinline__ ull* b_cnt(DevCtl* c, int kind, int slot) { return &c
 // a list count at the start of a pass (written by an earlier launch)
 __device__ __forceinline__ long long b_count(DevCtl* c, int kind, int slot) { return (long long)*b_cnt(c, kind, slot); }
 
-// gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]; load(o, u)
-template <typename Load, typename Apply>
-__device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl, int total, Load load, Apply apply) {
+// gc_chunk_edges_at over per-owner sources: owner o's x-th entry is s_src[o][x]; load(o, u).
+// skip(o): the owner needs no more entries (its entries after that point are not read)
+struct BNoSkip {
+    __device__ bool operator()(int) const { return false; }
+};
+template <typename Load, typename Apply, typename Skip = BNoSkip>
+__device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl, int total, Load load, Apply apply,
+                                              Skip skip = Skip()) {
     const int lane = gc_lane();
     for (int base = 0; base < total; base += GC_SLOTS * GC_WAVE) {
         int o[GC_SLOTS], x[GC_SLOTS], u[GC_SLOTS];
@@ -136,7 +141,7 @@ __device__ __forceinline__ void b_chunk_edges(const int* const* s_src, int excl,
             const int e = base + k * GC_WAVE + lane;
             o[k] = gc_owner(excl, e);
             x[k] = e - __shfl(excl, o[k], GC_WAVE);
-            ok[k] = e < total;
+            ok[k] = e < total && !skip(o[k]);
         }
 #pragma unroll
         for (int k = 0; k < GC_SLOTS; ++k) u[k] = ok[k] ? s_src[o[k]][x[k]] : 0;
@@ -648,7 +653,8 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
                     atomicMin(&s.minv[o], u);
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
                 }
-            });
+            },
+            [&](int o) { return g.b_refskip && s.kind[o] == 0 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         int keep = -1;  // the item that stays (-1: settled)
         if (kind == 0 && held) {
@@ -856,7 +862,8 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                     atomicMin(&s.minv[o], u);
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
                 }
-            });
+            },
+            [&](int o) { return g.b_refskip && s.kind[o] == 0 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         bool keep = false;
         if (kind == 0 && held) {
@@ -1111,6 +1118,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // watched entries (b_async_chunk_pass): a full admission rescan every GC_B_WATCH-th pass at most
     // otherwise; 0 off
     R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 8;
+    R.d.b_refskip = getenv("GC_B_REFSKIP") ? atoi(getenv("GC_B_REFSKIP")) : 1;
     const hipStream_t s = R.s;
     const GDev& d = R.d;
     const GLists& L = R.L;

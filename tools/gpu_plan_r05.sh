@@ -129,6 +129,9 @@ case ${1:-} in
   #    round): parity, the A/B against GC_SNAP_COPY=1
   y) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B"
                  env:AB_VARIANT=B ab:rmat24:4:base,blit=GC_SNAP_COPY:1 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|y" >&2; exit 2 ;;
+  # z: a refused admission reads no more of its entries (GC_B_REFSKIP): parity, the A/B
+  z) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_parity.py
+                 env:AB_VARIANT=B ab:rmat24:4:base,noskip=GC_B_REFSKIP:0 ab:rmat26:2:base,noskip=GC_B_REFSKIP:0 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|y|z" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
