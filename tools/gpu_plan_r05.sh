@@ -132,6 +132,11 @@ case ${1:-} in
   # z: a refused admission reads no more of its entries (GC_B_REFSKIP): parity, the A/B
   z) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_parity.py
                  env:AB_VARIANT=B ab:rmat24:4:base,noskip=GC_B_REFSKIP:0 ab:rmat26:2:base,noskip=GC_B_REFSKIP:0 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|y|z" >&2; exit 2 ;;
+  # aa: ascending eviction ranges (a cursor and windows, no kept list): variant B parity (golden,
+  #     randomized directed rows -- the kept-list form --, R-MAT and C3 -- the ascending form),
+  #     every GPU test, the A/B against GC_B_EVASC=0, the per-round profile
+  aa) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3" file:tests/test_gpu_parity.py tests
+                  env:AB_VARIANT=B ab:rmat24:4:base,noasc=GC_B_EVASC:0 ab:rmat26:2:base,noasc=GC_B_EVASC:0 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
