@@ -137,6 +137,12 @@ case ${1:-} in
   #     every GPU test, the A/B against GC_B_EVASC=0, the per-round profile
   aa) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3" file:tests/test_gpu_parity.py tests
                   env:AB_VARIANT=B ab:rmat24:4:base,noasc=GC_B_EVASC:0 ab:rmat26:2:base,noasc=GC_B_EVASC:0 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa" >&2; exit 2 ;;
+  # ab: the per-round fold profile with and without the ascending eviction ranges
+  ab) exec_steps=(env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05ab/bprof_asc.txt
+                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ab/records_asc.json,1"
+                  env:GC_B_EVASC=0 env:GC_B_PROF_OUT=gpurun_out/r05ab/bprof_noasc.txt
+                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ab/records_noasc.json,1"
+                  env:GC_B_EVASC= env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
