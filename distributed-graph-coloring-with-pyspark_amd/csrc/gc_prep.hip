@@ -430,15 +430,7 @@ __device__ void part_tile(const PartArgs& a, TileLdsP& S, long long t, ull* nbad
         const unsigned c0 = f16(b1, 0) - f16(b, 0), c1 = f16(b1, 1) - f16(b, 1);
         a.nlow[r0 + r] = (int)(c0 + c1);
         if (a.neq) a.neq[r0 + r] = (int)c1;
-        if (a.nhe) {
-            // bit 31: the row's class-3 entries (variant B's eviction range) ascend, so the fold
-            // can stop at the first potential evictor (gc_variant_b.hip, b_evs_*)
-            const unsigned c2 = f16(b1, 2) - f16(b, 2);
-            bool asc = !PRIO;
-            const int e0 = S.off[r] + (int)(c0 + c1 + c2), e1 = S.off[r + 1];
-            for (int e = e0; asc && e + 1 < e1; ++e) asc = (S.buf[e] & 0x7FFFFFFF) < (S.buf[e + 1] & 0x7FFFFFFF);
-            a.nhe[r0 + r] = (int)(c2 | (asc ? 0x80000000u : 0u));
-        }
+        if (a.nhe) a.nhe[r0 + r] = (int)(f16(b1, 2) - f16(b, 2));
     }
 }
 

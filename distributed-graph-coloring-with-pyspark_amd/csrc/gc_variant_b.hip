@@ -102,7 +102,6 @@ struct BLists {
     int* pend;     // nnz ints: each listed light vertex's still-pending entries, at rp[v] (see below)
     int* watch;    // n ints: an undecided vertex's smallest pending entry at its last scan (asynchronous fold)
     const int* nhe;  // n ints: the row's higher-degree earlier entries (gc_prep.hip's class 2)
-    int evasc;       // ascending eviction ranges used (GC_B_EVASC=0: every row in the kept-list form)
 };
 // Row layout (the (deg, pos) rank partition, gc_prep.hip): [lower degree | equal degree and
 // earlier | higher degree and earlier | the rest (later positions of equal or higher degree)].
@@ -110,69 +109,7 @@ struct BLists {
 // range [nlow[v] - neq[v], nlow[v] + nhe[v]).  v can only be evicted by a later u with
 // deg(u) > deg(v): the eviction range [nlow[v] + nhe[v], deg(v)) (its equal-degree entries
 // are skipped by their degree).
-__device__ __forceinline__ int b_adm_end(const GDev& g, const BLists& B, int v) {
-    return g.nlow[v] + (B.nhe[v] & 0x7FFFFFFF);
-}
-
-// Ascending eviction ranges (the partition's bit 31 of nhe[v]: the row's class-3 entries are
-// in increasing vertex order -- every row of a CSR whose rows are sorted, as the generators'
-// are): the smallest potential evictor of an admitted v is the FIRST one of its range, so its
-// eviction scan reads windows of GC_B_EVWIN entries and stops at the first one (a full range
-// scan and a kept list otherwise).  The item's cursor word, lcur[v]:
-//   GC_B_EVCOL                      not started (position 0);
-//   -c - 1                          searching from position c;
-//   -c - 1 - GC_B_EVS_WATCH         ev[v] = the evictor found in the window from c: while it is
-//                                   undecided v waits unscanned; admitted: final; refused: the
-//                                   search resumes at c past it (the ids ascend).
-// ev[v] only ever names a potential evictor (or INF), as the kept-list form's does, and is
-// never above the true eviction time: the values other waves read are the same.
-#define GC_B_EVCOL 0x7FFFFFFF  // (an item's cursor word before its first eviction scan; see BLists below)
-#define GC_B_EVWIN 64
-#define GC_B_EVS_WATCH (1 << 30)
-__device__ __forceinline__ bool b_ev_asc(const BLists& B, int v) { return B.evasc && B.nhe[v] < 0; }
-// 0: wait without a scan; 1: settled (ev[v] final); 2: scan [c, c + *len) of the range for
-// the smallest potential evictor above *thr
-__device__ __forceinline__ int b_evs_begin(const GDev& g, const int* ev, int v, int lc, int range, int* c, int* len,
-                                           int* thr) {
-    int e = -1;
-    if (lc == GC_B_EVCOL) {
-        *c = 0;
-    } else if (lc < -GC_B_EVS_WATCH) {
-        *c = -(lc + 1 + GC_B_EVS_WATCH);
-        e = ev[v];  // this wave's (or the last pass's) own word
-        const unsigned st = gc_k8_state(gc_ald8(g.k8 + e));
-        if (st == GC_JP_UND) return 0;
-        if (st == GC_JP_IN) return 1;
-    } else {
-        *c = -lc - 1;
-        e = ev[v];
-    }
-    *thr = e;
-    const int rem = range - *c;
-    *len = rem < GC_B_EVWIN ? (rem > 0 ? rem : 0) : GC_B_EVWIN;
-    return 2;
-}
-// after the scan (e: the smallest qualifying id of the window, GC_B_INF: none); true: the
-// item stays listed
-__device__ __forceinline__ bool b_evs_end(GDev& g, int* ev, int v, int c, int len, int range, int e,
-                                          int* lc_out = nullptr) {
-    int lc;
-    if (e != GC_B_INF) {
-        gc_asti(ev + v, e);
-        if (gc_k8_state(gc_ald8(g.k8 + e)) == GC_JP_IN) return false;  // final: evicted at e's arrival
-        lc = -c - 1 - GC_B_EVS_WATCH;
-    } else {
-        c += len;
-        if (c >= range) {
-            gc_asti(ev + v, GC_B_INF);  // never evicted
-            return false;
-        }
-        lc = -c - 1;
-    }
-    if (lc_out) *lc_out = lc;  // (the resident form keeps it in a register)
-    else g.lcur[v] = lc;
-    return true;
-}
+__device__ __forceinline__ int b_adm_end(const GDev& g, const BLists& B, int v) { return g.nlow[v] + B.nhe[v]; }
 // Pending entries (round 4).  A flag that reads 0 is final (a later arrival, a refused or
 // other-candidate vertex, an eviction before v), so after its first scan a light vertex only
 // ever needs the entries that were still pending: each scan writes them, compacted, to
@@ -262,7 +199,6 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
     __shared__ int s_d[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ unsigned s_c6[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cv[GC_WAVES_PER_BLOCK][GC_WAVE];
-    __shared__ int s_thr[GC_WAVES_PER_BLOCK][GC_WAVE];  // ascending range: ids above it qualify; -2: kept-list form
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int* __restrict__ list = B.l[2][rs];
@@ -283,32 +219,24 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
         // refused -- while that one is undecided v stays listed unscanned, once it is admitted
         // ev(v) is final; only a refusal asks for a rescan of the kept entries.
         int watch = 0;  // 1: still pending, no scan; 2: final, no scan
-        const bool asc = v >= 0 && b_ev_asc(B, v);
-        const int lo = v >= 0 ? b_adm_end(g, B, v) : 0;
-        int ec = 0, thr = -2, len = 0;
-        if (asc) {  // ascending range: the window from the cursor
-            const int a = b_evs_begin(g, ev, v, lc, d - lo, &ec, &len, &thr);
-            watch = a == 0 ? 1 : (a == 1 ? 2 : 0);
-            s_src[w][lane] = g.col + r0 + lo + ec;
-        } else if (v >= 0 && lc != GC_B_EVCOL) {
+        if (v >= 0 && lc != GC_B_EVCOL) {
             const unsigned st = gc_k8_state(k8[ev[v]]);
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
-        if (asc) {
-        } else if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's eviction range
+        int len = 0;
+        if (v >= 0 && lc == GC_B_EVCOL) {  // first eviction scan: the row's eviction range
+            const int lo = b_adm_end(g, B, v);
             len = d - lo;
             s_src[w][lane] = g.col + r0 + lo;
         } else if (v >= 0 && watch == 0) {  // the kept potential evictors
             len = -lc - 1;
             s_src[w][lane] = B.pend + r0;
         }
-        if (watch != 0) len = 0;
         s_dst[w][lane] = B.pend + r0;
         s_np[w][lane] = 0;
         s_min[w][lane] = GC_B_INF;
         s_v[w][lane] = v;
         s_d[w][lane] = d;
-        s_thr[w][lane] = asc ? thr : -2;
         s_c6[w][lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
         s_cv[w][lane] = v >= 0 ? b_cand(g, v, kv) : -1;
         const int incl = gc_wave_incl_scan(len);
@@ -331,19 +259,12 @@ __device__ void b_ev_pass(GDev& g, BLists& B, int* ev, int pass, int bid, int nb
                     if (u <= s_v[w][o] || (int)(du >> 32) <= s_d[w][o]) return;
                     if (!b_same(g, u, ku, s_c6[w][o], s_cv[w][o])) return;
                 }
-                const int t = s_thr[w][o];
-                if (t >= -1) {  // ascending range: the smallest above the threshold
-                    if (u > t) atomicMin(&s_min[w][o], u);
-                    return;
-                }
                 atomicMin(&s_min[w][o], u);
                 s_dst[w][o][atomicAdd(&s_np[w][o], 1)] = (int)((unsigned)u | GC_B_PMARK);
             });
         gc_wave_sync();
         bool pend = watch == 1;
-        if (asc && watch == 0) {
-            pend = b_evs_end(g, ev, v, ec, len, d - lo, s_min[w][lane]);
-        } else if (v >= 0 && watch == 0) {
+        if (v >= 0 && watch == 0) {
             const int e = s_min[w][lane];
             ev[v] = e;
             pend = e != GC_B_INF && gc_k8_state(k8[e]) != GC_JP_IN;
@@ -671,13 +592,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         const int lc = v >= 0 ? g.lcur[v] : 0;
         const long long r0 = v >= 0 ? g.rp[v] : 0;
         int watch = 0;  // eviction items: 1 still pending, 2 final, no scan (b_ev_pass)
-        const bool asc = kind == 2 && b_ev_asc(B, v);  // ascending eviction range: windows from a cursor
-        const int elo = kind == 2 ? b_adm_end(g, B, v) : 0;
-        int ec = 0, thr = -2, elen = 0;
-        if (asc) {
-            const int a = b_evs_begin(g, ev, v, lc, d - elo, &ec, &elen, &thr);
-            watch = a == 0 ? 1 : (a == 1 ? 2 : 0);
-        } else if (kind == 2 && lc != GC_B_EVCOL) {
+        if (kind == 2 && lc != GC_B_EVCOL) {
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + ev[v]));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
@@ -690,26 +605,23 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         if (kind == 0 && !held) {
             len = lc >= 0 ? b_adm_end(g, B, v) - lc : -lc - 1;
             s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0;
-        } else if (asc && watch == 0) {
-            len = elen;
-            s.src[lane] = g.col + r0 + elo + ec;
-        } else if (asc) {
         } else if (kind == 2 && lc == GC_B_EVCOL) {
-            len = d - elo;
-            s.src[lane] = g.col + r0 + elo;
+            const int lo = b_adm_end(g, B, v);
+            len = d - lo;
+            s.src[lane] = g.col + r0 + lo;
         } else if (kind == 2 && watch == 0) {
             len = -lc - 1;
             s.src[lane] = B.pend + r0;
         }
         s.dst[lane] = B.pend + r0;
         s.flag[lane] = 0;
-        s.np[lane] = asc ? thr : 0;  // (an ascending eviction item's threshold)
+        s.np[lane] = 0;
         s.minv[lane] = GC_B_INF;
         s.v[lane] = v;
         s.d[lane] = d;
         s.c6[lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
         s.cv[lane] = v >= 0 ? b_cand(g, v, kv) : -1;
-        s.kind[lane] = asc ? 3 : kind;
+        s.kind[lane] = kind;
         const int incl = gc_wave_incl_scan(len);
         const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -720,7 +632,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             [&](int o, int um) {
                 const int u = um & 0x7FFFFFFF;
                 const ull k = (ull)gc_ald8(g.k8 + u);
-                return (s.kind[o] >= 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
+                return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
             },
             [&](int o, int um, ull du, int) {
                 const int u = um & 0x7FFFFFFF;
@@ -738,10 +650,6 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
                         if (u <= s.v[o] || (int)(du >> 32) <= s.d[o]) return;
                         if (!b_same(g, u, ku, s.c6[o], s.cv[o])) return;
                     }
-                    if (s.kind[o] == 3) {  // ascending range: the smallest above the threshold
-                        if (u > s.np[o]) atomicMin(&s.minv[o], u);
-                        return;
-                    }
                     atomicMin(&s.minv[o], u);
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
                 }
@@ -749,10 +657,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             [&](int o) { return g.b_refskip && s.kind[o] == 0 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         int keep = -1;  // the item that stays (-1: settled)
-        if (asc) {
-            if (watch == 1) keep = it;
-            else if (watch == 0 && b_evs_end(g, ev, v, ec, elen, d - elo, s.minv[lane])) keep = it;
-        } else if (kind == 0 && held) {
+        if (kind == 0 && held) {
             keep = it;
         } else if (kind == 0) {
             const unsigned f = s.flag[lane];
@@ -870,13 +775,11 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
     const int lo = v >= 0 ? b_adm_end(g, B, v) : 0;  // the eviction range's start
     const int lc = v >= 0 ? g.lcur[v] : 0;
     const long long r0 = v >= 0 ? g.rp[v] : 0;
-    const bool asc = v >= 0 && b_ev_asc(B, v);  // its eviction range ascends: a cursor, no kept entries
-    int elc = lc;                                 // an ascending eviction item's cursor word
-    bool evcol = kind == 2 && !asc && lc == GC_B_EVCOL;
-    int np = (kind == 0 || (kind == 2 && !asc && !evcol)) ? -lc - 1 : 0;
-    int evv = (kind == 2 && !asc && !evcol) ? ev[v] : -1;  // own eviction time (only this wave writes it)
-    const bool bad = kind == 0 && lc >= 0;                  // first admission scan not done
-    const int need = kind == 0 ? (asc ? np : max(np, d - lo)) : (asc ? 0 : (evcol ? d - lo : np));
+    bool evcol = kind == 2 && lc == GC_B_EVCOL;
+    int np = (v >= 0 && !evcol) ? -lc - 1 : 0;
+    int evv = (kind == 2 && !evcol) ? ev[v] : -1;  // own eviction time (only this wave writes it)
+    const bool bad = kind == 0 && lc >= 0;          // first admission scan not done
+    const int need = kind == 0 ? max(np, d - lo) : (evcol ? d - lo : np);
     const int incl = gc_wave_incl_scan(need);
     const int off = incl - need;
     if (__ballot(bad) || __shfl(incl, GC_WAVE - 1, GC_WAVE) > GC_B_RES_CAP) return -1;
@@ -907,21 +810,12 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         if (kind == 0 && wu >= 0 && wu < g.n && g.b_watch > 0 && *npass % (ull)g.b_watch != 0)
             held = b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), c6, cv, ev) == 2u;
         int watch = 0;  // eviction items: 1 still pending, 2 final, no scan
-        int ec = 0, elen = 0, thr = -2;
-        if (kind == 2 && asc) {
-            const int a = b_evs_begin(g, ev, v, elc, d - lo, &ec, &elen, &thr);
-            watch = a == 0 ? 1 : (a == 1 ? 2 : 0);
-        } else if (kind == 2 && !evcol) {
+        if (kind == 2 && !evcol) {
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + evv));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
         int len = 0;
-        if (kind == 2 && asc) {
-            if (watch == 0) {
-                len = elen;
-                s.src[lane] = g.col + r0 + lo + ec;
-            }
-        } else if ((kind == 0 && !held) || (kind == 2 && !evcol && watch == 0)) {
+        if ((kind == 0 && !held) || (kind == 2 && !evcol && watch == 0)) {
             len = np;
             s.src[lane] = pe + off;
         } else if (kind == 2 && evcol) {
@@ -930,13 +824,13 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         }
         s.dst[lane] = pe + off;
         s.flag[lane] = 0;
-        s.np[lane] = (kind == 2 && asc) ? thr : 0;
+        s.np[lane] = 0;
         s.minv[lane] = GC_B_INF;
         s.v[lane] = v;
         s.d[lane] = d;
         s.c6[lane] = c6;
         s.cv[lane] = cv;
-        s.kind[lane] = (kind == 2 && asc) ? 3 : kind;
+        s.kind[lane] = kind;
         const int li = gc_wave_incl_scan(len);
         const int le = li - len;
         const int total = __shfl(li, GC_WAVE - 1, GC_WAVE);
@@ -947,7 +841,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
             [&](int o, int um) {
                 const int u = um & 0x7FFFFFFF;
                 const ull k = (ull)gc_ald8(g.k8 + u);
-                return (s.kind[o] >= 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
+                return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
             },
             [&](int o, int um, ull du, int) {
                 const int u = um & 0x7FFFFFFF;
@@ -964,10 +858,6 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                     if (!((unsigned)um & GC_B_PMARK)) {
                         if (u <= s.v[o] || (int)(du >> 32) <= s.d[o]) return;
                         if (!b_same(g, u, ku, s.c6[o], s.cv[o])) return;
-                    }
-                    if (s.kind[o] == 3) {  // ascending range: the smallest above the threshold
-                        if (u > s.np[o]) atomicMin(&s.minv[o], u);
-                        return;
                     }
                     atomicMin(&s.minv[o], u);
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
@@ -990,14 +880,10 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                 kv = (kv & ~3u) | GC_JP_IN;
                 gc_ast8(g.k8 + v, kv);
                 kind = 2;
-                evcol = !asc;
-                elc = GC_B_EVCOL;
+                evcol = true;
                 np = 0;
                 keep = true;
             }
-        } else if (kind == 2 && asc) {
-            if (watch == 1) keep = true;
-            else if (watch == 0) keep = b_evs_end(g, ev, v, ec, elen, d - lo, s.minv[lane], &elc);
         } else if (kind == 2) {
             if (watch == 1) {
                 keep = true;
@@ -1029,7 +915,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         n = nn;
     }
     // stopped: back to the global form -- cursor words, watched entries, entries, the item list
-    if (v >= 0) g.lcur[v] = (kind == 2 && asc) ? elc : (evcol ? GC_B_EVCOL : -np - 1);
+    if (v >= 0) g.lcur[v] = evcol ? GC_B_EVCOL : -np - 1;
     if (kind == 0 && g.b_watch > 0) B.watch[v] = wu;
     {
         const int pin = gc_wave_incl_scan(v >= 0 ? np : 0);
@@ -1302,7 +1188,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     }
     B.watch = g->bwatch;
     B.nhe = g->nhe;
-    B.evasc = getenv("GC_B_EVASC") ? atoi(getenv("GC_B_EVASC")) : 1;
     std::vector<RoundRec> recs;
     int status = GC_OK;
     long long sweeps_total = 0, fail_round = -1, fail_count = 0;
