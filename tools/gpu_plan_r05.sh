@@ -143,6 +143,8 @@ case ${1:-} in
                   env:GC_B_EVASC=0 env:GC_B_PROF_OUT=gpurun_out/r05ab/bprof_noasc.txt
                   "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ab/records_noasc.json,1"
                   env:GC_B_EVASC= env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab" >&2; exit 2 ;;
+  # ac: variant A's rounds by frontier class (where R-MAT-24's 130 ms of rounds go), and R-MAT-26
+  ac) exec_steps=(rounds:rmat24 rounds:rmat26) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
