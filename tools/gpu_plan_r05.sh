@@ -145,6 +145,11 @@ case ${1:-} in
                   env:GC_B_EVASC= env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
   # ac: variant A's rounds by frontier class (where R-MAT-24's 130 ms of rounds go), and R-MAT-26
   ac) exec_steps=(rounds:rmat24 rounds:rmat26) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac" >&2; exit 2 ;;
+  # fin: the final build: every GPU test, smoke, the default bench line (R-MAT-24 + north star + CPU
+  #      baseline, traffic from profiles/pmc), C5 on one GPU, variant B, C4 and C2
+  fin) exec_steps=(tests smoke bench:rmat24 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
+                   "bench:rmat24:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end"
+                   "bench:mesh512:--no-cpu-baseline,--no-end-to-end" "bench:uniform10M:--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
