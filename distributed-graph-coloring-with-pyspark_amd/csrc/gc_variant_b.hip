@@ -52,9 +52,11 @@ __device__ __forceinline__ bool b_same(const GDev& g, int u, unsigned ku, unsign
 __global__ void k_b_reset(GDev g, long long round) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     DevCtl* c = g.ctl;
-    // a list append overflowed (gc_stage_fits): stay halted -- every fold kernel returns at
-    // once -- until the host's next wait reports it
-    c->halt = c->loop_err == GC_LERR_LIST ? GC_H_STALLED : GC_RUN;
+    // halted -- a list append overflowed (gc_stage_fits), or the previous round's
+    // commit found the colouring done, failed or its fold unfinished (pipelined rounds,
+    // k_b_commit): this round is a no-op, every kernel of it returns at once, until the host
+    // clears the halt
+    if (c->halt) return;
     c->round = round;
     c->cur = 0;
     c->fcnt[0] = 0;
@@ -461,9 +463,26 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_adm(GDev g, BLists B, const int*
 
 // winners: admitted and never evicted, coloured (coloring_optimized.py:129-140); with hub
 // bitmaps, pushed into the hubs listing them (gc_hub_push_wave)
-__global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev, int* big) {
+// check_ws >= 0 (pipelined rounds: the host enqueued this commit without waiting for the
+// fold): the round's own decisions, as the host makes them otherwise -- no uncoloured vertex
+// left: GC_H_DONE; a bounded attempt with a failing proposer: GC_H_FAILED (nothing committed,
+// the state at the round start stays); the fold's lists of slot check_ws not empty (a give-up
+// of the asynchronous fold, or more passes needed): GC_H_SWEEPS.  Every workgroup reaches the
+// same decision from words no kernel of this launch writes.
+__global__ void __launch_bounds__(GC_BLOCK) k_b_commit(GDev g, GLists L, const int* ev, int* big, int check_ws) {
     DevCtl* c = g.ctl;
     if (c->halt) return;
+    if (check_ws >= 0) {
+        int h = GC_RUN;
+        if (c->fcnt[c->cur] == 0) h = GC_H_DONE;
+        else if (c->kbound >= 0 && c->failcnt > 0) h = GC_H_FAILED;
+        else if (c->loop_err) h = GC_H_STALLED;
+        else if (c->bcnt[check_ws] + c->bcnt[3 + check_ws] + c->bcnt[6 + check_ws]) h = GC_H_SWEEPS;
+        if (h != GC_RUN) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) c->halt = h;
+            return;
+        }
+    }
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
@@ -1198,7 +1217,116 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // (k_b_reset keeps it).  A round that ends the colouring (no uncoloured vertex) or
     // fails (bounded attempt) has only run fold passes, which change no colour.
     long long prev_passes = 2, prevU = 0, prev_maxmex = -1;
-    for (long long r = 0;; ++r) {
+    // Pipelined rounds (GC_B_PIPE, default on): round r + 1 is enqueued before the host reads
+    // round r's snapshot, and round r's commit makes the round's decisions itself
+    // (k_b_commit's check_ws): the device never idles on the host's round trip (~25 ms of
+    // R-MAT-24's colouring, one per round).  A round the commit halts -- done, failed, or a fold
+    // the enqueued passes did not finish -- leaves the next round a no-op (k_b_reset), which the
+    // host discards; an unfinished fold is finished by host passes as below and the pipeline
+    // restarts after its commit.
+    const bool pipe = !(getenv("GC_B_PIPE") && atoi(getenv("GC_B_PIPE")) == 0) && g->hsnap_dev != nullptr;
+    long long passes_of[2] = {0, 0};
+    auto enqueue_passes_into = [&](long long& passes, long long k) {
+        for (long long j = 0; j < k; ++j, ++passes) {
+            const int pi = (int)(passes % 3);
+            GC_LAUNCH(k_b_ev, dim3(grid_ev), dim3(GC_BLOCK), 0, s, d, B, ev, pi);
+            GC_LAUNCH(k_b_adm, dim3(grid_adm), dim3(GC_BLOCK), 0, s, d, B, (const int*)ev, pi);
+        }
+    };
+    auto enqueue_round = [&](long long rr) -> int {
+        kt.begin(GC_K_OTHER);
+        GC_LAUNCH(k_b_reset, dim3(1), dim3(64), 0, s, d, rr);
+        gcl_fsort(d, L, g->fsum, s);
+        gcl_pack_c4(d, s);
+        kt.begin(GC_K_PROPOSE);
+        gcl_propose(d, L, s);
+        gcl_propose_block(d, L, s);
+        if (h.kbound == 0) {
+            GC_HIP(hipMemsetAsync(&g->ctl->failcnt, 0, sizeof(ull), s));
+            GC_LAUNCH(k_b_fail0, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L);
+        }
+        kt.begin(GC_K_RESOLVE);
+        GC_LAUNCH(k_b_init, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, B, ev, (const int*)g->neq);
+        long long passes = 0;
+        if (b_async_grid > 0) {
+            enqueue_passes_into(passes, b_async_k);
+            if (b_async_k > 0) GC_HIP(hipMemsetAsync(&g->ctl->async_abort[0], 0, sizeof(int), s));
+            GC_LAUNCH(k_b_async, dim3(b_async_grid), dim3(GC_BLOCK), 0, s, d, B, ev, (int)(passes % 3), b_async_budget);
+            ++passes;
+        } else {
+            enqueue_passes_into(passes, std::max(2ll, std::min(prev_passes, 24ll)));
+        }
+        kt.begin(GC_K_COMMIT);
+        GC_LAUNCH(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist, (int)(passes % 3));
+        if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
+        kt.close();
+        gcl_snap(g->ctl, g->hsnap_dev + (rr & 1), s);
+        GC_HIP(hipGetLastError());
+        GC_HIP(hipEventRecord(g->evsnap[rr & 1], s));
+        passes_of[rr & 1] = passes;
+        return GC_OK;
+    };
+    if (pipe) {
+        if ((rc = enqueue_round(0))) return rc;
+        long long next = 1;
+        for (long long cur = 0;;) {
+            if (next > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
+            if ((rc = enqueue_round(next))) return rc;  // one round ahead: two in flight, two slots
+            ++next;
+            GC_HIP(hipEventSynchronize(g->evsnap[cur & 1]));
+            DevCtl sn;
+            memcpy(&sn, &g->hsnap[cur & 1], sizeof(DevCtl));
+            if (sn.loop_err == GC_LERR_LIST) { gc_set_error("variant B: a work-list append passed the list's capacity"); return GC_EHIP; }
+            if (sn.loop_err == 2) { gc_set_error("k_b_async: work list count out of range"); return GC_EHIP; }
+            const long long U = (long long)sn.fcnt[0];
+            const long long np = passes_of[cur & 1];
+            if (sn.halt == GC_RUN) {
+                recs.push_back(RoundRec{U, U, (long long)sn.maxmex, (long long)sn.accepted, 0, np});
+                sweeps_total += np;
+                prev_passes = np;
+                ++cur;
+                continue;
+            }
+            if (sn.halt == GC_H_DONE) {  // coloring_optimized.py: no uncoloured vertex left
+                recs.push_back(RoundRec{0, 0, -1, 0, 0, 0});
+                break;
+            }
+            if (sn.halt == GC_H_FAILED) {  // state at the round start is returned
+                recs.push_back(RoundRec{U, U, (long long)sn.maxmex, 0, 0, 0});
+                status = GC_FAILED;
+                fail_round = cur;
+                fail_count = (long long)sn.failcnt;
+                break;
+            }
+            if (sn.halt != GC_H_SWEEPS) { gc_set_error("variant B: unexpected halt %d", sn.halt); return GC_EHIP; }
+            // round cur's fold is unfinished (round cur + 1 ran as a no-op): its passes, its commit
+            if ((rc = R.sync())) return rc;
+            GC_HIP(hipMemsetAsync(&g->ctl->halt, 0, sizeof(int), s));
+            long long passes = np;
+            for (long long batch = 4;; batch = std::min(batch * 2, 16ll)) {
+                const int ws = (int)(passes % 3);
+                if (h.bcnt[ws] + h.bcnt[3 + ws] + h.bcnt[6 + ws] == 0) break;
+                if (passes > 2 * g->n + 64) { gc_set_error("variant B passes do not converge"); return GC_EROUNDS; }
+                kt.begin(GC_K_RESOLVE);
+                enqueue_passes_into(passes, batch);
+                kt.close();
+                if ((rc = R.sync())) return rc;
+            }
+            kt.begin(GC_K_COMMIT);
+            GC_LAUNCH(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist, -1);
+            if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
+            kt.close();
+            if ((rc = R.sync())) return rc;
+            recs.push_back(RoundRec{U, U, (long long)sn.maxmex, (long long)h.accepted, 0, passes});
+            sweeps_total += passes;
+            prev_passes = passes;
+            ++cur;
+            next = cur;  // the no-op round again
+            if ((rc = enqueue_round(next))) return rc;
+            ++next;
+        }
+    }
+    for (long long r = 0; !pipe; ++r) {
         if (r > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
         kt.begin(GC_K_OTHER);
         GC_LAUNCH(k_b_reset, dim3(1), dim3(64), 0, s, d, r);
@@ -1267,7 +1395,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if ((rc = synced())) return rc;
         }
         kt.begin(GC_K_COMMIT);
-        GC_LAUNCH(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist);
+        GC_LAUNCH(k_b_commit, dim3(GC_ROUND_GRID), dim3(GC_BLOCK), 0, s, d, L, (const int*)ev, g->ulist, -1);
         if (d.hbits_w) gcl_hub_push_big(d, g->ulist, &g->ctl->bigw_cnt, s);
         prev_passes = passes;
         prevU = U;

@@ -154,16 +154,20 @@ FOLD_SETTINGS = [
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "3"},
     {"GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"},                       # gives up at once: hands back to passes
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_BPC": "1"},                           # one workgroup per CU
+    {"GC_B_PIPE": "0"},                                                   # one host wait per round, no pipelining
+    {"GC_B_PIPE": "0", "GC_B_ASYNC": "0"},
+    {"GC_B_PIPE": "0", "GC_B_ASYNC": "1", "GC_ASYNC_BUDGET_US": "0"},
 ]
 
 
 @pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort",
-                                                    "async_bpc1"])
+                                                    "async_bpc1", "nopipe", "nopipe_grid", "nopipe_abort"])
 def test_variant_b_fold(monkeypatch, env):
     """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
     default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
-    every run equal to the oracle."""
-    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC"):
+    pipelined rounds (the default: the commit decides done / failed / unfinished) and one
+    host wait per round (GC_B_PIPE=0) -- every run equal to the oracle."""
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC", "GC_B_PIPE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)

@@ -150,6 +150,11 @@ case ${1:-} in
   fin) exec_steps=(tests smoke bench:rmat24 "bench:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end,--steps,3,--warmup,1"
                    "bench:rmat24:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end"
                    "bench:mesh512:--no-cpu-baseline,--no-end-to-end" "bench:uniform10M:--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin" >&2; exit 2 ;;
+  # ad: variant B's pipelined rounds (the commit decides; round r + 1 in flight while the host reads
+  #     round r): variant B parity (incl. forced give-ups and the passes-only path), the A/B
+  ad) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_resume.py
+                  env:AB_VARIANT=B ab:rmat24:4:base,nopipe=GC_B_PIPE:0 ab:rmat26:2:base,nopipe=GC_B_PIPE:0
+                  ab:uniform10M:4:base,nopipe=GC_B_PIPE:0 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
