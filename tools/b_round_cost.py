@@ -71,6 +71,7 @@ def analyze(trace, rec_path):
         a["wall_us"] += wall
         for nm, t0, t1 in rnd:
             d = (t1 - t0) / 1e3
+            a["busy_us"] += d
             if nm == "k_b_adm":
                 a["passes"] += 1
                 if first:
@@ -100,6 +101,9 @@ def analyze(trace, rec_path):
               f"{a['async_us'] / 1e3:>8.1f} {a['other_us'] / 1e3:>8.1f} {statistics.median(per_round[c]):>12.1f}")
         top = sorted(((k[6:], v) for k, v in a.items() if k.startswith("other:")), key=lambda kv: -kv[1])[:5]
         print(" " * 18 + "rest: " + ", ".join(f"{k} {v / 1e3:.1f}" for k, v in top))
+    tw = sum(a["wall_us"] for a in agg.values())
+    tb = sum(a["busy_us"] for a in agg.values())
+    print(f"rounds' wall {tw / 1e3:.1f} ms, kernels busy {tb / 1e3:.1f} ms, idle {(tw - tb) / 1e3:.1f} ms")
     if async_per_round:
         print("k_b_async per round (round, U, us): first 16 and every 25th")
         sel = async_per_round[:16] + async_per_round[16::25]

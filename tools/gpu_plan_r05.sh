@@ -155,6 +155,8 @@ case ${1:-} in
   ad) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_resume.py
                   env:AB_VARIANT=B ab:rmat24:4:base,nopipe=GC_B_PIPE:0 ab:rmat26:2:base,nopipe=GC_B_PIPE:0
                   ab:uniform10M:4:base,nopipe=GC_B_PIPE:0 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad" >&2; exit 2 ;;
+  # ae: where variant B's round goes with and without pipelining (kernel traces, per-round wall)
+  ae) exec_steps=(brounds:rmat24 env:GC_B_PIPE=0 brounds:rmat24 env:GC_B_PIPE=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
