@@ -44,3 +44,37 @@ def test_gen_uniform_host_entry_point():
 def test_last_error_is_callable():
     from gcolor_amd import _native
     assert isinstance(_native.load().gc_last_error(), bytes)
+
+
+def test_input_stream_is_set_around_one_call_and_restored():
+    """engine._input_stream names the caller's stream for one call (gc_set_input_stream) and
+    restores the device-wide ordering afterwards, also when the call raises; None leaves the
+    library untouched (no GPU needed: the library's setter only records the value)."""
+    import ctypes
+    from gcolor_amd import engine
+
+    calls = []
+
+    class Lib:
+        def gc_set_input_stream(self, stream, enable):
+            calls.append((stream.value if isinstance(stream, ctypes.c_void_p) else stream, enable))
+            return 0
+
+    lib = Lib()
+    with engine._input_stream(lib, None):
+        pass
+    assert calls == []
+    with engine._input_stream(lib, 0x1234):
+        assert calls == [(0x1234, 1)]
+    assert calls[-1] == (None, 0)
+    calls.clear()
+    try:
+        with engine._input_stream(lib, 0x10):
+            raise RuntimeError("inside")
+    except RuntimeError:
+        pass
+    assert calls == [(0x10, 1), (None, 0)]
+    # the real library accepts the setting on a host without a GPU
+    from gcolor_amd import _native as nat
+    real = nat.load()
+    assert real.gc_set_input_stream(ctypes.c_void_p(0), 0) == 0
