@@ -160,6 +160,8 @@ case ${1:-} in
   # af: variant A's launch-shape knobs re-swept on today's engine (most were set in round 2)
   af) exec_steps=("ab:rmat24:4:base,c512=GC_GRID_C:512,c1024=GC_GRID_C:1024,p512=GC_GRID_P:512,p2048=GC_GRID_P:2048,cb512=GC_GRID_CB:512,cb2048=GC_GRID_CB:2048,br1024=GC_BIGROW:1024,br4096=GC_BIGROW:4096"
                   "ab:rmat24:4:base,b2=GC_BATCH_MAX:2,b8=GC_BATCH_MAX:8,abpc3=GC_ASYNC_BPC:3,s128=GC_GRID_S:128,s512=GC_GRID_S:512,ps256=GC_GRID_PS:256,ps1024=GC_GRID_PS:1024,r512=GC_GRID_R:512,r2048=GC_GRID_R:2048") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af" >&2; exit 2 ;;
+  # ag: the rocprofv3 summaries of C5 (R-MAT-28 on one GPU) for its bench line's traffic
+  ag) exec_steps=("profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
