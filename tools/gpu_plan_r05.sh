@@ -162,6 +162,10 @@ case ${1:-} in
                   "ab:rmat24:4:base,b2=GC_BATCH_MAX:2,b8=GC_BATCH_MAX:8,abpc3=GC_ASYNC_BPC:3,s128=GC_GRID_S:128,s512=GC_GRID_S:512,ps256=GC_GRID_PS:256,ps1024=GC_GRID_PS:1024,r512=GC_GRID_R:512,r2048=GC_GRID_R:2048") ;;
   # ag: the rocprofv3 summaries of C5 (R-MAT-28 on one GPU) for its bench line's traffic
   ag) exec_steps=("profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag" >&2; exit 2 ;;
+  # ah: entries in flight per lane on today's engine (GC_SLOTS 1 / 2 / 4: the light kernels' edge
+  #     chunks; GC_CSLOTS 4: the commit's claims), where the rounds are bandwidth-bound (R-MAT-26/28)
+  ah) exec_steps=("abl:rmat26:3:2:base=-,s4=variants/s4/libgcolor.so,cs4=variants/cs4/libgcolor.so,s1=variants/s1/libgcolor.so"
+                  "abl:rmat24:3:2:base=-,s4=variants/s4/libgcolor.so,cs4=variants/cs4/libgcolor.so") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
