@@ -303,3 +303,23 @@ def test_hybrid_switch_after_peak(parts):
             assert_matches_oracle(r, o)
         if len(F) > sh.SWITCH_GRACE and any(f > 0 for f in F[sh.SWITCH_GRACE:]):
             assert calls[0][0] == next(i for i, f in enumerate(F) if i >= sh.SWITCH_GRACE and f > 0)
+
+
+@pytest.mark.parametrize("world,switch_below,deferred_ops", [(4, None, False), (4, 60, True), (8, 60, False)])
+def test_gloo_more_ranks(world, switch_below, deferred_ops, tmp_path):
+    """The driver's scaling runs use 4 and 8 ranks: the same exchange with 4 / 8 gloo processes
+    (every round sharded, and the hybrid's hand-over), every rank bit-exact with the oracle."""
+    ids, adj, rp, col = fixture_csr(load_golden("gen_1000_8_s1"))
+    path = str(tmp_path / "g.npz")
+    np.savez(path, rp=rp, col=col)
+    port = free_port()
+    torch.multiprocessing.spawn(_gloo_worker,
+                                args=(world, port, path, str(tmp_path), None, 4096, deferred_ops, switch_below),
+                                nprocs=world, join=True)
+    o = oracle.c_color(rp, col, "A")
+    for r in range(world):
+        got = json.load(open(tmp_path / f"r{r}.json"))
+        assert got["status"] == o["status"]
+        assert got["colors"] == list(o["colors"])
+        assert got["cround"] == list(o["colored_round"])
+        assert got["U"] == list(o["round_U"]) and got["acc"] == list(o["round_accepted"])
