@@ -529,6 +529,8 @@ class MultiStep:
         self.args, self.world, self.rank, self.comm, self.torch, self.dist = args, world, rank, comm, torch, dist
         self.sh = sh
         dg0, _ = build_graph(w)  # every rank generates the same graph (deterministic, on its own GPU)
+        if rank == 0:
+            progress(f"rank 0: graph generated ({dg0.n} vertices, {dg0.nnz} entries)")
         self.n, self.nnz, self.max_degree, self.sym = dg0.n, dg0.nnz, dg0.max_degree, dg0.symmetric
         rp, _ = dg0.export(col=False)
         self.ranges = sh.balanced_ranges(rp, world)
@@ -536,6 +538,8 @@ class MultiStep:
         del rp
         self.d_rp, self.d_col = resident_csr(dg0, torch)
         dg0.close()
+        if rank == 0:
+            progress("rank 0: resident CSR ready")
         self.hybrid = args.multi == "hybrid"
         self.switch_below = args.switch_below if args.switch_below > 0 else max(4096, self.n // 64)
 

@@ -169,7 +169,7 @@ case ${1:-} in
   # ai: bench.py --gpus 4 and --gpus 8 end to end (it starts the ranks itself), every rank on this
   #     box's one GPU over gloo: the 4- and 8-rank paths of the driver's scaling runs, not timings
   ai) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
-                  "bench:rmat24:--gpus,4,--steps,1,--warmup,1" "bench:rmat24:--gpus,8,--steps,1,--warmup,1"
+                  "bench:rmat20:--gpus,4,--steps,1,--warmup,1" "bench:rmat20:--gpus,8,--steps,1,--warmup,1"
                   env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
   *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai" >&2; exit 2 ;;
 esac
