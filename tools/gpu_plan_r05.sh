@@ -171,6 +171,9 @@ case ${1:-} in
   ai) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
                   "bench:rmat20:--gpus,4,--steps,1,--warmup,1" "bench:rmat20:--gpus,8,--steps,1,--warmup,1"
                   env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai" >&2; exit 2 ;;
+  # aj: variant B's fold, first scans against rescans per round (variants/bprof: -DGC_B_PROF=1)
+  aj) exec_steps=(env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05aj/bprof_rmat24.txt
+                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05aj/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
