@@ -593,10 +593,16 @@ struct BAsyncLds {  // one wave's rows
 // one pass over the wave's light admission / eviction items l1[0, n1); the unsettled ones
 // are compacted to the front (an admitted vertex comes back as an eviction item); returns
 // their number
-// Watched entries (g.b_watch = R > 0): an admission item's full rescan of its pending entries
-// waits until the smallest of them (B.watch[v], the entry the fold most likely settles first)
-// settles, or every R-th pass of the wave -- between those, a pass checks that one entry.
-// Refusals by other entries are only seen later; the decisions are the same.
+// Admission cursors (g.b_watch = R > 0): between full rescans (every R-th pass of the wave) an
+// admission item reads only a window of GC_B_AWIN of its pending entries from a cursor
+// (B.watch[v]: the entries before it are settled 0), advances the cursor past the settled
+// prefix and stops at the first entry still pending; a refusal in the window settles it, the
+// cursor reaching the end admits it.  Each pending entry is then read about once more after it
+// settles, where a rescan of every pending entry per settled one cost O(pending^2) (round 5:
+// 5.8 of the fold's 10.7 G entries were admission rescans on R-MAT-24).  A refusal by an entry
+// past the first pending one is seen at the next full rescan at the latest; the decisions are
+// the same.
+#define GC_B_AWIN 16
 __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, ull* scanned,
                                   ull npass) {
     const bool full_pass = g.b_watch <= 0 || npass % (ull)g.b_watch == 0;
@@ -615,15 +621,21 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + ev[v]));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
-        bool held = false;  // admission item whose watched entry is still pending: no rescan
-        if (kind == 0 && lc < 0 && !full_pass) {
-            const int wu = B.watch[v];
-            held = wu >= 0 && wu < g.n && b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), gc_k8_cand(kv), b_cand(g, v, kv), ev) == 2u;
+        // admission items in the pending-list form: cursor and pending count
+        const int anp = (kind == 0 && lc < 0) ? -lc - 1 : 0;
+        int acur = 0;
+        if (kind == 0 && lc < 0 && g.b_watch > 0) {
+            acur = B.watch[v];
+            acur = acur < 0 ? 0 : (acur > anp ? anp : acur);
         }
+        const bool win = kind == 0 && lc < 0 && !full_pass;  // a window from the cursor
         int len = 0;
-        if (kind == 0 && !held) {
-            len = lc >= 0 ? b_adm_end(g, B, v) - lc : -lc - 1;
-            s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0;
+        if (win) {
+            len = anp - acur < GC_B_AWIN ? anp - acur : GC_B_AWIN;
+            s.src[lane] = B.pend + r0 + acur;
+        } else if (kind == 0) {
+            len = lc >= 0 ? b_adm_end(g, B, v) - lc : anp - acur;
+            s.src[lane] = lc >= 0 ? g.col + r0 + lc : B.pend + r0 + acur;
         } else if (kind == 2 && lc == GC_B_EVCOL) {
             const int lo = b_adm_end(g, B, v);
             len = d - lo;
@@ -640,7 +652,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         s.d[lane] = d;
         s.c6[lane] = v >= 0 ? gc_k8_cand(kv) : 0x100u;
         s.cv[lane] = v >= 0 ? b_cand(g, v, kv) : -1;
-        s.kind[lane] = kind;
+        s.kind[lane] = win ? 1 : kind;  // (1: an admission window; no heavy item is listed here)
         const int incl = gc_wave_incl_scan(len);
         const int excl = incl - len;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -653,16 +665,17 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
                 const ull k = (ull)gc_ald8(g.k8 + u);
                 return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
             },
-            [&](int o, int um, ull du, int) {
+            [&](int o, int um, ull du, int x) {
                 const int u = um & 0x7FFFFFFF;
                 const unsigned ku = (unsigned)du & 0xFFu;
-                if (s.kind[o] == 0) {  // admission (k_b_adm)
+                if (s.kind[o] == 1) {  // admission window: the first entry still pending
                     const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
                     if (f) atomicOr(&s.flag[o], f);
-                    if (f == 2u) {
-                        s.dst[o][atomicAdd(&s.np[o], 1)] = u;
-                        atomicMin(&s.minv[o], u);
-                    }
+                    if (f == 2u) atomicMin(&s.minv[o], x);
+                } else if (s.kind[o] == 0) {  // admission (k_b_adm)
+                    const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
+                    if (f) atomicOr(&s.flag[o], f);
+                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
                 } else {  // eviction time (k_b_ev)
                     if (gc_k8_state(ku) == GC_JP_OUT) return;
                     if (!((unsigned)um & GC_B_PMARK)) {
@@ -673,18 +686,29 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
                 }
             },
-            [&](int o) { return g.b_refskip && s.kind[o] == 0 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
+            [&](int o) { return g.b_refskip && s.kind[o] <= 1 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         int keep = -1;  // the item that stays (-1: settled)
-        if (kind == 0 && held) {
-            keep = it;
+        if (win) {
+            const unsigned f = s.flag[lane];
+            const int x = s.minv[lane];
+            if (f & 1u) {
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
+            } else if (x != GC_B_INF || acur + len < anp) {  // still pending: past the settled prefix
+                B.watch[v] = acur + (x != GC_B_INF ? x : len);
+                keep = it;
+            } else {  // every pending entry settled 0
+                g.lcur[v] = GC_B_EVCOL;
+                gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_IN);
+                keep = v | (2 << GC_BI_SHIFT);
+            }
         } else if (kind == 0) {
             const unsigned f = s.flag[lane];
             if (f & 1u) {
                 gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
             } else if (f & 2u) {
                 g.lcur[v] = -s.np[lane] - 1;
-                if (g.b_watch > 0) B.watch[v] = s.minv[lane];
+                if (g.b_watch > 0) B.watch[v] = 0;  // the compacted list from its start
                 keep = it;
             } else {
                 g.lcur[v] = GC_B_EVCOL;
@@ -822,19 +846,27 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
     const int cv = v >= 0 ? b_cand(g, v, kv) : -1;
     int n = __popcll(__ballot(v >= 0));
     int idle = 0;
-    int wu = (kind == 0 && g.b_watch > 0) ? B.watch[v] : -1;  // admission items: the watched entry
+    int acur = 0;  // admission items: the cursor into their pending entries (b_async_chunk_pass)
+    if (kind == 0 && g.b_watch > 0) {
+        acur = B.watch[v];
+        acur = acur < 0 ? 0 : (acur > np ? np : acur);
+    }
     while (n > 0) {
         ++*npass;
-        bool held = false;
-        if (kind == 0 && wu >= 0 && wu < g.n && g.b_watch > 0 && *npass % (ull)g.b_watch != 0)
-            held = b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), c6, cv, ev) == 2u;
+        const bool win = kind == 0 && g.b_watch > 0 && *npass % (ull)g.b_watch != 0;
         int watch = 0;  // eviction items: 1 still pending, 2 final, no scan
         if (kind == 2 && !evcol) {
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + evv));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
         int len = 0;
-        if ((kind == 0 && !held) || (kind == 2 && !evcol && watch == 0)) {
+        if (win) {
+            len = np - acur < GC_B_AWIN ? np - acur : GC_B_AWIN;
+            s.src[lane] = pe + off + acur;
+        } else if (kind == 0) {
+            len = np - acur;
+            s.src[lane] = pe + off + acur;
+        } else if (kind == 2 && !evcol && watch == 0) {
             len = np;
             s.src[lane] = pe + off;
         } else if (kind == 2 && evcol) {
@@ -849,7 +881,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         s.d[lane] = d;
         s.c6[lane] = c6;
         s.cv[lane] = cv;
-        s.kind[lane] = kind;
+        s.kind[lane] = win ? 1 : kind;
         const int li = gc_wave_incl_scan(len);
         const int le = li - len;
         const int total = __shfl(li, GC_WAVE - 1, GC_WAVE);
@@ -862,16 +894,17 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                 const ull k = (ull)gc_ald8(g.k8 + u);
                 return (s.kind[o] == 2 && !((unsigned)um & GC_B_PMARK)) ? ((ull)(unsigned)g.deg[u] << 32) | k : k;
             },
-            [&](int o, int um, ull du, int) {
+            [&](int o, int um, ull du, int x) {
                 const int u = um & 0x7FFFFFFF;
                 const unsigned ku = (unsigned)du & 0xFFu;
-                if (s.kind[o] == 0) {
+                if (s.kind[o] == 1) {  // admission window
                     const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
                     if (f) atomicOr(&s.flag[o], f);
-                    if (f == 2u) {
-                        s.dst[o][atomicAdd(&s.np[o], 1)] = u;
-                        atomicMin(&s.minv[o], u);
-                    }
+                    if (f == 2u) atomicMin(&s.minv[o], x);
+                } else if (s.kind[o] == 0) {
+                    const unsigned f = b_adm_flag_a(g, s.v[o], u, ku, s.c6[o], s.cv[o], ev);
+                    if (f) atomicOr(&s.flag[o], f);
+                    if (f == 2u) s.dst[o][atomicAdd(&s.np[o], 1)] = u;
                 } else {
                     if (gc_k8_state(ku) == GC_JP_OUT) return;
                     if (!((unsigned)um & GC_B_PMARK)) {
@@ -882,19 +915,23 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
                     s.dst[o][atomicAdd(&s.np[o], 1)] = (int)((unsigned)u | GC_B_PMARK);
                 }
             },
-            [&](int o) { return g.b_refskip && s.kind[o] == 0 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
+            [&](int o) { return g.b_refskip && s.kind[o] <= 1 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         bool keep = false;
-        if (kind == 0 && held) {
+        const unsigned af = s.flag[lane];
+        const int ax = s.minv[lane];
+        const bool apend = kind == 0 && !(af & 1u) && (win ? (ax != GC_B_INF || acur + len < np) : (af & 2u) != 0);
+        if (kind == 0 && apend) {
+            if (win) {
+                acur += ax != GC_B_INF ? ax : len;
+            } else {
+                np = s.np[lane];
+                acur = 0;
+            }
             keep = true;
         } else if (kind == 0) {
-            const unsigned f = s.flag[lane];
-            if (f & 1u) {
+            if (af & 1u) {
                 gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
-            } else if (f & 2u) {
-                np = s.np[lane];
-                wu = s.minv[lane];
-                keep = true;
             } else {  // admitted: its eviction time next (the row's higher-rank part first)
                 kv = (kv & ~3u) | GC_JP_IN;
                 gc_ast8(g.k8 + v, kv);
@@ -935,7 +972,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
     }
     // stopped: back to the global form -- cursor words, watched entries, entries, the item list
     if (v >= 0) g.lcur[v] = evcol ? GC_B_EVCOL : -np - 1;
-    if (kind == 0 && g.b_watch > 0) B.watch[v] = wu;
+    if (kind == 0 && g.b_watch > 0) B.watch[v] = acur;
     {
         const int pin = gc_wave_incl_scan(v >= 0 ? np : 0);
         const int pex = pin - (v >= 0 ? np : 0);

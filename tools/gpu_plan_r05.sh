@@ -174,6 +174,12 @@ case ${1:-} in
   # aj: variant B's fold, first scans against rescans per round (variants/bprof: -DGC_B_PROF=1)
   aj) exec_steps=(env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05aj/bprof_rmat24.txt
                   "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05aj/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_B_PROF_OUT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj" >&2; exit 2 ;;
+  # ak: admission cursors (a window of pending entries from a cursor between full rescans, instead
+  #     of a full rescan whenever the smallest pending entry settles): variant B parity, the A/B
+  #     against the previous build (variants/prev), the watch period
+  ak) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_parity.py
+                  env:AB_VARIANT=B "abl:rmat24:3:2:base=-,prev=variants/prev/libgcolor.so" "abl:rmat26:2:2:base=-,prev=variants/prev/libgcolor.so"
+                  ab:rmat24:3:base,w4=GC_B_WATCH:4,w32=GC_B_WATCH:32 env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
