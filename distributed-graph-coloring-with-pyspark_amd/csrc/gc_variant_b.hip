@@ -177,6 +177,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_b_init(GDev g, GLists L, BLists B,
             const int bc = g.nlow[v] - neq[v];
             g.lcur[v] = bc;
             ev[v] = -1;
+            B.watch[v] = 0;
             heavy = b_adm_end(g, B, v) - bc > GC_B_HEAVY;
         }
         gc_wave_append(heavy, v, B.l[1][0], b_cnt(c, 1, 0));
@@ -432,6 +433,7 @@ __device__ void b_adm_pass(GDev& g, BLists& B, const int* ev, int pass, int bid,
                 g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_OUT);
             } else if (f & 2u) {
                 g.lcur[v] = -s_np[w][lane] - 1;
+                B.watch[v] = 0;  // the compacted list from its start (the asynchronous fold's cursor)
                 kind = 0;
             } else {
                 g.k8[v] = (unsigned char)((kv & ~3u) | GC_JP_IN);
