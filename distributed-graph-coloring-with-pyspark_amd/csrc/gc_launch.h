@@ -60,8 +60,10 @@ struct GDev {
     int tail_hmax;            // heavy entries the one-workgroup tail sweeps may take (GC_TAIL_HMAX[_HUB])
     int b_resident;           // variant B: the asynchronous fold's resident form on (b_async_resident)
     int a_watch;              // variant A's asynchronous JP: held lights between full passes every a_watch-th (0 off)
-    int b_watch;
-    int b_refskip;            // variant B's asynchronous fold: a refused admission reads no more entries              // variant B: admission rescans only when the watched entry settles, or every b_watch-th pass (0 off)
+    int b_watch;              // variant B's asynchronous fold: a full admission rescan every b_watch-th pass, a
+                              //   window of b_awin pending entries from the cursor between them (0 off)
+    int b_awin;
+    int b_refskip;            // variant B's asynchronous fold: a refused admission reads no more entries
     int tail_lmax;            // light entries the tail sweeps may take (GC_TAIL_MAX; env GC_TAIL_LMAX)
     int tail_nw;              // waves of the tail's workgroup: 4, 8 or 16 (env GC_TAIL_WAVES)
     int heavy_wg;             // heavy vertices are resolved a workgroup each (no hub JP, some deg > heavy_t):

@@ -596,7 +596,7 @@ struct BAsyncLds {  // one wave's rows
 // are compacted to the front (an admitted vertex comes back as an eviction item); returns
 // their number
 // Admission cursors (g.b_watch = R > 0): between full rescans (every R-th pass of the wave) an
-// admission item reads only a window of GC_B_AWIN of its pending entries from a cursor
+// admission item reads only a window of g.b_awin of its pending entries from a cursor
 // (B.watch[v]: the entries before it are settled 0), advances the cursor past the settled
 // prefix and stops at the first entry still pending; a refusal in the window settles it, the
 // cursor reaching the end admits it.  Each pending entry is then read about once more after it
@@ -604,7 +604,6 @@ struct BAsyncLds {  // one wave's rows
 // 5.8 of the fold's 10.7 G entries were admission rescans on R-MAT-24).  A refusal by an entry
 // past the first pending one is seen at the next full rescan at the latest; the decisions are
 // the same.
-#define GC_B_AWIN 16
 __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, ull* scanned,
                                   ull npass) {
     const bool full_pass = g.b_watch <= 0 || npass % (ull)g.b_watch == 0;
@@ -633,7 +632,7 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         const bool win = kind == 0 && lc < 0 && !full_pass;  // a window from the cursor
         int len = 0;
         if (win) {
-            len = anp - acur < GC_B_AWIN ? anp - acur : GC_B_AWIN;
+            len = anp - acur < g.b_awin ? anp - acur : g.b_awin;
             s.src[lane] = B.pend + r0 + acur;
         } else if (kind == 0) {
             len = lc >= 0 ? b_adm_end(g, B, v) - lc : anp - acur;
@@ -863,7 +862,7 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
         }
         int len = 0;
         if (win) {
-            len = np - acur < GC_B_AWIN ? np - acur : GC_B_AWIN;
+            len = np - acur < g.b_awin ? np - acur : g.b_awin;
             s.src[lane] = pe + off + acur;
         } else if (kind == 0) {
             len = np - acur;
@@ -1176,6 +1175,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // watched entries (b_async_chunk_pass): a full admission rescan every GC_B_WATCH-th pass at most
     // otherwise; 0 off
     R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 8;
+    R.d.b_awin = getenv("GC_B_AWIN") ? atoi(getenv("GC_B_AWIN")) : 16;  // the window's entries
+    if (R.d.b_awin < 1) R.d.b_awin = 1;
     R.d.b_refskip = getenv("GC_B_REFSKIP") ? atoi(getenv("GC_B_REFSKIP")) : 1;
     const hipStream_t s = R.s;
     const GDev& d = R.d;

@@ -180,6 +180,10 @@ case ${1:-} in
   ak) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" file:tests/test_gpu_parity.py
                   env:AB_VARIANT=B "abl:rmat24:3:2:base=-,prev=variants/prev/libgcolor.so" "abl:rmat26:2:2:base=-,prev=variants/prev/libgcolor.so"
                   ab:rmat24:3:base,w4=GC_B_WATCH:4,w32=GC_B_WATCH:32 env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak" >&2; exit 2 ;;
+  al) exec_steps=(file:tests/test_gpu_variant_b.py env:AB_VARIANT=B
+                  "ab:rmat24:3:base,w4=GC_B_WATCH:4,w2=GC_B_WATCH:2,w4a32=GC_B_WATCH:4+GC_B_AWIN:32,w4a8=GC_B_WATCH:4+GC_B_AWIN:8,w8a32=GC_B_AWIN:32,w8a64=GC_B_AWIN:64"
+                  "ab:rmat26:2:base,w4=GC_B_WATCH:4,w4a32=GC_B_WATCH:4+GC_B_AWIN:32,w8a32=GC_B_AWIN:32"
+                  env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
