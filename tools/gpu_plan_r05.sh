@@ -184,6 +184,10 @@ case ${1:-} in
                   "ab:rmat24:3:base,w4=GC_B_WATCH:4,w2=GC_B_WATCH:2,w4a32=GC_B_WATCH:4+GC_B_AWIN:32,w4a8=GC_B_WATCH:4+GC_B_AWIN:8,w8a32=GC_B_AWIN:32,w8a64=GC_B_AWIN:64"
                   "ab:rmat26:2:base,w4=GC_B_WATCH:4,w4a32=GC_B_WATCH:4+GC_B_AWIN:32,w8a32=GC_B_AWIN:32"
                   env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al" >&2; exit 2 ;;
+  am) exec_steps=(env:AB_VARIANT=B
+                  "ab:rmat24:3:base,a8=GC_B_AWIN:8,a4=GC_B_AWIN:4,w16a8=GC_B_WATCH:16+GC_B_AWIN:8,w16a4=GC_B_WATCH:16+GC_B_AWIN:4,w4a4=GC_B_WATCH:4+GC_B_AWIN:4"
+                  "ab:rmat26:2:base,a8=GC_B_AWIN:8,a4=GC_B_AWIN:4,w16a8=GC_B_WATCH:16+GC_B_AWIN:8,w4a8=GC_B_WATCH:4+GC_B_AWIN:8"
+                  env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
