@@ -595,8 +595,8 @@ struct BAsyncLds {  // one wave's rows
 // one pass over the wave's light admission / eviction items l1[0, n1); the unsettled ones
 // are compacted to the front (an admitted vertex comes back as an eviction item); returns
 // their number
-// Admission cursors (g.b_watch = R > 0): between full rescans (every R-th pass of the wave) an
-// admission item reads only a window of g.b_awin of its pending entries from a cursor
+// Admission cursors (g.b_watch = R > 0, 4): between full rescans (every R-th pass of the wave) an
+// admission item reads only a window of g.b_awin (8) of its pending entries from a cursor
 // (B.watch[v]: the entries before it are settled 0), advances the cursor past the settled
 // prefix and stops at the first entry still pending; a refusal in the window settles it, the
 // cursor reaching the end admits it.  Each pending entry is then read about once more after it
@@ -1174,8 +1174,8 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     R.d.b_resident = getenv("GC_B_RESIDENT") ? atoi(getenv("GC_B_RESIDENT")) : 1;
     // watched entries (b_async_chunk_pass): a full admission rescan every GC_B_WATCH-th pass at most
     // otherwise; 0 off
-    R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 8;
-    R.d.b_awin = getenv("GC_B_AWIN") ? atoi(getenv("GC_B_AWIN")) : 16;  // the window's entries
+    R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 4;
+    R.d.b_awin = getenv("GC_B_AWIN") ? atoi(getenv("GC_B_AWIN")) : 8;  // the window's entries
     if (R.d.b_awin < 1) R.d.b_awin = 1;
     R.d.b_refskip = getenv("GC_B_REFSKIP") ? atoi(getenv("GC_B_REFSKIP")) : 1;
     const hipStream_t s = R.s;

@@ -188,6 +188,9 @@ case ${1:-} in
                   "ab:rmat24:3:base,a8=GC_B_AWIN:8,a4=GC_B_AWIN:4,w16a8=GC_B_WATCH:16+GC_B_AWIN:8,w16a4=GC_B_WATCH:16+GC_B_AWIN:4,w4a4=GC_B_WATCH:4+GC_B_AWIN:4"
                   "ab:rmat26:2:base,a8=GC_B_AWIN:8,a4=GC_B_AWIN:4,w16a8=GC_B_WATCH:16+GC_B_AWIN:8,w4a8=GC_B_WATCH:4+GC_B_AWIN:8"
                   env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am" >&2; exit 2 ;;
+  an) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B"
+                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
+  ao) exec_steps=(profile:mesh512 profile:uniform10M "profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
