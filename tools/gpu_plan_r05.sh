@@ -191,6 +191,13 @@ case ${1:-} in
   an) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B"
                   profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26) ;;
   ao) exec_steps=(profile:mesh512 profile:uniform10M "profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao" >&2; exit 2 ;;
+  # ap: the fold's scanned entries with the admission cursors (variants/bprof: -DGC_B_PROF=1 with the
+  #     first-scan / admission-rescan / eviction-rescan split), and with them off (GC_B_WATCH=0)
+  ap) exec_steps=(env:GC_LIB_PATH=variants/bprof/libgcolor.so env:GC_B_PROF_OUT=gpurun_out/r05ap/bprof_rmat24.txt
+                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ap/records_rmat24.json,1"
+                  env:GC_B_WATCH=0 env:GC_B_PROF_OUT=gpurun_out/r05ap/bprof_rmat24_w0.txt
+                  "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ap/records_rmat24_w0.json,1"
+                  env:GC_LIB_PATH= env:GC_B_PROF_OUT= env:GC_B_WATCH=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
