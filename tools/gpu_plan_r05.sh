@@ -198,6 +198,10 @@ case ${1:-} in
                   env:GC_B_WATCH=0 env:GC_B_PROF_OUT=gpurun_out/r05ap/bprof_rmat24_w0.txt
                   "py:tools/b_round_cost.py:run,rmat24,gpurun_out/r05ap/records_rmat24_w0.json,1"
                   env:GC_LIB_PATH= env:GC_B_PROF_OUT= env:GC_B_WATCH=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap" >&2; exit 2 ;;
+  # aq: the cursor entry checked before the window (GC_B_HOLD): variant B parity, the A/B
+  aq) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" env:AB_VARIANT=B
+                  "ab:rmat24:3:base,hold0=GC_B_HOLD:0,a16=GC_B_AWIN:16,w8a16=GC_B_WATCH:8+GC_B_AWIN:16"
+                  "ab:rmat26:2:base,hold0=GC_B_HOLD:0,a16=GC_B_AWIN:16" env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
