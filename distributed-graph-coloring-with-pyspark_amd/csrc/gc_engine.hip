@@ -116,7 +116,6 @@ GDev gc_view(const gc_graph* g) {
     d.b_resident = 0;
     d.b_watch = 0;
     d.b_awin = 8;
-    d.b_hold = 0;
     d.b_refskip = 0;
     d.a_watch = getenv("GC_A_WATCH") ? atoi(getenv("GC_A_WATCH")) : 0;
     d.tail_lmax = getenv("GC_TAIL_LMAX") ? atoi(getenv("GC_TAIL_LMAX")) : GC_TAIL_MAX;

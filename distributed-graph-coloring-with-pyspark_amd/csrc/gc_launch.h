@@ -63,7 +63,6 @@ struct GDev {
     int b_watch;              // variant B's asynchronous fold: a full admission rescan every b_watch-th pass, a
                               //   window of b_awin pending entries from the cursor between them (0 off)
     int b_awin;
-    int b_hold;               //   ... the cursor entry checked first: still pending, no window read
     int b_refskip;            // variant B's asynchronous fold: a refused admission reads no more entries
     int tail_lmax;            // light entries the tail sweeps may take (GC_TAIL_MAX; env GC_TAIL_LMAX)
     int tail_nw;              // waves of the tail's workgroup: 4, 8 or 16 (env GC_TAIL_WAVES)

@@ -630,17 +630,9 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
             acur = acur < 0 ? 0 : (acur > anp ? anp : acur);
         }
         const bool win = kind == 0 && lc < 0 && !full_pass;  // a window from the cursor
-        // the cursor entry first (g.b_hold): still pending, the item waits without reading its
-        // window; settled 0, the window starts past it; refusing, the item is refused
-        unsigned pre = 0u;
-        if (win && g.b_hold && acur < anp) {
-            const int wu = B.pend[r0 + acur];
-            pre = b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), gc_k8_cand(kv), b_cand(g, v, kv), ev);
-            if (pre == 0u) ++acur;
-        }
         int len = 0;
         if (win) {
-            len = pre ? 0 : (anp - acur < g.b_awin ? anp - acur : g.b_awin);
+            len = anp - acur < g.b_awin ? anp - acur : g.b_awin;
             s.src[lane] = B.pend + r0 + acur;
         } else if (kind == 0) {
             len = lc >= 0 ? b_adm_end(g, B, v) - lc : anp - acur;
@@ -699,12 +691,10 @@ __device__ int b_async_chunk_pass(GDev& g, const BLists& B, int* l1, int n1, int
         gc_wave_sync();
         int keep = -1;  // the item that stays (-1: settled)
         if (win) {
-            const unsigned f = s.flag[lane] | pre;
+            const unsigned f = s.flag[lane];
             const int x = s.minv[lane];
             if (f & 1u) {
                 gc_ast8(g.k8 + v, (kv & ~3u) | GC_JP_OUT);
-            } else if (pre == 2u) {  // the cursor entry still pending
-                keep = it;
             } else if (x != GC_B_INF || acur + len < anp) {  // still pending: past the settled prefix
                 B.watch[v] = acur + (x != GC_B_INF ? x : len);
                 keep = it;
@@ -870,15 +860,9 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
             const unsigned st = gc_k8_state(gc_ald8(g.k8 + evv));
             watch = st == GC_JP_UND ? 1 : (st == GC_JP_IN ? 2 : 0);
         }
-        unsigned pre = 0u;  // the cursor entry first (b_async_chunk_pass)
-        if (win && g.b_hold && acur < np) {
-            const int wu = pe[off + acur];
-            pre = b_adm_flag_a(g, v, wu, gc_ald8(g.k8 + wu), c6, cv, ev);
-            if (pre == 0u) ++acur;
-        }
         int len = 0;
         if (win) {
-            len = pre ? 0 : (np - acur < g.b_awin ? np - acur : g.b_awin);
+            len = np - acur < g.b_awin ? np - acur : g.b_awin;
             s.src[lane] = pe + off + acur;
         } else if (kind == 0) {
             len = np - acur;
@@ -935,10 +919,9 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
             [&](int o) { return g.b_refskip && s.kind[o] <= 1 && (s.flag[o] & 1u); });  // refused: the rest cannot matter
         gc_wave_sync();
         bool keep = false;
-        const unsigned af = s.flag[lane] | pre;
+        const unsigned af = s.flag[lane];
         const int ax = s.minv[lane];
-        const bool apend =
-            kind == 0 && !(af & 1u) && (win ? (pre == 2u || ax != GC_B_INF || acur + len < np) : (af & 2u) != 0);
+        const bool apend = kind == 0 && !(af & 1u) && (win ? (ax != GC_B_INF || acur + len < np) : (af & 2u) != 0);
         if (kind == 0 && apend) {
             if (win) {
                 acur += ax != GC_B_INF ? ax : len;
@@ -1193,7 +1176,6 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
     // otherwise; 0 off
     R.d.b_watch = getenv("GC_B_WATCH") ? atoi(getenv("GC_B_WATCH")) : 4;
     R.d.b_awin = getenv("GC_B_AWIN") ? atoi(getenv("GC_B_AWIN")) : 8;  // the window's entries
-    R.d.b_hold = getenv("GC_B_HOLD") ? atoi(getenv("GC_B_HOLD")) : 1;  // the cursor entry checked first
     if (R.d.b_awin < 1) R.d.b_awin = 1;
     R.d.b_refskip = getenv("GC_B_REFSKIP") ? atoi(getenv("GC_B_REFSKIP")) : 1;
     const hipStream_t s = R.s;

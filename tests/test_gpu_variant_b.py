@@ -160,20 +160,18 @@ FOLD_SETTINGS = [
     {"GC_B_ASYNC": "1", "GC_B_WATCH": "0"},                               # admission cursors off: full rescans
     {"GC_B_ASYNC": "1", "GC_B_WATCH": "64", "GC_B_AWIN": "1"},            # one entry per window, rare rescans
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "1", "GC_B_WATCH": "2", "GC_B_AWIN": "3"},
-    {"GC_B_ASYNC": "1", "GC_B_HOLD": "0"},                                # windows without the cursor-entry check
 ]
 
 
 @pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort",
                                                     "async_bpc1", "nopipe", "nopipe_grid", "nopipe_abort",
-                                                    "cursor_off", "cursor_w1", "cursor_k1_w3", "cursor_nohold"])
+                                                    "cursor_off", "cursor_w1", "cursor_k1_w3"])
 def test_variant_b_fold(monkeypatch, env):
     """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
     default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
     pipelined rounds (the default: the commit decides done / failed / unfinished) and one
     host wait per round (GC_B_PIPE=0) -- every run equal to the oracle."""
-    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC", "GC_B_PIPE", "GC_B_WATCH", "GC_B_AWIN",
-              "GC_B_HOLD"):
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC", "GC_B_PIPE", "GC_B_WATCH", "GC_B_AWIN"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
