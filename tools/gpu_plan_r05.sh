@@ -202,6 +202,10 @@ case ${1:-} in
   aq) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B" env:AB_VARIANT=B
                   "ab:rmat24:3:base,hold0=GC_B_HOLD:0,a16=GC_B_AWIN:16,w8a16=GC_B_WATCH:8+GC_B_AWIN:16"
                   "ab:rmat26:2:base,hold0=GC_B_HOLD:0,a16=GC_B_AWIN:16" env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq" >&2; exit 2 ;;
+  # ar: the N > 1 bench paths on the final build (every rank on this box's one GPU over gloo)
+  ar) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
+                  "bench:rmat24:--gpus,2,--steps,2,--warmup,1" "bench:rmat20:--gpus,4,--steps,1,--warmup,1"
+                  "bench:rmat20:--gpus,8,--steps,1,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
