@@ -206,6 +206,8 @@ case ${1:-} in
   ar) exec_steps=(env:GC_BENCH_BACKEND=gloo env:GC_BENCH_DEVICE=0
                   "bench:rmat24:--gpus,2,--steps,2,--warmup,1" "bench:rmat20:--gpus,4,--steps,1,--warmup,1"
                   "bench:rmat20:--gpus,8,--steps,1,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar" >&2; exit 2 ;;
+  # as: variant B at R-MAT-26 on the final build (trace + PMC passes)
+  as) exec_steps=("profile:rmat26:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
