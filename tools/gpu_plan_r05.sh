@@ -208,6 +208,13 @@ case ${1:-} in
                   "bench:rmat20:--gpus,8,--steps,1,--warmup,1" env:GC_BENCH_BACKEND= env:GC_BENCH_DEVICE=) ;;
   # as: variant B at R-MAT-26 on the final build (trace + PMC passes)
   as) exec_steps=("profile:rmat26:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as" >&2; exit 2 ;;
+  # at: the fold's resident form capped at 1024 / 2048 entries per wave (compile-time; LDS: 5 / 3
+  #     workgroups per CU instead of 4), and 1024 with 5 workgroups per CU (GC_B_ASYNC_BPC=5)
+  at) exec_steps=(env:AB_VARIANT=B
+                  "abl:rmat24:3:2:base=-,r1024=variants/r1024/libgcolor.so,r2048=variants/r2048/libgcolor.so"
+                  env:GC_B_ASYNC_BPC=5 "abl:rmat24:3:2:base=-,r1024b5=variants/r1024/libgcolor.so"
+                  "abl:rmat26:2:2:base=-,r1024b5=variants/r1024/libgcolor.so" env:GC_B_ASYNC_BPC=
+                  "abl:rmat26:2:2:base=-,r1024=variants/r1024/libgcolor.so" env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
