@@ -805,8 +805,8 @@ __device__ int b_async_heavy_pass(GDev& g, const BLists& B, int* l2, int n2, int
 // stop check runs only on a pass without progress.  Returns -1 (not eligible: nothing
 // changed), 0 (every item settled) or the items left on a stop, written back in the global
 // form (l1, lcur, pend) for the hand-off.
-#ifndef GC_B_RES_CAP
-#define GC_B_RES_CAP 1536
+#ifndef GC_B_RES_CAP  // 1024: the fold's LDS allows 5 workgroups per CU (1536: 4; R-MAT-24 -1 to -2%, profiles/r05/at)
+#define GC_B_RES_CAP 1024
 #endif
 __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, int* pe, DevCtl* c,
                                 ull t0, long long budget, bool* stop, ull* npass, ull* scanned) {
@@ -1204,7 +1204,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
             rate_khz > 0) {
-            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 4;
+            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 5;
             // every workgroup resident (gc_resident_blocks_per_cu): the static slices all progress
             b_async_grid = std::min(bpc, std::max(1, gcl_b_async_resident(d, s))) * cus;
             const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
