@@ -215,6 +215,8 @@ case ${1:-} in
                   env:GC_B_ASYNC_BPC=5 "abl:rmat24:3:2:base=-,r1024b5=variants/r1024/libgcolor.so"
                   "abl:rmat26:2:2:base=-,r1024b5=variants/r1024/libgcolor.so" env:GC_B_ASYNC_BPC=
                   "abl:rmat26:2:2:base=-,r1024=variants/r1024/libgcolor.so" env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at" >&2; exit 2 ;;
+  au) exec_steps=(profile:mesh512 profile:uniform10M "profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end"
+                  "profile:rmat26:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at|au" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
