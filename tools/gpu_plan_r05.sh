@@ -217,6 +217,11 @@ case ${1:-} in
                   "abl:rmat26:2:2:base=-,r1024=variants/r1024/libgcolor.so" env:AB_VARIANT=) ;;
   au) exec_steps=(profile:mesh512 profile:uniform10M "profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end"
                   "profile:rmat26:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at|au" >&2; exit 2 ;;
+  # av: 6 workgroups per CU for the fold (variants/w6: amdgpu_waves_per_eu(6), 80 VGPRs with 28 B of
+  #     scratch, resident cap 768; variants/c768: the cap alone) -- for the next round, not the build
+  av) exec_steps=(env:AB_VARIANT=B env:GC_B_ASYNC_BPC=6
+                  "abl:rmat24:3:2:base=-,w6=variants/w6/libgcolor.so,c768=variants/c768/libgcolor.so"
+                  "abl:rmat26:2:2:base=-,w6=variants/w6/libgcolor.so" env:GC_B_ASYNC_BPC= env:AB_VARIANT=) ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at|au|av" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
