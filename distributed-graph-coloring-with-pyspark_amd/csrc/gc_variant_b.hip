@@ -805,8 +805,8 @@ __device__ int b_async_heavy_pass(GDev& g, const BLists& B, int* l2, int n2, int
 // stop check runs only on a pass without progress.  Returns -1 (not eligible: nothing
 // changed), 0 (every item settled) or the items left on a stop, written back in the global
 // form (l1, lcur, pend) for the hand-off.
-#ifndef GC_B_RES_CAP  // 1024: the fold's LDS allows 5 workgroups per CU (1536: 4; R-MAT-24 -1 to -2%, profiles/r05/at)
-#define GC_B_RES_CAP 1024
+#ifndef GC_B_RES_CAP  // 768: the fold's LDS allows 6 workgroups per CU (1536: 4, 1024: 5; profiles/r05/at, av)
+#define GC_B_RES_CAP 768
 #endif
 __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* ev, BAsyncLds& s, int* pe, DevCtl* c,
                                 ull t0, long long budget, bool* stop, ull* npass, ull* scanned) {
@@ -997,7 +997,9 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
 // pass `pass` of the round as one asynchronous launch: reads the three lists of slot
 // pass % 3, spills to slot (pass + 1) % 3, uses the arrays of slot (pass + 2) % 3 as the
 // waves' scratch and clears that slot's counts (as k_b_ev does)
-__global__ void __launch_bounds__(GC_BLOCK) k_b_async(GDev g, BLists B, int* ev, int pass, long long budget) {
+// 6 waves per SIMD (80 VGPRs, 28 B of scratch per lane): R-MAT-26 -2.4 to -4.5% against 5, R-MAT-24 flat (r05/av)
+__global__ void __launch_bounds__(GC_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) k_b_async(GDev g, BLists B, int* ev, int pass,
+                                                                                       long long budget) {
     DevCtl* c = g.ctl;
     if (budget < 0) {  // residency probe (gcl_b_async_resident)
         gc_residency_probe(c);
@@ -1204,7 +1206,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g->device) == hipSuccess && cus > 0 &&
             rate_khz > 0) {
-            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 5;
+            const int bpc = getenv("GC_B_ASYNC_BPC") && atoi(getenv("GC_B_ASYNC_BPC")) > 0 ? atoi(getenv("GC_B_ASYNC_BPC")) : 6;
             // every workgroup resident (gc_resident_blocks_per_cu): the static slices all progress
             b_async_grid = std::min(bpc, std::max(1, gcl_b_async_resident(d, s))) * cus;
             const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;

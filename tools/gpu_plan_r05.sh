@@ -222,6 +222,10 @@ case ${1:-} in
   av) exec_steps=(env:AB_VARIANT=B env:GC_B_ASYNC_BPC=6
                   "abl:rmat24:3:2:base=-,w6=variants/w6/libgcolor.so,c768=variants/c768/libgcolor.so"
                   "abl:rmat26:2:2:base=-,w6=variants/w6/libgcolor.so" env:GC_B_ASYNC_BPC= env:AB_VARIANT=) ;;
-  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at|au|av" >&2; exit 2 ;;
+  aw) exec_steps=(file:tests/test_gpu_variant_b.py "file:tests/test_gpu_fullsize.py:c3 and B"
+                  profile:rmat24 "profile:rmat24:--variant,B" profile:rmat26
+                  profile:mesh512 profile:uniform10M "profile:rmat28:--no-north-star,--no-cpu-baseline,--no-end-to-end"
+                  "profile:rmat26:--variant,B,--no-north-star,--no-cpu-baseline,--no-end-to-end") ;;
+  *) echo "usage: $0 a|b|...|z|aa|ab|ac|fin|ad|ae|af|ag|ah|ai|aj|ak|al|am|an|ao|ap|aq|ar|as|at|au|av|aw" >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r05$1" "${exec_steps[@]}"
