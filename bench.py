@@ -218,6 +218,23 @@ def cpu_baseline(w, host_csr, colors_gpu):
             "colors": int(o["max_color"]) + 1, "seconds": dt, "identical": same}
 
 
+def cpu_baseline_sample(torch):
+    """The N > 1 line's CPU baseline: the N = 1 workload (C3, R-MAT-24) as a bounded sample of
+    the R-MAT family the N > 1 run colours (its R-MAT-28 would take minutes on the host), the GPU
+    colouring of the same sample beside it for the identity check."""
+    from gcolor_amd.engine import DeviceGraph
+    w = WORKLOADS["rmat24"]
+    with DeviceGraph.rmat(w["scale"], w["ef"], seed=w["seed"]) as dg:
+        csr = dg.export()
+        colors = dg.color("A").colors
+    out = cpu_baseline(w, csr, colors)
+    out["identical_to_gpu"] = bool(out.pop("identical"))
+    out.pop("colors")
+    out.pop("seconds")
+    out["sample"] = "bounded sample (the N = 1 workload, same generator): " + out["sample"]
+    return out
+
+
 def python_restatement(scale=14):
     """Context for the CPU baseline: the oracle's pure-Python restatement (oracle.py py_color:
     the reference's per-vertex lambdas as Python loops, one thread, without Spark's overhead)
@@ -402,16 +419,25 @@ def north_star(torch, barrier, args):
            "ms_per_step": t * 1e3, "edges_per_s": m / t, "colors_used": r.num_colors, "rounds": r.rounds,
            "async_jp_aborts": r.async_aborts, "hubs": r.hubs, "hubs_on": r.hubs > 0,
            "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
-           # §8d bytes / t / peak: raw, and with no class credited more than the peak could move
-           # in its (event-timed) time -- propose's §8d credit for hub rows the bitmaps replace
-           # is otherwise above the peak
-           "algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
-           "algorithmic_frac_capped": capped_alg(probe.kernels, S.n, S.nnz) / t / 1e9 / HBM_PEAK_GBS,
+           # §8d bytes / t / peak: a WORK ratio, not bandwidth -- §8d credits every hub proposal
+           # with its whole row, which the pushed bitmaps never read (propose's class is above the
+           # peak); the capped ratio credits no class more than the peak could move in its time
+           "work_ratio": balg / t / 1e9 / HBM_PEAK_GBS,
+           "work_ratio_capped": capped_alg(probe.kernels, S.n, S.nnz) / t / 1e9 / HBM_PEAK_GBS,
            "classes_probe_step": class_table(probe.kernels, pmc_class_bytes("rmat26", "A")[0]),
            # the physical figures: every kernel's bytes of a step (as counted, and calibrated:
            # 2 x FETCH + WRITE) / t / peak, and the dominant class on the calibrated basis
            "pmc_frac": pmc_step_frac("rmat26", "A", t),
            "roofline_calibrated": calibrated_roofline("rmat26", "A", probe.kernels)}
+    # THE north-star figure: the whole step's HBM bytes on the calibrated basis
+    # (2 x FETCH_SIZE + WRITE_SIZE of every kernel of a step, profiles/pmc/rmat26.json "_step",
+    # the gfx950 correction of MI355X_MICROARCH.md) / this run's step time / 8 TB/s; null when
+    # that summary is not of this build.  The as-counted figure stays beside it.
+    pf = out["pmc_frac"]
+    out["roofline_frac"] = pf.get("frac_calibrated") if pf else None
+    out["roofline_frac_as_counted"] = pf.get("frac") if pf else None
+    out["roofline_frac_basis"] = ("(2 x FETCH_SIZE + WRITE_SIZE per step, profiles/pmc/rmat26.json _step) / "
+                                  "ms_per_step / 8 TB/s")
     S.close()
     return out
 
@@ -449,8 +475,9 @@ def class_table(kern, pmc):
         if v["ms"] > 0:
             e["alg_GBps"] = round(v["bytes"] / v["ms"] / 1e6, 1)
             e["alg_frac"] = round(e["alg_GBps"] / HBM_PEAK_GBS, 4)
-            if e["alg_frac"] > 1.0:
-                e["alg_over_peak"] = True  # credited bytes the path does not move (hub bitmaps)
+            if e["alg_frac"] > 1.0:  # credited bytes the path does not move (hub bitmaps): a work
+                e["alg_over_peak"] = True  # ratio, not a bandwidth fraction
+                e["work_ratio"] = e.pop("alg_frac")
         if k in pmc:
             e["pmc_GB"] = round(pmc[k] * v["launches"] / 1e9, 4)
             if v["bytes"] > 0:  # physical / algorithmic: > 1 is traffic the §8d model does not need
@@ -652,6 +679,21 @@ def run_multi(args, world, rank, local_rank, dist, torch):
         assert np.array_equal(one_colours, res.colors), "multi-GPU colouring differs from the one-GPU engine"
         cap = capped_alg(probe.kernels, S.n, S.nnz)
         achieved = cap / world / t / 1e9
+        # traffic: the same graph's one-GPU step's HBM bytes (rocprofv3, calibrated 2 x FETCH +
+        # WRITE, profiles/pmc/<workload>.json of this build) split over the N ranks -- the
+        # ranks' own counters are not collected (rocprofv3 runs one process); null when stale
+        one_pmc = pmc_step_frac(args.workload, "A", t1) if w["desc"] == WORKLOADS[args.workload]["desc"] else None
+        step_bytes = one_pmc and one_pmc.get("bytes_per_step_calibrated")
+        phys = ({"traffic": step_bytes / world, "achieved": step_bytes / world / t / 1e9,
+                 "frac": step_bytes / world / t / 1e9 / HBM_PEAK_GBS, "source": one_pmc["source"],
+                 "basis": "the one-GPU step's calibrated HBM bytes per step / N / t"} if step_bytes else None)
+        cpu = None
+        if not args.no_cpu_baseline:
+            try:  # a bounded sample of the same R-MAT family: C3 (R-MAT-24), ~10 s on 16 threads
+                progress("CPU baseline (bounded sample: R-MAT-24)")
+                cpu = cpu_baseline_sample(torch)
+            except Exception as e:  # noqa: BLE001 -- a failing baseline is reported, not the line lost
+                cpu = {"error": f"{type(e).__name__}: {e}"}
         line = {
             "metric": METRIC, "value": m / t, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": t * 1e3, "higher_is_better": True,
@@ -678,11 +720,15 @@ def run_multi(args, world, rank, local_rank, dist, torch):
                        "single_gpu_ms": round(t1 * 1e3, 2), "speedup_vs_single_gpu": round(t1 / t, 3)},
             "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
             "colors_used": res.max_color + 1,
-            "roofline": {"bound": "hbm", "kernel": "whole colouring per GPU, §8d algorithmic bytes of the one-GPU "
-                                                   "colouring (no class credited above the peak) / N / t",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
-            "cpu_baseline": None,
+            "roofline": {"bound": "hbm", "kernel": "whole step per GPU",
+                         "achieved": phys["achieved"] if phys else achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (phys["achieved"] if phys else achieved) / HBM_PEAK_GBS,
+                         "achieved_basis": (phys["basis"] + f" ({phys['source']})") if phys else
+                         "§8d algorithmic bytes of the one-GPU colouring (no class credited above the peak) / N / t "
+                         "(no rocprofv3 summary of this build)",
+                         "traffic": phys["traffic"] if phys else None,
+                         "algorithmic": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS}},
+            "cpu_baseline": cpu,
         }
     barrier()  # every rank waits for rank 0's one-GPU reference
     S.close()
@@ -752,6 +798,12 @@ def main():
         raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU: the library may park all but 48 GB of HBM between steps (a large
+    # handle's destroy otherwise frees ~40 GB that the next step's hipMalloc waits seconds for,
+    # csrc/gc_alloc.hip).  Not when ranks share one GPU (GC_BENCH_DEVICE rehearsals): the
+    # library's conservative 64 GB default then stays.
+    if "GC_BENCH_DEVICE" not in os.environ:
+        os.environ.setdefault("GC_ALLOC_IDLE_RESERVE_GB", "48")
     import torch
     dist = None
     if world == 1 and args.sharded:  # a one-rank group without a launcher
@@ -836,19 +888,8 @@ def main():
     launches = max(dom["launches"], 1)
     avg_ms = dom["ms"] / launches
     alg_per_launch = dom["bytes"] / launches
-    traffic = pmc.get(dom_class)
+    traffic_counted = pmc.get(dom_class)
     alg_rate = alg_per_launch / (avg_ms / 1e3) / 1e9 if dom["ms"] > 0 else 0.0
-    if alg_per_launch > 0 and dom["ms"] > 0 and alg_rate <= HBM_PEAK_GBS:
-        basis, achieved = "algorithmic (SURVEY.md §8d)", alg_rate
-    elif traffic is not None and dom["ms"] > 0:
-        basis = ("rocprofv3 FETCH_SIZE+WRITE_SIZE (" + ("class has no §8d credit" if alg_per_launch <= 0 else
-                 "§8d credits bytes the kernels do not move: hub rows replaced by pushed bitmaps") + ")")
-        achieved = traffic / (avg_ms / 1e3) / 1e9
-    else:
-        basis = ("unmeasured: " + ("the class has no §8d credit" if alg_per_launch <= 0 else
-                 "§8d credit above the HBM peak (hub bitmaps stand in for rows)") +
-                 " and no rocprofv3 summary of this build (profiles/pmc)")
-        achieved = None
     balg = sum(v["bytes"] for v in kern.values()) + 20.0 * S.n + 8.0 * S.nnz
     cal_roof = None
     pmc_c, _ = pmc_class_bytes(args.workload, V, "hbm_bytes_per_launch_calibrated")
@@ -857,6 +898,28 @@ def main():
         a = pmc_c[dom_class] / (avg_ms / 1e3) / 1e9
         cal_roof = {"achieved": a, "frac": a / HBM_PEAK_GBS, "traffic": pmc_c[dom_class],
                     "gather_ceiling": cal["gather_ceiling_GBps"], "frac_of_gather_ceiling": a / cal["gather_ceiling_GBps"]}
+    # The headline figure: the dominant class's HBM bytes per launch on the
+    # calibrated physical basis -- 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
+    # correction, from a rocprofv3 summary of THIS build -- / its event-timed launch time.  The
+    # as-counted PMC rate and the §8d algorithmic rate stay beside it.
+    as_counted = ({"achieved": traffic_counted / (avg_ms / 1e3) / 1e9,
+                   "frac": traffic_counted / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic_counted}
+                  if traffic_counted is not None and dom["ms"] > 0 else None)
+    algorithmic = ({"achieved": alg_rate, "frac": alg_rate / HBM_PEAK_GBS, "bytes_per_launch": alg_per_launch,
+                    "over_peak": alg_rate > HBM_PEAK_GBS} if alg_per_launch > 0 and dom["ms"] > 0 else None)
+    if cal_roof is not None:
+        basis, achieved, traffic = ("rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch (calibrated, "
+                                    "profiles/calib/gather_bytes.json)"), cal_roof["achieved"], cal_roof["traffic"]
+    elif algorithmic is not None and not algorithmic["over_peak"]:
+        basis, achieved, traffic = "algorithmic (SURVEY.md §8d): no rocprofv3 summary of this build", alg_rate, None
+    elif as_counted is not None:
+        basis, achieved, traffic = "rocprofv3 FETCH_SIZE+WRITE_SIZE as counted (no calibration file)", \
+            as_counted["achieved"], traffic_counted
+    else:
+        basis = ("unmeasured: " + ("the class has no §8d credit" if alg_per_launch <= 0 else
+                 "§8d credit above the HBM peak (hub bitmaps stand in for rows)") +
+                 " and no rocprofv3 summary of this build (profiles/pmc)")
+        achieved, traffic = None, None
 
     if rank != 0:
         if dist is not None:
@@ -948,7 +1011,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom_class, "kernels": CLASS_KERNELS.get(dom_class),
                      "achieved": achieved, "achieved_basis": basis, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                     "traffic_source": pmc_src and f"{pmc_src} (bytes per launch, FETCH_SIZE+WRITE_SIZE)",
+                     "traffic_source": pmc_src and f"{pmc_src} (HBM bytes per launch, 2 x FETCH_SIZE + WRITE_SIZE)",
+                     "as_counted": as_counted, "algorithmic": algorithmic,
                      "algorithmic_bytes_per_launch": alg_per_launch, "avg_launch_ms": avg_ms,
                      "launches_per_step": dom["launches"],
                      "share_of_step": dom["ms"] / (t_ev * 1e3) if t_ev else None,
@@ -961,9 +1025,9 @@ def main():
         # whole job, §8d algorithmic bytes / t: a work-efficiency ratio against the peak, NOT
         # bandwidth (hub bitmaps skip row reads §8d credits); the capped figure credits no class
         # more bytes than the peak could move in its time
-        "whole_job_algorithmic_frac": balg / t / 1e9 / HBM_PEAK_GBS,
-        "whole_job_algorithmic_frac_capped": capped_alg(probe.kernels, info["n"], info["nnz"]) / t / 1e9
-                                              / HBM_PEAK_GBS,
+        "whole_job_work_ratio": balg / t / 1e9 / HBM_PEAK_GBS,
+        "whole_job_work_ratio_capped": capped_alg(probe.kernels, info["n"], info["nnz"]) / t / 1e9
+                                        / HBM_PEAK_GBS,
         "whole_job_pmc_frac": pmc_step_frac(args.workload, V, t),
         "north_star": ns,
         "cpu_baseline": cpu,

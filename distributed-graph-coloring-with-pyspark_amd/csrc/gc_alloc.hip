@@ -118,24 +118,35 @@ hipError_t alloc(void** p, size_t bytes, bool host) {
 hipError_t gc_dmalloc(void** p, size_t bytes) { return alloc(p, bytes, false); }
 hipError_t gc_hmalloc(void** p, size_t bytes) { return alloc(p, bytes, true); }
 
-// Parked bytes beyond this are freed at once: the device's memory less 48 GB (at least 64 GB;
-// GC_ALLOC_IDLE_CAP_GB sets it).  A parked block is only idle memory of this process: an
-// allocation of ours that fails gives the whole cache back and retries.  Round 4's fixed 64 GB
-// was below one R-MAT-28 handle's buffers (~110 GB: the partitioned CSR, the hub transpose and
-// its hlow copies, the work lists), so every step's destroy freed ~40 GB with hipFree -- which
-// returns at once -- and the next large hipMalloc waited ~3 s for that memory (GC_ALLOC_TRACE=1,
-// profiles/r05/a: "malloc 1024 MB 3123 ms"): R-MAT-28's bench step 2.93 s against 1.77 s
-// without it.  Half of the memory (round 5's first cap) fixed the one-GPU step but not the
-// multi-GPU one, whose shard state adds its in-rows and replicas (~1.75 s stalls a step,
-// profiles/r05/w).
+// Parked bytes beyond this are freed at once.  The library's default is 64 GB: parked blocks
+// are idle memory of this process only (an allocation of ours that fails gives the whole cache
+// back and retries, but torch in the same process or other processes sharing the GPU cannot
+// reach them), so the default stays conservative.  Two settings raise it:
+//   GC_ALLOC_IDLE_CAP_GB=G       a cap of G GB;
+//   GC_ALLOC_IDLE_RESERVE_GB=R   the device's memory less R GB (at least 64 GB) -- bench.py's
+//                                one-process-per-GPU runs set R = 48.
+// Why bench.py opts in: a fixed 64 GB was below one R-MAT-28 handle's buffers (~110 GB: the
+// partitioned CSR, the hub transpose and its hlow copies, the work lists), so every step's
+// destroy freed ~40 GB with hipFree -- which returns at once -- and the next large hipMalloc
+// waited ~3 s for that memory (GC_ALLOC_TRACE=1, profiles/r05/a: "malloc 1024 MB 3123 ms"):
+// R-MAT-28's bench step 2.93 s against 1.77 s without it.  Half of the memory fixed the
+// one-GPU step but not the multi-GPU one, whose shard state adds its in-rows and replicas
+// (~1.75 s stalls a step, profiles/r05/w).
 static size_t idle_cap() {
     static size_t cap = 0;
     if (!cap) {
         size_t freeb = 0, total = 0;
-        const size_t floor = (size_t)64 << 30, reserve = (size_t)48 << 30;
+        const size_t floor = (size_t)64 << 30;
         const char* env = getenv("GC_ALLOC_IDLE_CAP_GB");
-        if (env && atoll(env) > 0) cap = (size_t)atoll(env) << 30;
-        else cap = (hipMemGetInfo(&freeb, &total) == hipSuccess && total > floor + reserve) ? total - reserve : floor;
+        const char* res = getenv("GC_ALLOC_IDLE_RESERVE_GB");
+        if (env && atoll(env) > 0) {
+            cap = (size_t)atoll(env) << 30;
+        } else if (res && atoll(res) >= 0) {
+            const size_t reserve = (size_t)atoll(res) << 30;
+            cap = (hipMemGetInfo(&freeb, &total) == hipSuccess && total > floor + reserve) ? total - reserve : floor;
+        } else {
+            cap = floor;
+        }
     }
     return cap;
 }

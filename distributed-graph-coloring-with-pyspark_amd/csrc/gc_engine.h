@@ -65,6 +65,11 @@ struct gc_graph {
     int* hkcnt = nullptr;         // hub x: kept-row entries written by the long-row first pass this round
     long long nhch = 0;           // static chunks
     unsigned* hk = nullptr;       // hub-indexed mirror of (candidate, JP state) (gc_hk; GC_HK_COLOURED)
+    int* hcore = nullptr;         // hub core (gc_core.hip): hub -> core index, core index -> hub,
+    int* core_hub = nullptr;      //   the core's bitsets and the build's per-workgroup counts
+    unsigned* core_bits = nullptr;
+    ull* core_wcnt = nullptr;
+    int core_cap = 0;             //   the capacity they were allocated for
     unsigned* fsum = nullptr;  // per-workgroup counts of the frontier re-sort
     RoundRec* rec = nullptr;   // device round records
     long long rcap = 0;
@@ -186,6 +191,7 @@ int gc_build_in_csr_sym(gc_graph* g, long long lo, long long hi);  // the same, 
 int gc_filter_rows_sym(gc_graph* g, gc_graph* v, long long lo, long long hi);  // the same over g's tiling (gc_prep.hip)
 int gc_alloc_run_state(gc_graph* g);     // gc_engine.hip
 int gc_hubs_prepare(gc_graph* g, GDev& d);
+int gc_core_prepare(gc_graph* g, GDev& d);  // gc_core.hip: the hub core's buffers (once per graph); d.core_cap
 int gc_alloc_heavy_pending(gc_graph* g);  // gc_engine.hip: the hubs-off heavy JP's pending lists, on first use  // gc_hubs.hip: build (once) + reset; fills d's hub fields
 void gc_hubs_free(gc_graph* g);
 int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, int32_t* cround_out,

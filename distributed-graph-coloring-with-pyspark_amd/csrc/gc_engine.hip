@@ -128,6 +128,12 @@ GDev gc_view(const gc_graph* g) {
     d.nhch = 0;
     d.hch_mul = 1;
     d.hprep = 0;
+    d.hcore = d.core_hub = nullptr;
+    d.core_bits = nullptr;
+    d.core_wcnt = nullptr;
+    d.core_cap = 0;
+    d.nhub_core = 0;
+    d.core_iters = 0;
     d.hub_scan = 0;
     d.hk = nullptr;
     d.hid = nullptr;
@@ -299,6 +305,35 @@ struct Run {
         const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
         async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
         async_grid = cus * bpc;
+        // the hub core (gc_core.hip): its buffers once per graph; GC_HUB_CORE=0 off
+        if (!d.hub_repl && gc_core_prepare(g, d) == GC_OK) core_on = d.core_cap > 0;
+    }
+    // The hub core: a build is attempted (gcl_core_build, before the next batch) once a
+    // snapshot's next frontier is at most twice the core's capacity and 20% below the last
+    // attempt's; k_hub_core runs ahead of every k_sweep_async once a snapshot shows it READY.
+    bool core_on = false, core_ready = false, core_pending = false;
+    long long core_try_f = -1;  // frontier at the last build attempt (-1: none yet)
+    // k_hub_core only while the last snapshot's frontier is at least GC_HUB_CORE_MINF (1024): below
+    // it a round has ~100 hub proposers, ~2 JP passes, and k_sweep_async alone is as fast
+    long long core_f = 0;
+    const long long core_min_f = getenv("GC_HUB_CORE_MINF") ? atoll(getenv("GC_HUB_CORE_MINF")) : 1024;
+    const bool core_debug = getenv("GC_CORE_DEBUG") != nullptr;
+    void core_check(const DevCtl& x) {
+        core_f = (long long)x.fcnt[x.cur];
+        if (!core_on || core_ready) return;
+        if (x.core_state == GC_CORE_READY) {
+            core_ready = true;
+            if (core_debug) fprintf(stderr, "[gc core] ready at round %lld: %d hubs\n", x.round, x.core_n);
+            return;
+        }
+        const long long f = (long long)x.fcnt[x.cur];
+        if (f > 0 && f <= 2ll * d.core_cap && (core_try_f < 0 || f * 5 <= core_try_f * 4)) {
+            if (core_debug)
+                fprintf(stderr, "[gc core] build attempt before round %lld (frontier %lld; last attempt: state %d, %llu "
+                                "uncoloured hubs)\n", x.round, f, x.core_state, x.core_cnt);
+            core_pending = true;
+            core_try_f = f;
+        }
     }
     void init_loop() {
         const char* e = getenv("GC_SWEEP_LOOP");
@@ -387,6 +422,7 @@ struct Run {
         const bool tail = mode == GC_CM_ROUND && (nsweeps > 0 || !skip_tail);
         if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
             kt.begin(GC_K_SWEEP);
+            if (core_ready && core_f >= core_min_f) gcl_hub_core(d, L, nsweeps, async_par, s);  // decides the hubs when it can
             gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
             async_par ^= 1;
             kt.end();
@@ -479,6 +515,12 @@ struct Run {
     // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
     const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
     int enqueue_batch(int B, int S, int slot) {
+        if (core_pending) {  // between rounds: the colours it reads are a round start
+            kt.begin(GC_K_OTHER);
+            gcl_core_build(d, s);
+            kt.end();
+            core_pending = false;
+        }
         for (int b = 0; b < B; ++b) {
             if (b == B - 1 && !snap_copy) snap_ptr = g->hsnap_dev + slot;
             enqueue_round(S);
@@ -554,6 +596,7 @@ struct Run {
         h.fail_round = -1;
         h.want_cround = cround_out != nullptr;
         h.pull_off = getenv("GC_NO_PULL") ? 1 : 0;
+        h.core_round = -1;
         if (rs) {
             h.round = rs->round0;
             h.rbase = rs->round0;
@@ -595,6 +638,7 @@ struct Run {
                 if (sn.round > max_rounds) { gc_set_error("round limit exceeded"); return GC_EROUNDS; }
                 resort_hint = (long long)sn.fcnt[sn.cur] * 256 >= g->n;
                 maxc_hint = sn.maxcolor;
+                core_check(sn);
                 S = pick_sweeps(sn);
                 c4_hint = pick_c4(sn, g->n);
                 batch = pick_batch(sn, g->n, batch);
@@ -619,6 +663,7 @@ struct Run {
             proposed = h.proposed != 0;
             resort_hint = (long long)h.fcnt[h.cur] * 256 >= g->n;
             maxc_hint = h.maxcolor;
+            core_check(h);
             S = pick_sweeps(h);
             c4_hint = pick_c4(h, g->n);
             batch = pick_batch(h, g->n, 1);
@@ -662,6 +707,12 @@ struct Run {
         if (cround_out) GC_HIP(hipMemcpyAsync(cround_out, g->cround, sizeof(int) * g->n, hipMemcpyDeviceToHost, s));
         if ((rc = sync_ctl())) return rc;
         if ((rc = drain_records())) return rc;
+        if (core_debug)
+            fprintf(stderr, "[gc core] %lld of %zu rounds decided by the core: %lld iterations (max %lld)\n",
+                    h.core_handled, recs.size(), h.core_iters_sum, h.core_iters_max);
+#ifdef GC_A_PROF
+        gcl_aprof_dump(recs.data(), recs.size());
+#endif
         GC_HIP(hipGetLastError());
         const int status = h.halt == GC_H_FAILED ? GC_FAILED : (h.halt == GC_H_STALLED ? GC_STALLED : GC_OK);
         if (st) {
@@ -673,6 +724,7 @@ struct Run {
             st->jp_sweeps = h.sweep_total;
             st->async_aborts = (int64_t)h.async_aborts;
             st->hubs = d.hbits_w ? (int64_t)g->nhub : 0;
+            st->core_rounds = (int64_t)h.core_handled;
             st->fail_round = h.halt == GC_H_FAILED ? h.fail_round : -1;
             st->fail_count = h.halt == GC_H_FAILED ? h.fail_count : 0;
             for (const RoundRec& r : recs) st->reseeds += r.seeds;

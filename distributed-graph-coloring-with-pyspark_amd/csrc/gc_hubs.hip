@@ -390,7 +390,7 @@ int build(gc_graph* g, int T, int W) {
 void gc_hubs_free(gc_graph* g) {
     void* ptrs[] = {g->hubpre, g->hperm, g->hid, g->hub_v, g->hin_rp, g->hin_col, g->hbits, g->hkill, g->hlow_rp, g->hlow_col,
                     g->hcur, g->hpc, g->hpend[0], g->hpend[1], g->hlow2[0], g->hlow2[1], g->hrow, g->hlen,
-                    g->hch_rp, g->hch_own, g->hkcnt, g->hk};
+                    g->hch_rp, g->hch_own, g->hkcnt, g->hk, g->hcore, g->core_hub, g->core_bits, g->core_wcnt};
     for (void* p : ptrs)
         if (p) gc_dfree(p);
     gc_hub_bits_free(g);
@@ -401,6 +401,10 @@ void gc_hubs_free(gc_graph* g) {
     g->hin_rp = g->hlow_rp = g->hch_rp = nullptr;
     g->hch_own = g->hkcnt = nullptr;
     g->hk = nullptr;
+    g->hcore = g->core_hub = nullptr;
+    g->core_bits = nullptr;
+    g->core_wcnt = nullptr;
+    g->core_cap = 0;
     g->nhch = 0;
     g->hbits = g->hkill = nullptr;
     g->nhub = 0;

@@ -174,7 +174,19 @@ struct DevCtl {
     long long dbg[4];       // GC_CHECKS builds: the first out-of-range value a checked kernel met (code, a, b, c)
     ull sumdeg[8];     // per kernel class: sum of degrees touched (algorithmic bytes)
     ull nvert[8];      // per kernel class: vertices processed
+    // the hub core (gc_core.hip): the uncoloured hubs' adjacency as bitsets, built once a round's
+    // uncoloured hubs fit; k_hub_core then decides a round's hubs in one workgroup
+    long long core_round;   // the round whose hubs k_hub_core decided (k_sweep_async returns at once); -1 none
+    ull core_cnt;           // build: uncoloured hubs counted
+    int core_state;         // GC_CORE_NONE / _FAILED (more uncoloured hubs than the cap) / _READY
+    int core_n;             // hubs in the core (core index = rank order among them)
+    long long core_handled; // rounds decided by k_hub_core (stats)
+    long long core_iters_sum;  // their iterations (the chain: the most winners of one class), summed
+    long long core_iters_max;  //   and the largest
 };
+#define GC_CORE_NONE 0
+#define GC_CORE_FAILED 2
+#define GC_CORE_READY 4
 
 __device__ __forceinline__ int gc_lane() { return (int)__lane_id(); }
 __device__ __forceinline__ ull gc_lanemask_lt() { return (1ull << gc_lane()) - 1ull; }

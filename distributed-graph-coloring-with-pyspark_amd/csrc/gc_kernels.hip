@@ -1483,6 +1483,15 @@ __device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull
     return nw;
 }
 
+#ifdef GC_A_PROF
+// (diagnostic build, -DGC_A_PROF: per round, where k_sweep_async's time goes -- the light
+// phase, the wait for the last light, the hub phase -- and the passes each took; dumped by
+// the engine at the end of the colouring, GC_A_PROF_OUT=path)
+#define GC_A_PROF_ROUNDS 4096
+#define GC_A_PROF_K 16
+__device__ ull gc_aprof[GC_A_PROF_ROUNDS][GC_A_PROF_K];
+#endif
+
 // One pass of a wave over its pending hubs hl[0, nh), GC_HUB_NG at a time (a 16-lane
 // group each): the resumable scan of gc_hub_scan_groups, with agent-scope loads of the
 // hub mirror and the kill flags and agent-scope stores of the decisions.  Pending hubs
@@ -1546,6 +1555,17 @@ __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
         unsigned f = kill ? 1u : 0u;
         if (act) f = out ? 1u : (block >= 0 ? 2u : 0u);
         const bool lead = li == 0 && x >= 0;
+#ifdef GC_A_PROF
+        if (lead && act && g.ctl->round < GC_A_PROF_ROUNDS) {
+            ull* r = gc_aprof[g.ctl->round];
+            const int p0 = first ? hstart : cursor;
+            const ull sc = (ull)(std::min(pos, full) - p0);
+            atomicAdd(r + 12, sc);
+            atomicMax(r + 13, sc);
+            if (f == 0u) atomicAdd(r + 14, 1ull);
+            if (first) atomicAdd(r + 15, (ull)(full - hstart));
+        }
+#endif
         if (lead && act) {
             if (first) {
                 g.hcur[x] = 1;
@@ -1588,6 +1608,7 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
     for (int i = gc_lane(); i < cnt; i += GC_WAVE) out[base + i] = src[i];
 }
 
+
 // The launch after sweep S (k_resolve = 0, or the last host sweep): reads slot S % 3,
 // spills to slot (S + 1) % 3 (cleared by sweep S), clears slot (S + 2) % 3 and sets
 // tail_last = S + 1, the slot the commit checks -- exactly what a tail that ran one more
@@ -1602,6 +1623,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         return;
     }
     if (c->halt) return;
+    if (c->core_round == c->round) return;  // k_hub_core decided this round's hubs (gc_core.hip)
     __shared__ GcAsyncLds s_w[GC_WAVES_PER_BLOCK];
     const int w = threadIdx.x / GC_WAVE;
     const long long j = S;
@@ -1633,10 +1655,20 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
     const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
     bool stop = false;
+#ifdef GC_A_PROF
+    ull* aprof = (gc_lane() == 0 && c->round < GC_A_PROF_ROUNDS) ? gc_aprof[c->round] : nullptr;
+    if (aprof && wid == 0) {
+        aprof[5] = (ull)cl;
+        aprof[6] = (ull)ch;
+    }
+#endif
     // lights: the wave's static slice of the list, compacted in place pass after pass
     {
         const long long la = cl * wid / W, lb = cl * (wid + 1) / W;
         int np = (int)(lb - la);
+#ifdef GC_A_PROF
+        if (aprof && np > 0) atomicMax(aprof + 9, (ull)np);
+#endif
         int* lst = L.undL[in] + la;
         ull decided = 0;
         int idle = 0, lpass = 0;
@@ -1652,6 +1684,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
             }
         }
         if (stop) gc_async_spill(lst, np, L.undL[out], &c->und_cnt[out]);
+#ifdef GC_A_PROF
+        if (aprof && lpass > 0) {
+            atomicMax(aprof + 0, wall_clock64() - t0);
+            atomicMax(aprof + 3, (ull)lpass);
+            atomicAdd(aprof + 7, (ull)lpass);
+            atomicAdd(aprof + 8, 1ull);
+        }
+#endif
         if (decided) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its state and kill-flag stores have landed
             if (gc_lane() == 0) {
@@ -1683,6 +1723,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         }
         stop = __shfl(st, 0, GC_WAVE) != 0;
     }
+#ifdef GC_A_PROF
+    if (aprof) atomicMax(aprof + 1, wall_clock64() - t0);
+#endif
     if (stop) {
         // hubs unevaluated: always listed.  The lights may still converge after this wave
         // gave up (the last light wave publishing late), and then hub_start = S + 1 and every
@@ -1695,8 +1738,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     for (int i = gc_lane(); i < nh0; i += GC_WAVE) hl[i] = src[i];
     gc_wave_sync();
     int nh = nh0, idle = 0;
+#ifdef GC_A_PROF
+    ull hpass = 0;
+#endif
     while (nh > 0) {
         const int before = nh;
+#ifdef GC_A_PROF
+        ++hpass;
+#endif
         nh = gc_async_hub_pass(g, hl, nh);
         if (nh == 0) break;
         if ((stop = gc_async_stop(c, par, t0, budget))) break;
@@ -1707,6 +1756,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         }
     }
     if (stop) gc_async_spill(hl, nh, L.undH[out], &c->undh_cnt[out]);
+#ifdef GC_A_PROF
+    if (aprof) {
+        atomicMax(aprof + 2, wall_clock64() - t0);
+        atomicMax(aprof + 4, hpass);
+        atomicAdd(aprof + 10, hpass);
+        atomicMax(aprof + 11, (ull)nh0);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -3146,6 +3203,30 @@ __global__ void __launch_bounds__(GC_BLOCK) k_hub_push_big(GDev g, const int* bi
         }
         __syncthreads();
     }
+}
+#endif
+#ifdef GC_A_PROF
+// append this colouring's per-round k_sweep_async records (GC_A_PROF_OUT) and clear them
+void gcl_aprof_dump(const RoundRec* recs, size_t nrec) {
+    const char* pp = getenv("GC_A_PROF_OUT");
+    if (!pp) return;
+    static ull hb[GC_A_PROF_ROUNDS][GC_A_PROF_K];
+    if (hipMemcpyFromSymbol(hb, HIP_SYMBOL(gc_aprof), sizeof(hb)) != hipSuccess) return;
+    if (FILE* f = fopen(pp, "a")) {
+        fprintf(f, "# colouring: %zu rounds; per round: r U F light_end_us light_wait_end_us hub_end_us max_lpass max_hpass "
+                   "lights hubs sum_lpass light_waves max_wave_lights sum_hpass max_wave_hubs hub_scanned max_hub_scan hubs_in "
+                   "hub_remaining\n", nrec);
+        for (size_t i = 0; i < nrec && i < GC_A_PROF_ROUNDS; ++i) {
+            const ull* r = hb[i];
+            fprintf(f, "%zu %lld %lld %.2f %.2f %.2f %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", i,
+                    recs[i].U, recs[i].F, r[0] / 100.0, r[1] / 100.0, r[2] / 100.0, r[3], r[4], r[5], r[6], r[7], r[8], r[9],
+                    r[10], r[11], r[12], r[13], r[14], r[15]);
+        }
+        gcl_cprof_dump(f, nrec);
+        fclose(f);
+    }
+    static ull z[GC_A_PROF_ROUNDS][GC_A_PROF_K];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gc_aprof), z, sizeof(z));
 }
 #endif
 void gcl_hub_push_big(const GDev& g, const int* big, const ull* cnt, hipStream_t s) {

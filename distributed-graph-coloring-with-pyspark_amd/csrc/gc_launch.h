@@ -92,6 +92,13 @@ struct GDev {
     int* hlowb[3];            // hlow_col and two working copies (hlow's offsets)
     int* hpc;                 //   undecided same-candidate entries kept in hpend (count << 1 | half)
     int* hpend[2];            //   ping-pong halves, hlow's offsets
+    int* hcore;               // hub core (gc_core.hip): hub x -> core index (-1: coloured when the core was built)
+    int* core_hub;            //   core index -> hub index
+    unsigned* core_bits;      //   core index i -> bitset over core indices: the higher-rank core hubs listing hub i
+    ull* core_wcnt;           //   build scratch: uncoloured hubs per workgroup range
+    int core_cap;             //   core hubs at most (GC_CORE_MAX, GC_HUB_CORE_CAP lowers it); 0 = no core
+    long long nhub_core;      //   hubs of the graph (the build's range)
+    int core_iters;           //   winners one class may need in k_hub_core (GC_HUB_CORE_ITERS)
 };
 
 // Work lists of the round pipeline (counts live in DevCtl).
@@ -167,6 +174,14 @@ void gcl_shard_hub_claim(const GDev& g, const GLists& L, int slot_next, hipStrea
 // replicated hubs after a slice seam: the other ranks' light winners flag their hubs
 void gcl_shard_hub_flags(const GDev& g, long long lo, long long hi, hipStream_t s);
 void gcl_finalize(const GDev& g, int grid, hipStream_t s);
+// hub core (gc_core.hip): build attempt (indices + bitsets; does nothing past core_cap uncoloured
+// hubs) and the per-round decision of the hubs (before gcl_sweep_async, same S and parity)
+void gcl_core_build(const GDev& g, hipStream_t s);
+void gcl_hub_core(const GDev& g, const GLists& L, int S, int par, hipStream_t s);
+#ifdef GC_A_PROF
+void gcl_aprof_dump(const RoundRec* recs, size_t nrec);
+void gcl_cprof_dump(FILE* f, size_t nrec);  // gc_core.hip
+#endif
 void gcl_snap(DevCtl* ctl, DevCtl* snap, hipStream_t s);
 // gc_color_resume: the round-start state from colours + frontier (big: scratch list + its count)
 void gcl_resume(const GDev& g, const GLists& L, const int* colors, const int* cround, const int* front, long long nf,

@@ -65,7 +65,7 @@ class GcStats(ctypes.Structure):
                 ("k_bytes", ctypes.c_double * GC_NKERNELS),
                 ("round_cap", ctypes.c_int64), ("round_U", _I64P), ("round_F", _I64P),
                 ("round_maxmex", _I64P), ("round_accepted", _I64P), ("round_seeds", _I64P),
-                ("async_aborts", ctypes.c_int64), ("hubs", ctypes.c_int64)]
+                ("async_aborts", ctypes.c_int64), ("hubs", ctypes.c_int64), ("core_rounds", ctypes.c_int64)]
 
 
 class GcolorError(RuntimeError):

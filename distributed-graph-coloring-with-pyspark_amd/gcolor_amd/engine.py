@@ -53,6 +53,7 @@ class ColorResult:
     kernels: dict = field(default_factory=dict)
     async_aborts: int = 0  # asynchronous JP launches that handed their rest to host sweeps (0 expected)
     hubs: int = 0  # vertices with pushed hub state (0: no hub, or the hub index did not fit)
+    core_rounds: int = 0  # rounds whose hub JP the hub core decided in one workgroup (csrc/gc_core.hip)
 
     @property
     def ok(self):
@@ -252,7 +253,8 @@ class DeviceGraph:
                            round_seeds=rb["seeds"][:r].copy() if want_rounds else None,
                            fail_round=st.fail_round, fail_count=st.fail_count, reseeds=st.reseeds,
                            max_color=st.max_color, jp_sweeps=st.jp_sweeps, device_ms=st.device_ms,
-                           kernels=kernels, async_aborts=int(st.async_aborts), hubs=int(st.hubs))
+                           kernels=kernels, async_aborts=int(st.async_aborts), hubs=int(st.hubs),
+                           core_rounds=int(st.core_rounds))
 
     def validate(self, colors=None, lo=None, hi=None):
         """validate_graph_coloring counts on the device (coloring.py:149-162): (#uncoloured,
@@ -274,8 +276,9 @@ class DeviceGraph:
 
 def release_cache():
     """Give the library's parked device blocks back to the runtime (gc_release_cache).  The
-    allocator keeps freed blocks for the next graph of the same size (up to half the device's
-    memory); call this before handing a large share of HBM to another allocator (torch)."""
+    allocator keeps freed blocks for the next graph of the same size (up to 64 GB by default;
+    GC_ALLOC_IDLE_CAP_GB / GC_ALLOC_IDLE_RESERVE_GB raise it, csrc/gc_alloc.hip); call this
+    before handing a large share of HBM to another allocator (torch)."""
     nat.check("gc_release_cache", nat.load().gc_release_cache())
 
 

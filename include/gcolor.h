@@ -140,6 +140,9 @@ typedef struct gc_stats {
     int64_t hubs;          /* vertices with pushed hub state (forbidden-colour bitmaps) in
                               this colouring; 0 when none is above the hub threshold or the
                               hub index did not fit (then gc_color printed a warning)      */
+    int64_t core_rounds;   /* rounds whose hub JP the hub core decided in one workgroup
+                              (k_hub_core, csrc/gc_core.hip); the rest went through the
+                              asynchronous JP (diagnostic)                                 */
 } gc_stats;
 
 /* Colour the graph.  colors_out (host int32[n], may be NULL): final state, -1 =
@@ -175,8 +178,12 @@ int gc_validate(gc_graph* g, const int32_t* colors, int64_t* uncolored, int64_t*
    range and every conflicting listed pair (v, u) with v in the range.  Disjoint ranges that
    cover [0, n) add up to gc_validate's counts, so ranks that each hold the colouring split
    validate_graph_coloring (coloring.py:149-162) by vertex range and sum the two counts (the
-   multi-GPU bench step: one all-reduce).  On a graph created GC_GRAPH_SYMMETRIC the pair
-   (v, u) is counted from the row of its lower-rank end (twice), as gc_validate does.        */
+   multi-GPU bench step: one all-reduce).  On a graph created GC_GRAPH_SYMMETRIC (and
+   GC_VALIDATE_HALF on, the default) a conflicting pair is counted twice from the row of its
+   HIGHER-rank end -- the row whose lower-rank part lists the other end -- as gc_validate does,
+   so the count of one range is not the conflicts of its own rows: only the sum over disjoint
+   ranges covering [0, n) is meaningful.  GC_VALIDATE_HALF=0 counts every listed entry of the
+   range's rows (then a range's count is its rows' own).                                      */
 int gc_validate_range(gc_graph* g, const int32_t* colors, int64_t lo, int64_t hi, int64_t* uncolored,
                       int64_t* conflicts);
 

@@ -20,7 +20,8 @@ for p in (REPO, PKG_DIR):
     if p not in sys.path:
         sys.path.insert(0, p)
 # the tests share the device with torch's own allocations (resident CSRs, shard buffers): the
-# library parks at most half of it between calls (the bench's default is all but 48 GB)
+# library parks at most 144 GB between calls (half of an MI355X's HBM; the library's default is
+# 64 GB, bench.py's one-process-per-GPU runs all but 48 GB)
 os.environ.setdefault("GC_ALLOC_IDLE_CAP_GB", "144")
 
 
@@ -71,7 +72,7 @@ def fixture_csr(rec):
 @pytest.fixture(autouse=True, scope="module")
 def _release_device_cache():
     """After each test module, the library's parked device blocks go back to the runtime (the
-    allocator keeps up to half of HBM for the next graph of the same size; the next module may
+    allocator keeps up to GC_ALLOC_IDLE_CAP_GB for the next graph of the same size; the next module may
     need that memory for torch tensors).  Only if the module loaded the library."""
     yield
     mod = sys.modules.get("gcolor_amd._native")

@@ -53,17 +53,28 @@ SETTINGS = [
     {"GC_HUB_T": "512", "GC_INLINE_PB": "0"},
     {"GC_HUB_T": "1024", "GC_ASYNC": "0"},                    # k_propose<1> with the full-grid sweeps
     {"GC_HUB_T": "2", "GC_HUB_W": "2"},                       # a 64-colour bitmap: inline only while colours are few
+    {"GC_HUB_T": "0", "GC_HUB_CORE": "1"},                    # the hub core (opt-in) from frontiers of 1024
+    {"GC_HUB_T": "512", "GC_HUB_CORE": "1"},
+    {"GC_HUB_T": "0", "GC_HUB_CORE": "1", "GC_HUB_CORE_CAP": "16", "GC_HUB_CORE_MINF": "0"},  # a 16-hub core
+    {"GC_HUB_T": "2", "GC_HUB_CORE": "1", "GC_HUB_CORE_CAP": "1", "GC_HUB_CORE_MINF": "0"},
+    {"GC_HUB_T": "0", "GC_HUB_CORE": "1", "GC_HUB_CORE_MINF": "0"},  # the core in every round it can take
+    {"GC_HUB_T": "64", "GC_HUB_CORE": "1", "GC_HUB_CORE_MINF": "0"},
+    {"GC_HUB_T": "0", "GC_HUB_CORE": "1", "GC_HUB_CORE_ITERS": "1", "GC_HUB_CORE_MINF": "0"},  # 2nd window: async
+    {"GC_HUB_T": "3", "GC_HUB_CORE": "1", "GC_HUB_CORE_ITERS": "1", "GC_HUB_CORE_MINF": "0",
+     "GC_ASYNC_BUDGET_US": "0"},                              # ... which gives up to host sweeps
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
        "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
        "T2loop", "offloop8", "T0async_abort", "T2async_abort", "offasync_abort", "T3async_bpc1",
-       "T0sync", "offsync", "T0noinl", "T512noinl", "T1024sync", "T2w2"]
+       "T0sync", "offsync", "T0noinl", "T512noinl", "T1024sync", "T2w2", "T0core", "T512core", "T0core16",
+       "T2core1", "T0coreall", "T64coreall", "T0coreit1", "T3coreit1_abort"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
     for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP",
-              "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC", "GC_INLINE_PB"):
+              "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC", "GC_INLINE_PB", "GC_HUB_CORE",
+              "GC_HUB_CORE_CAP", "GC_HUB_CORE_ITERS", "GC_HUB_CORE_MINF"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)

@@ -160,18 +160,24 @@ FOLD_SETTINGS = [
     {"GC_B_ASYNC": "1", "GC_B_WATCH": "0"},                               # admission cursors off: full rescans
     {"GC_B_ASYNC": "1", "GC_B_WATCH": "64", "GC_B_AWIN": "1"},            # one entry per window, rare rescans
     {"GC_B_ASYNC": "1", "GC_B_ASYNC_K": "1", "GC_B_WATCH": "2", "GC_B_AWIN": "3"},
+    {"GC_B_ASYNC": "1", "GC_B_RESIDENT": "0"},                            # the fold's non-resident form only
+    {"GC_B_ASYNC": "1", "GC_B_REFSKIP": "0"},                             # refused admissions read on
+    {"GC_B_ASYNC": "1", "GC_B_RESIDENT": "0", "GC_B_REFSKIP": "0"},
+    {"GC_B_ASYNC": "1", "GC_B_RESIDENT": "1", "GC_ASYNC_BUDGET_US": "0"},  # resident form's stop-and-write-back
 ]
 
 
 @pytest.mark.parametrize("env", FOLD_SETTINGS, ids=["grid", "default", "async", "async_k1", "async_k3", "async_abort",
                                                     "async_bpc1", "nopipe", "nopipe_grid", "nopipe_abort",
-                                                    "cursor_off", "cursor_w1", "cursor_k1_w3"])
+                                                    "cursor_off", "cursor_w1", "cursor_k1_w3", "resident_off",
+                                                    "refskip_off", "resident_refskip_off", "resident_abort"])
 def test_variant_b_fold(monkeypatch, env):
     """The fold's passes on the full grid, the asynchronous fold where there are hubs (the
     default), on every graph after 0, 1 or 3 full passes, and forced to hand back at once --
     pipelined rounds (the default: the commit decides done / failed / unfinished) and one
     host wait per round (GC_B_PIPE=0) -- every run equal to the oracle."""
-    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC", "GC_B_PIPE", "GC_B_WATCH", "GC_B_AWIN"):
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_ASYNC_BPC", "GC_B_PIPE", "GC_B_WATCH", "GC_B_AWIN",
+              "GC_B_RESIDENT", "GC_B_REFSKIP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -259,7 +265,7 @@ def test_rmat20_variant_b_against_oracle(monkeypatch, env):
     """R-MAT-20 (10^6 vertices, hubs of 10^4 entries, ~200 rounds): variant B's fold at a size
     where the asynchronous fold spreads every round over thousands of waves, and the full-grid
     passes -- every colour and per-round record equal to the C oracle's (variant 1)."""
-    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_B_ASYNC_BPC"):
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_B_ASYNC_BPC", "GC_B_RESIDENT", "GC_B_REFSKIP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)

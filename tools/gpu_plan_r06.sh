@@ -1,0 +1,44 @@
+#!/bin/bash
+# Round 6's GPU sessions, one gpurun call each (<= 1200 s):
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_plan_r06.sh a
+# (round 5's sessions: tools/gpu_plan_r05.sh; the step kinds: tools/gpu_session.sh)
+set -uo pipefail
+cd "$(dirname "$0")/.."
+case ${1:-} in
+  # a: the round-5 build's line on this box, then where k_sweep_async's time goes per round
+  #    (variants/aprof: -DGC_A_PROF=1 -- light phase, wait for the last light, hub phase, passes)
+  #    on R-MAT-24 and R-MAT-26
+  a) exec_steps=("bench:rmat24:--no-north-star,--no-cpu-baseline,--no-end-to-end"
+                 env:GC_LIB_PATH=variants/aprof/libgcolor.so env:GC_A_PROF_OUT=gpurun_out/r06a/aprof_rmat24.txt
+                 "py:tools/round_cost.py:run,rmat24,gpurun_out/r06a/records_rmat24.json,1"
+                 env:GC_A_PROF_OUT=gpurun_out/r06a/aprof_rmat26.txt
+                 "py:tools/round_cost.py:run,rmat26,gpurun_out/r06a/records_rmat26.json,1"
+                 env:GC_LIB_PATH= env:GC_A_PROF_OUT=) ;;
+  # a2: the same with the hub scan's entries counted (scanned, longest scan, winners, entries left)
+  a2) exec_steps=(env:GC_LIB_PATH=variants/aprof/libgcolor.so env:GC_A_PROF_OUT=gpurun_out/r06a2/aprof_rmat24.txt
+                 "py:tools/round_cost.py:run,rmat24,gpurun_out/r06a2/records_rmat24.json,1"
+                 env:GC_A_PROF_OUT=gpurun_out/r06a2/aprof_rmat26.txt
+                 "py:tools/round_cost.py:run,rmat26,gpurun_out/r06a2/records_rmat26.json,1"
+                 env:GC_LIB_PATH= env:GC_A_PROF_OUT=) ;;
+  # b: the hub core (csrc/gc_core.hip): its parity tests, the hub settings, then the interleaved A/B
+  b) exec_steps=(env:GC_CORE_DEBUG=1 "py:tools/core_probe.py" env:GC_CORE_DEBUG=
+                 file:tests/test_gpu_core.py file:tests/test_gpu_hubs.py file:tests/test_gpu_parity.py
+                 "ab:rmat24:3:base,nocore=GC_HUB_CORE:0" "ab:rmat26:2:base,nocore=GC_HUB_CORE:0") ;;
+  # c: k_hub_core's launch times against k_sweep_async's (kernel trace of R-MAT-24, core on then off)
+  c) mkdir -p gpurun_out/r06c && cd /tmp && export TMPDIR=/tmp &&
+     timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/gpurun_out/r06c/trace" -o run -- \
+       python3 "$GRAFT_REPO_ROOT/tools/core_probe.py" 24:512 > "$GRAFT_REPO_ROOT/gpurun_out/r06c/probe.log" 2>&1
+     rc=$?; cd "$GRAFT_REPO_ROOT"; f=$(find gpurun_out/r06c/trace -name '*kernel_stats.csv' | head -1)
+     [ -n "$f" ] && cp "$f" gpurun_out/r06c/kernel_stats.csv; find gpurun_out/r06c/trace -name '*kernel_trace.csv' -delete
+     [ $rc -eq 0 ] || exit $rc
+     GC_LIB_PATH=variants/aprof/libgcolor.so GC_A_PROF_OUT=gpurun_out/r06c/aprof_rmat24.txt timeout -k 10 300 \
+       python -u tools/round_cost.py run rmat24 gpurun_out/r06c/records_rmat24.json 1 > gpurun_out/r06c/aprof.log 2>&1
+     exit $? ;;
+  # d: per-round kernel cost with the hub core (the default build), R-MAT-24, and with it off
+  d) exec_steps=(rounds:rmat24:core env:GC_HUB_CORE=0 rounds:rmat24:nocore env:GC_HUB_CORE=) ;;
+  # e: k_hub_core's phases per round (variants/aprof: load + setup, windows), R-MAT-24
+  e) exec_steps=(file:tests/test_gpu_core.py env:GC_LIB_PATH=variants/aprof/libgcolor.so env:GC_A_PROF_OUT=gpurun_out/r06e/aprof_rmat24.txt
+                 "py:tools/round_cost.py:run,rmat24,gpurun_out/r06e/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_A_PROF_OUT=) ;;
+  *) echo "usage: $0 a|..." >&2; exit 2 ;;
+esac
+bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"

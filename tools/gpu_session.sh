@@ -6,7 +6,6 @@
 #   tests             pytest -m gpu (every GPU test)
 #   tests:EXPR        pytest -m gpu -k EXPR (~ stands for a space: not~slow)
 #   file:PATH[:EXPR]  pytest -m gpu on one test file (optionally -k EXPR)
-#   staged[:EXPR]     the staged GPU tests (tests/test_gpu_staged.py, -m gpu_staged, GC_RUN_STAGED=1)
 #   smoke             __graft_entry__.smoke()
 #   bench:WL[:ARGS]   bench.py --workload WL [ARGS, comma-separated]
 #   step:WL           tools/step_timing.py WL (phase times of the step)
@@ -14,7 +13,7 @@
 #   py:SCRIPT[:ARGS]  python SCRIPT [ARGS, comma-separated] (a tools/ script; 600 s limit)
 #   env:NAME=VALUE    export NAME=VALUE for the steps after it (env:NAME= unsets it)
 #   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
-#   rounds:WL         per-round kernel cost by frontier size (tools/round_cost.py under
+#   rounds:WL[:SFX]   per-round kernel cost by frontier size (tools/round_cost.py under
 #                     rocprofv3 --kernel-trace; the raw trace is deleted after the analysis)
 #   brounds:WL        variant B's per-round cost (tools/b_round_cost.py, likewise)
 #   torchrun:N[:ARGS] bench.py --gpus N under torch.distributed.run, every rank on GPU 0, gloo
@@ -57,12 +56,6 @@ for st in "$@"; do
       else
         timeout -k 10 1000 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
       fi ;;
-    staged)
-      if [ -n "$rest" ]; then
-        GC_RUN_STAGED=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v --timeout 300 --timeout-method thread -k "$rest" > "$log" 2>&1
-      else
-        GC_RUN_STAGED=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_staged.py -m gpu_staged -x -v --timeout 300 --timeout-method thread > "$log" 2>&1
-      fi ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
     bench)
@@ -91,13 +84,15 @@ for st in "$@"; do
         ( cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$C/pmc_write" -o run -- "$C/gather_bytes" 5 ) >> "$log" 2>&1 &&
         python tools/ubench_pmc.py "$C" > "$C/calibration.json" 2>> "$log" && cat "$C/timing.txt" "$C/calibration.json" >> "$log" ;;
     rounds)
-      mkdir -p "$O/rounds_$rest"
-      ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/rounds_$rest" -o run -- \
-          python3 "$ROOT/tools/round_cost.py" run "$rest" "$O/rounds_$rest/records.json" 2 ) > "$log" 2>&1 &&
-        tr=$(find "$O/rounds_$rest" -name '*kernel_trace.csv' -print -quit) && [ -n "$tr" ] &&
-        python tools/round_cost.py analyze "$tr" "$O/rounds_$rest/records.json" \
-          > "$O/rounds_$rest/round_cost.txt" 2>> "$log" &&
-        rm -f "$tr" && cat "$O/rounds_$rest/round_cost.txt" >> "$log" ;;
+      wl=${rest%%:*}; sfx=${rest#*:}; [ "$sfx" = "$rest" ] && sfx=""
+      RD="$O/rounds_$wl${sfx:+_$sfx}"
+      mkdir -p "$RD"
+      ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$RD" -o run -- \
+          python3 "$ROOT/tools/round_cost.py" run "$wl" "$RD/records.json" 2 ) > "$log" 2>&1 &&
+        tr=$(find "$RD" -name '*kernel_trace.csv' -print -quit) && [ -n "$tr" ] &&
+        python tools/round_cost.py analyze "$tr" "$RD/records.json" \
+          > "$RD/round_cost.txt" 2>> "$log" &&
+        rm -f "$tr" && cat "$RD/round_cost.txt" >> "$log" ;;
     brounds)
       mkdir -p "$O/brounds_$rest"
       ( cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace -T -f csv -d "$O/brounds_$rest" -o run -- \
