@@ -442,6 +442,27 @@ def north_star(torch, barrier, args):
     return out
 
 
+def variant_b_line(torch, barrier, args):
+    """coloring_optimized.py's path (variant B) on the bench workload's graph (C3, R-MAT-24),
+    the same §8d step, a few steps -- so the driver's own run measures it too.
+    Its fold is the resolve class: roofline on the calibrated PMC basis of profiles/pmc/rmat24_B.json
+    when that summary is of this build."""
+    w = WORKLOADS["rmat24"]
+    dg0, _ = build_graph(w)
+    S = StepRunner(dg0, "B", {"priority": None, "speculative": False}, torch, barrier)
+    dg0.close()
+    probe, _ = S.step(timing=True)  # warmup, every class event-timed
+    t, kern, r, ph = S.steps(args.variant_b_steps, None)
+    m = S.nnz // 2
+    out = {"workload": w["desc"], "variant": "B (coloring_optimized.py)", "steps": args.variant_b_steps,
+           "ms_per_step": t * 1e3, "edges_per_s": m / t, "colors_used": r.num_colors, "rounds": r.rounds,
+           "async_fold_aborts": r.async_aborts, "phases_ms": {k: round(v * 1e3, 3) for k, v in ph.items()},
+           "roofline_calibrated": calibrated_roofline("rmat24", "B", probe.kernels),
+           "pmc_frac": pmc_step_frac("rmat24", "B", t)}
+    S.close()
+    return out
+
+
 def calibrated_roofline(workload, variant, kern):
     """The dominant class (by event-timed time) on the calibrated physical basis: 2 x FETCH_SIZE
     + WRITE_SIZE per launch (calibration()) / the class's average launch time, against the HBM
@@ -749,6 +770,9 @@ def main():
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: rmat24 (C3) on one GPU; rmat28 (C5, the north star's scaling graph) for the "
                          "modes that split one colouring over N > 1 GPUs (hybrid, sharded)")
+    ap.add_argument("--no-variant-b", action="store_true",
+                    help="skip the variant-B (coloring_optimized.py) measurement the default run adds (variant_b object)")
+    ap.add_argument("--variant-b-steps", type=int, default=3)
     ap.add_argument("--variant", default="A", choices=["A", "B"],
                     help="A = coloring.py semantics, B = coloring_optimized.py ('Optimizovano')")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
@@ -965,6 +989,14 @@ def main():
         except Exception as e:  # noqa: BLE001 -- reported in the line, which still prints
             ns = {"error": f"{type(e).__name__}: {e}"}
             print(f"WARNING: north_star failed: {ns['error']}", file=sys.stderr, flush=True)
+    vb = None
+    if world == 1 and args.workload == "rmat24" and not args.no_variant_b and V == "A" and not any(mode.values()):
+        try:
+            progress("variant B (R-MAT-24)")
+            vb = variant_b_line(torch, barrier, args)
+        except Exception as e:  # noqa: BLE001 -- reported in the line, which still prints
+            vb = {"error": f"{type(e).__name__}: {e}"}
+            print(f"WARNING: variant_b failed: {vb['error']}", file=sys.stderr, flush=True)
     classes = class_table(probe.kernels, pmc)
     line = {
         "metric": METRIC,
@@ -1030,6 +1062,7 @@ def main():
                                         / HBM_PEAK_GBS,
         "whole_job_pmc_frac": pmc_step_frac(args.workload, V, t),
         "north_star": ns,
+        "variant_b": vb,
         "cpu_baseline": cpu,
     }
     s = json.dumps(line)

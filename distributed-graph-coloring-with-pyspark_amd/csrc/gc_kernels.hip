@@ -3303,16 +3303,25 @@ int gc_measure_resident(const void* key, gc_graph_ctl_view v, int query, void (*
     if (query <= 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         return query;
     const int grid = cus * std::min(8, query + 1);  // one more per CU than the runtime allows
-    ull r[2] = {0, 0};
-    if (hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess) return std::max(1, query - 1);
-    launch(*v.g, grid, v.s);
-    if (hipMemcpyAsync(r, v.g->ctl->async_done, sizeof(r), hipMemcpyDeviceToHost, v.s) != hipSuccess ||
-        hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess || hipStreamSynchronize(v.s) != hipSuccess)
-        return std::max(1, query - 1);
-    const int per_cu = std::max(1, std::min(query, (int)(r[1] / (ull)cus)));
-    if (getenv("GC_DEBUG"))
-        fprintf(stderr, "[gc] residency probe: %llu of %d workgroups resident at once (runtime answer %d per CU) -> %d per CU\n",
-                r[1], grid, query, per_cu);
+    // A process's first launches of a kernel can dispatch slowly enough that the probe's
+    // 100-us window closes before every resident workgroup arrived (round 6 saw 256 of 2048 in
+    // one process, and the grid would have stayed at 1 per CU for good): the probe
+    // runs again while it reads below the runtime's answer, and the largest reading counts.
+    ull best = 0;
+    for (int attempt = 0; attempt < 4 && best < (ull)cus * (ull)query; ++attempt) {
+        ull r[2] = {0, 0};
+        if (hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess) return std::max(1, query - 1);
+        launch(*v.g, grid, v.s);
+        if (hipMemcpyAsync(r, v.g->ctl->async_done, sizeof(r), hipMemcpyDeviceToHost, v.s) != hipSuccess ||
+            hipMemsetAsync(v.g->ctl->async_done, 0, sizeof(r), v.s) != hipSuccess || hipStreamSynchronize(v.s) != hipSuccess)
+            return std::max(1, query - 1);
+        if (getenv("GC_DEBUG"))
+            fprintf(stderr, "[gc] residency probe %d: %llu of %d workgroups resident at once (runtime answer %d per CU)\n",
+                    attempt, r[1], grid, query);
+        best = std::max(best, r[1]);
+    }
+    const int per_cu = std::max(1, std::min(query, (int)(best / (ull)cus)));
+    if (getenv("GC_DEBUG")) fprintf(stderr, "[gc] residency: %d per CU\n", per_cu);
     std::lock_guard<std::mutex> lk(mu);
     cache[{key, dev}] = per_cu;
     return per_cu;

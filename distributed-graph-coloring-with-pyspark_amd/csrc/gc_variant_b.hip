@@ -998,7 +998,10 @@ __device__ int b_async_resident(GDev& g, const BLists& B, int* l1, int n1, int* 
 // pass % 3, spills to slot (pass + 1) % 3, uses the arrays of slot (pass + 2) % 3 as the
 // waves' scratch and clears that slot's counts (as k_b_ev does)
 // 6 waves per SIMD (80 VGPRs, 28 B of scratch per lane): R-MAT-26 -2.4 to -4.5% against 5, R-MAT-24 flat (r05/av)
-__global__ void __launch_bounds__(GC_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) k_b_async(GDev g, BLists B, int* ev, int pass,
+#ifndef GC_B_WPE  // waves per SIMD the fold is compiled for (6: 80 VGPRs; a diagnostic build of the 7-8 per CU cliff raises it)
+#define GC_B_WPE 6
+#endif
+__global__ void __launch_bounds__(GC_BLOCK) __attribute__((amdgpu_waves_per_eu(GC_B_WPE))) k_b_async(GDev g, BLists B, int* ev, int pass,
                                                                                        long long budget) {
     DevCtl* c = g.ctl;
     if (budget < 0) {  // residency probe (gcl_b_async_resident)
@@ -1156,6 +1159,71 @@ struct RunB {
 // The (deg, pos) rank partition (graph creation, gc_set_priority) already splits every low
 // part by degree and counts the equal-degree entries (neq); variant A never looks inside a
 // low part, so the layout serves both variants.
+// GC_B_STALL_DUMP=prefix (diagnostics of the asynchronous fold's give-ups): the
+// first time a round's fold is left unfinished by a k_b_async launch that stopped at its budget,
+// write the state the host's passes start from -- the unsettled items (the three lists of the
+// spill slot), k8, cand, the eviction times, cursors, watched entries and pending entries -- as
+// raw arrays <prefix>.<name>.bin, for tools/b_stall_analyze.py
+static int b_stall_dump(gc_graph* g, const BLists& B, const int* ev, const DevCtl& h, long long passes, long long round) {
+    static bool done = false;
+    const char* pre = getenv("GC_B_STALL_DUMP");
+    if (!pre || done || h.async_aborts == 0) return GC_OK;
+    done = true;
+    const int ws = (int)(passes % 3);
+    auto dump = [&](const char* name, const void* dev, size_t bytes) -> int {
+        std::vector<char> buf(bytes);
+        if (bytes) GC_READ(g->stream, buf.data(), (const char*)dev, bytes);
+        std::string path = std::string(pre) + "." + name + ".bin";
+        if (FILE* f = fopen(path.c_str(), "wb")) {
+            fwrite(buf.data(), 1, bytes, f);
+            fclose(f);
+        }
+        return GC_OK;
+    };
+    int rc;
+    for (int k = 0; k < 3; ++k) {
+        const char* nm[3] = {"adm", "heavy", "evict"};
+        if ((rc = dump(nm[k], B.l[k][ws], sizeof(int) * (size_t)h.bcnt[3 * k + ws]))) return rc;
+    }
+    if ((rc = dump("k8", g->k8, (size_t)g->n)) || (rc = dump("cand", g->cand, sizeof(int) * (size_t)g->n)) ||
+        (rc = dump("ev", ev, sizeof(int) * (size_t)g->n)) || (rc = dump("lcur", g->lcur, sizeof(int) * (size_t)g->n)) ||
+        (rc = dump("watch", B.watch, sizeof(int) * (size_t)g->n)) ||
+        (rc = dump("nhe", B.nhe, sizeof(int) * (size_t)g->n)) || (rc = dump("neq", g->neq, sizeof(int) * (size_t)g->n)))
+        return rc;
+    {  // the listed items' pending entries only: [v, count, entries...] per item (the whole array is nnz ints)
+        std::vector<long long> rp((size_t)g->n + 1);
+        std::vector<int> lcur((size_t)g->n), pend((size_t)g->nnz);
+        GC_READ(g->stream, rp.data(), g->rp, rp.size());
+        GC_READ(g->stream, lcur.data(), g->lcur, lcur.size());
+        if (g->nnz) GC_READ(g->stream, pend.data(), B.pend, pend.size());
+        std::vector<int> outv;
+        for (int k = 0; k < 3; ++k) {
+            std::vector<int> items((size_t)h.bcnt[3 * k + ws]);
+            if (!items.empty()) GC_READ(g->stream, items.data(), B.l[k][ws], items.size());
+            for (int v : items) {
+                const int lc = lcur[(size_t)v];
+                const int cnt = lc < 0 ? -lc - 1 : 0;
+                outv.push_back(v);
+                outv.push_back(cnt);
+                for (int i = 0; i < cnt; ++i) outv.push_back(pend[(size_t)rp[(size_t)v] + i]);
+            }
+        }
+        std::string path = std::string(pre) + ".pendrows.bin";
+        if (FILE* f = fopen(path.c_str(), "wb")) {
+            fwrite(outv.data(), sizeof(int), outv.size(), f);
+            fclose(f);
+        }
+    }
+    std::string path = std::string(pre) + ".info.txt";
+    if (FILE* f = fopen(path.c_str(), "w")) {
+        fprintf(f, "round %lld passes %lld aborts %llu n %lld nnz %lld adm %llu heavy %llu evict %llu\n", round, passes,
+                (unsigned long long)h.async_aborts, g->n, g->nnz, (unsigned long long)h.bcnt[ws],
+                (unsigned long long)h.bcnt[3 + ws], (unsigned long long)h.bcnt[6 + ws]);
+        fclose(f);
+    }
+    return GC_OK;
+}
+
 static int ensure_bpart(gc_graph* g) {
     if (g->part_prio != GC_PRIORITY_REF || !g->bpart || !g->neq || !g->nhe) {
         gc_set_error("variant B needs the (deg, pos) row partition");
@@ -1343,6 +1411,7 @@ int gc_color_variant_b(gc_graph* g, const gc_options* opt, int32_t* colors_out, 
             if (sn.halt != GC_H_SWEEPS) { gc_set_error("variant B: unexpected halt %d", sn.halt); return GC_EHIP; }
             // round cur's fold is unfinished (round cur + 1 ran as a no-op): its passes, its commit
             if ((rc = R.sync())) return rc;
+            if ((rc = b_stall_dump(g, B, ev, h, np, cur))) return rc;
             GC_HIP(hipMemsetAsync(&g->ctl->halt, 0, sizeof(int), s));
             long long passes = np;
             for (long long batch = 4;; batch = std::min(batch * 2, 16ll)) {

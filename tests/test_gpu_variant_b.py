@@ -276,6 +276,23 @@ def test_rmat20_variant_b_against_oracle(monkeypatch, env):
         assert dg.validate() == (0, 0)
 
 
+@pytest.mark.parametrize("bpc", ["7", "8"])
+def test_fold_past_six_per_cu_requested(monkeypatch, bpc):
+    """variant B's asynchronous fold asked for 7 / 8 workgroups per CU on R-MAT-20
+    (round 5's cliff: 10-13 give-ups a colouring) -- no give-up, the oracle's colouring.  The
+    default build is compiled for 6 waves per SIMD (80 VGPRs), so the grid is capped at the
+    residency the probe measures (6); builds for 7 and 8 (-DGC_B_WPE=7/8, resident caps 640 /
+    512) ran every workgroup resident with no give-up either (profiles/r06/f, g)."""
+    for k in ("GC_B_ASYNC", "GC_B_ASYNC_K", "GC_ASYNC_BUDGET_US", "GC_B_RESIDENT", "GC_B_REFSKIP"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("GC_B_ASYNC_BPC", bpc)
+    with _dg().rmat(20, 16, seed=5) as dg:
+        rp, col = dg.export()
+        g = dg.color("B")
+        assert g.async_aborts == 0
+        assert_same_run(g, oracle.c_color(rp, col, "B"))
+
+
 def test_async_grids_sized_from_measured_residency(monkeypatch):
     """The asynchronous kernels' grids (variant B's fold k_b_async, variant A's k_sweep_async)
     are capped at the workgroups measured resident (gc_residency_probe); any requested grid,

@@ -39,6 +39,23 @@ case ${1:-} in
   # e: k_hub_core's phases per round (variants/aprof: load + setup, windows), R-MAT-24
   e) exec_steps=(file:tests/test_gpu_core.py env:GC_LIB_PATH=variants/aprof/libgcolor.so env:GC_A_PROF_OUT=gpurun_out/r06e/aprof_rmat24.txt
                  "py:tools/round_cost.py:run,rmat24,gpurun_out/r06e/records_rmat24.json,1" env:GC_LIB_PATH= env:GC_A_PROF_OUT=) ;;
+  # f: variant B's fold at 6 / 7 / 8 workgroups per CU (variants/bwpe8: compiled for 8 waves per SIMD,
+  #    resident cap 512), the state of the first give-up dumped (tools/b_stall_analyze.py)
+  f) exec_steps=(env:GC_LIB_PATH=variants/bwpe8/libgcolor.so "py:tools/b_stall_probe.py:gpurun_out/r06f,20,6,7,8"
+                 env:GC_LIB_PATH=) ;;
+  # g: the fold compiled for 7 / 8 waves per SIMD (variants/bwpe7: 72 VGPRs, resident cap 640;
+  #    bwpe8: 64 VGPRs, cap 512) against the default (6), GC_B_ASYNC_BPC=8 (each capped by its measured
+  #    residency), variant B on R-MAT-24 and R-MAT-26; the default build at 6 / 7 / 8 per CU requested
+  g) exec_steps=("py:tools/b_stall_probe.py:gpurun_out/r06g,20,6,7,8" env:AB_VARIANT=B env:GC_B_ASYNC_BPC=8
+                 "abl:rmat24:3:2:base=-,w7=variants/bwpe7/libgcolor.so,w8=variants/bwpe8/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,w7=variants/bwpe7/libgcolor.so,w8=variants/bwpe8/libgcolor.so"
+                 env:AB_VARIANT= env:GC_B_ASYNC_BPC=) ;;
+  # h: C5's full-size fixture: R-MAT-28 coloured by the multi-core restatement on the box's 16 threads
+  #    (tests/golden/rmat_omp_s28.json; heartbeat lines every 20 s)
+  h) exec_steps=("pyl:tools/make_rmat27_omp_fixture.py:gpurun_out/r06h/rmat_omp_s28.json,28") ;;
+  # i: a fold stopped on purpose (zero budget): the dumped state of its first give-up, R-MAT-18, for
+  #    tools/b_stall_analyze.py (does every listed item wait on an earlier listed one?)
+  i) exec_steps=(env:GC_ASYNC_BUDGET_US=0 "py:tools/b_stall_probe.py:gpurun_out/r06i,18,6" env:GC_ASYNC_BUDGET_US=) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"

@@ -23,14 +23,14 @@ timeout -k 10 400 python -u bench.py --workload $WL --json-out "$OUT/bench.json"
 tail -1 "$OUT/bench.log" | cut -c1-600
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/trace" -o run -- \
-  python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-end-to-end --steps 3 --warmup 1 "$@" > "$OUT/trace.log" 2>&1
+  python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-variant-b --no-end-to-end --steps 3 --warmup 1 "$@" > "$OUT/trace.log" 2>&1
 # counters: the same command at 3 and at 1 timed steps; per-kernel numbers from the first,
 # the whole step's bytes from the difference / 2 (setup, warmup and the rest cancel)
 for K in 3 1; do
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -T -f csv -d "$OUT/pmc_fetch$K" -o run -- \
-    python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-end-to-end --no-event-timing --steps $K --warmup 1 "$@" > "$OUT/pmc_fetch$K.log" 2>&1
+    python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-variant-b --no-end-to-end --no-event-timing --steps $K --warmup 1 "$@" > "$OUT/pmc_fetch$K.log" 2>&1
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -T -f csv -d "$OUT/pmc_write$K" -o run -- \
-    python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-end-to-end --no-event-timing --steps $K --warmup 1 "$@" > "$OUT/pmc_write$K.log" 2>&1
+    python "$ROOT/bench.py" --workload $WL --no-cpu-baseline --no-north-star --no-variant-b --no-end-to-end --no-event-timing --steps $K --warmup 1 "$@" > "$OUT/pmc_write$K.log" 2>&1
 done
 cd "$ROOT"
 python tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.json"

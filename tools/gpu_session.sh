@@ -11,6 +11,7 @@
 #   step:WL           tools/step_timing.py WL (phase times of the step)
 #   profile:WL[:ARGS] tools/gpu_profile.sh TAG WL [ARGS] (trace + PMC passes, summaries)
 #   py:SCRIPT[:ARGS]  python SCRIPT [ARGS, comma-separated] (a tools/ script; 600 s limit)
+#   pyl:SCRIPT[:ARGS] the same with an 1100 s limit (fixture builds)
 #   env:NAME=VALUE    export NAME=VALUE for the steps after it (env:NAME= unsets it)
 #   ubench:NAME[:ARGS] build tools/ubench/NAME.hip for gfx950 and run it (120 s limit)
 #   rounds:WL[:SFX]   per-round kernel cost by frontier size (tools/round_cost.py under
@@ -111,6 +112,9 @@ for st in "$@"; do
     py)
       sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
+    pyl)
+      sc=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      timeout -k 10 1100 python -u "$sc" ${a//,/ } > "$log" 2>&1 ;;
     abl)
       wl=${rest%%:*}; a=${rest#*:}; reps=${a%%:*}; a=${a#*:}; cyc=${a%%:*}; vs=${a#*:}
       timeout -k 10 1100 bash tools/ab_libs.sh "$wl" "$reps" "$cyc" ${vs//,/ } > "$log" 2>&1 &&
