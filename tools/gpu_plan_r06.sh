@@ -56,6 +56,10 @@ case ${1:-} in
   # i: a fold stopped on purpose (zero budget): the dumped state of its first give-up, R-MAT-18, for
   #    tools/b_stall_analyze.py (does every listed item wait on an earlier listed one?)
   i) exec_steps=(env:GC_ASYNC_BUDGET_US=0 "py:tools/b_stall_probe.py:gpurun_out/r06i,18,6" env:GC_ASYNC_BUDGET_US=) ;;
+  # j: the full-size pins (R-MAT-24 restatement vs the single-thread oracle, R-MAT-26 vs the single-thread
+  #    oracle, R-MAT-27/28 vs the restatement), then the hub threshold re-swept on the round-6 engine
+  j) exec_steps=("file:tests/test_gpu_fullsize.py:against_single_thread_oracle~or~engine_against_multicore"
+                 "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
