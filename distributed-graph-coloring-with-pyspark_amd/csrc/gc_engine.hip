@@ -305,6 +305,8 @@ struct Run {
         const long long us = getenv("GC_ASYNC_BUDGET_US") ? atoll(getenv("GC_ASYNC_BUDGET_US")) : 20000;
         async_budget = std::max(1ll, us) * (long long)rate_khz / 1000;
         async_grid = cus * bpc;
+        // GC_ASYNC_WG (tests): fewer workgroups, so each wave holds long hub and light lists
+        if (getenv("GC_ASYNC_WG") && atoi(getenv("GC_ASYNC_WG")) > 0) async_grid = std::min(async_grid, atoi(getenv("GC_ASYNC_WG")));
         // the hub core (gc_core.hip): its buffers once per graph; GC_HUB_CORE=0 off
         if (!d.hub_repl && gc_core_prepare(g, d) == GC_OK) core_on = d.core_cap > 0;
     }

@@ -264,6 +264,9 @@ __device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex) {
 // (mex >= 64, so mex <= deg <= heavy_t < GC_INL_BITS) are proposed here, the whole wave on
 // one of them at a time, instead of in a k_propose_block launch after this one.
 #define GC_INL_WORDS 32  // 2048-bit LDS window per wave for a wide light's mex
+#ifndef GC_PH_B
+#define GC_PH_B 4  // hub bitmaps read together by k_propose<1>
+#endif
 #define GC_INL_BITS (64 * GC_INL_WORDS)
 template <int INL>
 __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
@@ -342,24 +345,51 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
             gc_wave_append(iswide, v, L.wide, &c->wide_cnt);
             continue;
         }
-        // hubs: the first zero bit of the pushed bitmap (as k_propose_block's hub waves)
-        for (ull hm = __ballot(isheavy); hm; hm &= hm - 1) {
-            const int l = __ffsll((long long)hm) - 1;
-            const int hv = __shfl(v, l, GC_WAVE);
-            const int x = g.hid[hv];
-            const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
-            long long mex = -1;
-            for (int t0 = 0; t0 < hwords && mex < 0; t0 += GC_WAVE) {  // a zero bit lies in range
-                const int t = t0 + lane;
-                const unsigned wd = t < hwords ? hb[t] : 0xFFFFFFFFu;
-                const ull zm = __ballot(wd != 0xFFFFFFFFu);
-                if (zm) {
-                    const int zl = __ffsll((long long)zm) - 1;
-                    const unsigned zw = __shfl(wd, zl, GC_WAVE);
-                    mex = 32ll * (t0 + zl) + __builtin_ctz(~zw);
+        // hubs: the first zero bit of the pushed bitmap (as k_propose_block's hub waves), the
+        // whole wave on each bitmap's words; the chunk's hub indices are loaded one per lane and
+        // GC_PH_B bitmaps are read together, so a chunk of h hubs costs 1 + h / GC_PH_B
+        // dependent trips (a hub at a time: 2 h), and every hub's own state is written by its
+        // lane, all at once
+        if (const ull hm0 = __ballot(isheavy)) {
+            const int xl = isheavy ? g.hid[v] : -1;
+            long long hmex = -1;  // this lane's hub's mex
+            for (ull hm = hm0; hm;) {
+                int hl[GC_PH_B];
+                const unsigned* hb[GC_PH_B];
+                long long mx[GC_PH_B];
+#pragma unroll
+                for (int k = 0; k < GC_PH_B; ++k) {
+                    hl[k] = hm ? __ffsll((long long)hm) - 1 : -1;  // wave-uniform
+                    hm &= hm - 1;
+                    const int xk = __shfl(xl, hl[k] < 0 ? 0 : hl[k], GC_WAVE);
+                    hb[k] = g.hbits + (long long)(hl[k] < 0 ? 0 : xk) * g.hbits_w;
+                    mx[k] = hl[k] < 0 ? 0 : -1;
                 }
+                for (int t0 = 0; t0 < hwords; t0 += GC_WAVE) {  // a zero bit lies in range
+                    const int t = t0 + lane;
+                    unsigned wd[GC_PH_B];
+#pragma unroll
+                    for (int k = 0; k < GC_PH_B; ++k) wd[k] = (mx[k] < 0 && t < hwords) ? hb[k][t] : 0xFFFFFFFFu;
+                    bool done = true;
+#pragma unroll
+                    for (int k = 0; k < GC_PH_B; ++k) {
+                        const ull zm = __ballot(wd[k] != 0xFFFFFFFFu);
+                        if (mx[k] < 0 && zm) {
+                            const int zl = __ffsll((long long)zm) - 1;
+                            const unsigned zw = __shfl(wd[k], zl, GC_WAVE);
+                            mx[k] = 32ll * (t0 + zl) + __builtin_ctz(~zw);
+                        }
+                        done = done && mx[k] >= 0;
+                    }
+                    if (done) break;
+                }
+#pragma unroll
+                for (int k = 0; k < GC_PH_B; ++k)
+                    if (lane == hl[k]) hmex = mx[k];
             }
-            if (lane == 0) {
+            if (isheavy) {
+                const int x = xl;
+                const long long mex = hmex;
                 if (g.hub_w) {  // the hub JP's state: this round's conflict flag, cursors, mirror
                     g.hkill[x] = 0u;
                     g.hcur[x] = 0;
@@ -367,10 +397,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
                     if (g.hprep) g.hkcnt[x] = 0;
                     g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);
                 }
-                gc_set_cand(g, hv, mex);
+                gc_set_cand(g, v, mex);
                 lmax = mex > lmax ? mex : lmax;
                 if (kbound >= 0 && mex >= kbound) lfail++;
-                lsum += (ull)g.deg[hv];
+                lsum += (ull)d;
                 lnv++;
             }
         }
@@ -728,7 +758,7 @@ __device__ unsigned gc_hub_scan_wave(const GDev& g, int x, unsigned cv6, int cv,
 // another paid a chain of dependent loads per hub -- the hub-start sweep's floor.  The
 // hubs' state comes prefetched, one per lane (slot j of the prefetch = lane j).
 #ifndef GC_HUB_NG
-#define GC_HUB_NG 4
+#define GC_HUB_NG 8  // (4: R-MAT-26 +1.0%, R-MAT-24 +-0.5%; 16: R-MAT-24 +4%, profiles/r06/n)
 #endif
 __device__ void gc_hub_scan_groups(GDev& g, int nj, int pv, unsigned pkv, int pcv, int px, unsigned pkill,
                                    const GcHubPre& pp, GcStage& st, int* ho, ull* ho_cnt, ull& lsum, ull& lnv,
@@ -1496,12 +1526,58 @@ __device__ ull gc_aprof[GC_A_PROF_ROUNDS][GC_A_PROF_K];
 // group each): the resumable scan of gc_hub_scan_groups, with agent-scope loads of the
 // hub mirror and the kill flags and agent-scope stores of the decisions.  Pending hubs
 // are compacted to the front of hl; returns their number.
+// The hubs' own words (k8, cand, hid, then hkill, hlow_rp, hpc, hcur, hlen) are loaded for
+// 64 hubs at once, one per lane, and handed to the groups by shuffles (GC_HUB_PREFETCH, the
+// default; as the host sweeps' gc_hub_scan_groups): a group that loaded its hub's words
+// itself paid three dependent trips per hub before its row scan, ~16 times per 64 hubs.
+// (The kill flags are final during the hub phase: every light of the round has decided
+// before it starts.)  Entries are read a batch at a time, and survivors only move down, so
+// the compaction never overwrites an entry not yet read.
+#ifndef GC_HUB_PREFETCH
+#define GC_HUB_PREFETCH 1
+#endif
 __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
     constexpr int GS = GC_WAVE / GC_HUB_NG;
     const int lane = gc_lane();
     const int grp = lane / GS, li = lane % GS;
     const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
     int nw = 0;
+#if GC_HUB_PREFETCH
+    for (int b0 = 0; b0 < nh; b0 += GC_WAVE) {
+    const int bn = nh - b0 < GC_WAVE ? nh - b0 : GC_WAVE;
+    const int pv = lane < bn ? hl[b0 + lane] : -1;
+    const unsigned pkv = pv >= 0 ? (unsigned)g.k8[pv] : 0u;  // own byte
+    const int pcb = pv >= 0 ? g.cand[pv] : 0;                // read with k8: used when the candidate is >= 62
+    const int px = pv >= 0 ? g.hid[pv] : -1;                 // every heavy proposer is a hub while the hub JP is on
+    const int pcv = gc_k8_cand(pkv) == GC_K8_BIG ? pcb : (int)gc_k8_cand(pkv);
+    const int pkill = px >= 0 ? (int)gc_ald32(g.hkill + px) : 0;
+    long long pbase = 0;
+    int pfull = 0, pcur = 0, phc0 = 1, phs = 0;
+    if (px >= 0) {
+        pbase = g.hlow_rp[px];
+        pfull = (int)(g.hlow_rp[px + 1] - pbase);
+        pcur = g.hpc[px];
+        phc0 = g.hcur[px];
+        phs = g.hlen[px];
+    }
+    for (int j0 = 0; j0 < bn; j0 += GC_HUB_NG) {
+        const int j = j0 + grp;
+        const bool has = j < bn;
+        const int jj = has ? j : 0;  // every lane takes part in every shuffle
+        const int vs = __shfl(pv, jj, GC_WAVE);
+        const int v = has ? vs : -1;
+        const unsigned kv = (unsigned)__shfl((int)pkv, jj, GC_WAVE);
+        const int cv = __shfl(pcv, jj, GC_WAVE);
+        const int xs = __shfl(px, jj, GC_WAVE);
+        const int x = has ? xs : -1;
+        const int ks = __shfl(pkill, jj, GC_WAVE);  // not under a condition: a lane left out of a
+        const bool kill = x >= 0 && ks != 0;         // shuffle reads back nothing from its source
+        const long long base = __shfl(pbase, jj, GC_WAVE);
+        const int full = __shfl(pfull, jj, GC_WAVE);
+        const int cursor = __shfl(pcur, jj, GC_WAVE);
+        const int hc0 = __shfl(phc0, jj, GC_WAVE);
+        const int hstart = __shfl(phs, jj, GC_WAVE);
+#else
     for (int j0 = 0; j0 < nh; j0 += GC_HUB_NG) {
         const int j = j0 + grp;
         const int v = j < nh ? hl[j] : -1;
@@ -1518,6 +1594,7 @@ __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
             hc0 = g.hcur[x];
             hstart = g.hlen[x];
         }
+#endif
         const bool act = x >= 0 && !kill;  // group-uniform
         const bool first = hc0 == 0;
         int pos = first ? hstart : cursor;
@@ -1583,6 +1660,9 @@ __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
         if (pend) hl[nw + __popcll(pm & gc_lanemask_lt())] = v;
         nw += __popcll(pm);
     }
+#if GC_HUB_PREFETCH
+    }
+#endif
     return nw;
 }
 

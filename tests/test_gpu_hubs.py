@@ -62,19 +62,21 @@ SETTINGS = [
     {"GC_HUB_T": "0", "GC_HUB_CORE": "1", "GC_HUB_CORE_ITERS": "1", "GC_HUB_CORE_MINF": "0"},  # 2nd window: async
     {"GC_HUB_T": "3", "GC_HUB_CORE": "1", "GC_HUB_CORE_ITERS": "1", "GC_HUB_CORE_MINF": "0",
      "GC_ASYNC_BUDGET_US": "0"},                              # ... which gives up to host sweeps
+    {"GC_HUB_T": "0", "GC_ASYNC_WG": "1"},                    # k_sweep_async on 4 waves: hundreds of hubs
+    {"GC_HUB_T": "2", "GC_ASYNC_WG": "3"},                    # per wave, in 64-hub batches with ragged ends
 ]
 IDS = ["T0", "T2", "T5w1", "T3", "T16w2", "T64", "T512", "T1024", "off", "T0long4", "T2long0", "T0noprep",
        "T0pend", "T2pend_long0", "T0tail0", "T2tail128", "T0tail4096",
        "T2loop", "offloop8", "T0async_abort", "T2async_abort", "offasync_abort", "T3async_bpc1",
        "T0sync", "offsync", "T0noinl", "T512noinl", "T1024sync", "T2w2", "T0core", "T512core", "T0core16",
-       "T2core1", "T0coreall", "T64coreall", "T0coreit1", "T3coreit1_abort"]
+       "T2core1", "T0coreall", "T64coreall", "T0coreit1", "T3coreit1_abort", "T0async_wg1", "T2async_wg3"]
 
 
 @pytest.fixture(params=SETTINGS, ids=IDS)
 def hubenv(request, monkeypatch):
     for k in ("GC_HUB_T", "GC_HUB_W", "GC_HUB_LONG", "GC_HUB_PREP", "GC_HUB_SCAN", "GC_TAIL_HMAX_HUB", "GC_SWEEP_LOOP",
               "GC_LOOP_WG", "GC_ASYNC", "GC_ASYNC_BUDGET_US", "GC_ASYNC_BPC", "GC_INLINE_PB", "GC_HUB_CORE",
-              "GC_HUB_CORE_CAP", "GC_HUB_CORE_ITERS", "GC_HUB_CORE_MINF"):
+              "GC_HUB_CORE_CAP", "GC_HUB_CORE_ITERS", "GC_HUB_CORE_MINF", "GC_ASYNC_WG"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param.items():
         monkeypatch.setenv(k, v)

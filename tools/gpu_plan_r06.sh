@@ -60,6 +60,20 @@ case ${1:-} in
   #    oracle, R-MAT-27/28 vs the restatement), then the hub threshold re-swept on the round-6 engine
   j) exec_steps=("file:tests/test_gpu_fullsize.py:against_single_thread_oracle~or~engine_against_multicore"
                  "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768") ;;
+  k) exec_steps=("file:tests/test_gpu_fullsize.py:engine_against_multicore"
+                 "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768,t1024=GC_HUB_T:1024"
+                 "ab:rmat26:2:base,t768=GC_HUB_T:768,t1024=GC_HUB_T:1024,t2048=GC_HUB_T:2048") ;;
+  m) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_core.py"
+                 "abl:rmat24:3:2:base=-,nopf=variants/nopf/libgcolor.so,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,nopf=variants/nopf/libgcolor.so,ng8=variants/ng8/libgcolor.so"
+                 "file:tests/test_gpu_fullsize.py:engine_against_multicore") ;;
+  n) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_core.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,nopf=variants/nopf/libgcolor.so,phb1=variants/phb1/libgcolor.so,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,nopf=variants/nopf/libgcolor.so,phb1=variants/phb1/libgcolor.so,ng8=variants/ng8/libgcolor.so"
+                 "file:tests/test_gpu_fullsize.py:engine_against_multicore~or~north_star_rmat26") ;;
+  l) exec_steps=("abl:rmat24:3:2:base=-,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so,ng2=variants/ng2/libgcolor.so,ng8u4=variants/ng8u4/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so,ng8u4=variants/ng8u4/libgcolor.so") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
