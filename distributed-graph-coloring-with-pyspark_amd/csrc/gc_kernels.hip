@@ -268,6 +268,16 @@ __device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex) {
 #define GC_PH_B 4  // hub bitmaps read together by k_propose<1>
 #endif
 #define GC_INL_BITS (64 * GC_INL_WORDS)
+#ifndef GC_PROP_HINT
+#define GC_PROP_HINT 1  // k_propose<1>: hub bitmaps read from the last proposal's word (round 6)
+#endif
+#ifndef GC_HOIST_HIN
+#define GC_HOIST_HIN 0  // light kernels: cand / hin_rp loaded with the vertex's other words (round 6;
+                        // measured slower: the big rounds' extra loads, R-MAT-26 +3.6 ms, profiles/r06/q)
+#endif
+#ifndef GC_PB_HUB_LANES
+#define GC_PB_HUB_LANES 1  // k_propose_block: a run of hubs per wave, one per lane (round 6)
+#endif
 template <int INL>
 __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     DevCtl* c = g.ctl;
@@ -309,6 +319,28 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
         const int de = isheavy ? 0 : d;
         s_mask[w][lane] = 0;
         s_start[w][lane] = v >= 0 ? g.rp[v] : 0;
+        // GC_PROP_HINT (round 6): a hub's bitmap is read from the word of its last proposal on:
+        // bits are only ever set, so the mex never moves down, and a hub proposes about the
+        // newest colour every round (the first ~maxcolor/32 words are full).  The hint comes
+        // from its own k8 / cand words, loaded with its degree, and the two words from it are
+        // in flight with the light rows' loads: no dependent trip of its own.
+        int hx = -1, hw0 = 0;
+        unsigned hwa = 0xFFFFFFFFu, hwb = 0xFFFFFFFFu;
+        if (INL && GC_PROP_HINT) {
+            const int xs = v >= 0 ? g.hid[v] : -1;
+            const unsigned k8v = v >= 0 ? (unsigned)g.k8[v] : 0u;
+            const int cbv = v >= 0 ? g.cand[v] : 0;
+            if (isheavy && xs >= 0) {
+                hx = xs;
+                const unsigned c6 = gc_k8_cand(k8v);
+                const long long hint = c6 == GC_K8_NONE ? 0ll : (c6 == GC_K8_BIG ? (long long)cbv : (long long)c6);
+                hw0 = (int)(hint >> 5);
+                if (hw0 < 0 || hw0 >= hwords) hw0 = 0;
+                const unsigned* hb = g.hbits + (long long)hx * g.hbits_w;
+                hwa = hb[hw0];
+                if (hw0 + 1 < hwords) hwb = hb[hw0 + 1];
+            }
+        }
         const int incl = gc_wave_incl_scan(de);
         const int excl = incl - de;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -350,7 +382,33 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
         // GC_PH_B bitmaps are read together, so a chunk of h hubs costs 1 + h / GC_PH_B
         // dependent trips (a hub at a time: 2 h), and every hub's own state is written by its
         // lane, all at once
-        if (const ull hm0 = __ballot(isheavy)) {
+        if (GC_PROP_HINT && hx >= 0) {  // the first zero bit from the hint's word on
+            long long mex = -1;
+            if (hwa != 0xFFFFFFFFu) {
+                mex = 32ll * hw0 + __builtin_ctz(~hwa);
+            } else if (hwb != 0xFFFFFFFFu) {
+                mex = 32ll * (hw0 + 1) + __builtin_ctz(~hwb);
+            } else {
+                const unsigned* hb = g.hbits + (long long)hx * g.hbits_w;
+                for (int t = hw0 + 2; t < hwords && mex < 0; ++t) {
+                    const unsigned wd = hb[t];
+                    if (wd != 0xFFFFFFFFu) mex = 32ll * t + __builtin_ctz(~wd);
+                }
+            }
+            if (g.hub_w) {  // the hub JP's state: this round's conflict flag, cursors, mirror
+                g.hkill[hx] = 0u;
+                g.hcur[hx] = 0;
+                g.hpc[hx] = 0;
+                if (g.hprep) g.hkcnt[hx] = 0;
+                g.hk[hx] = gc_hk((unsigned)mex, GC_JP_UND);
+            }
+            gc_set_cand(g, v, mex);
+            lmax = mex > lmax ? mex : lmax;
+            if (kbound >= 0 && mex >= kbound) lfail++;
+            lsum += (ull)d;
+            lnv++;
+        }
+        if (const ull hm0 = GC_PROP_HINT ? 0ull : __ballot(isheavy)) {
             const int xl = isheavy ? g.hid[v] : -1;
             long long hmex = -1;  // this lane's hub's mex
             for (ull hm = hm0; hm;) {
@@ -458,7 +516,46 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
     // Hubs whose bitmap covers every colour in use: a wave each (first zero bit of a
     // <= 4096-bit bitmap), not a workgroup with its barriers.  Heavy == hub while hubs are on.
     const bool hub_waves = g.hbits_w && maxc + 2 <= 32ll * g.hbits_w;
-    if (hub_waves) {
+    if (hub_waves && GC_PB_HUB_LANES) {
+        // a run of up to 64 hubs per wave, one per lane: each lane reads its own hub's bitmap
+        // words, 8 in flight per step (round 6: a wave per hub walked ~46 hubs of a big round
+        // one after another, three dependent trips each)
+        const int lane = gc_lane();
+        const int w = threadIdx.x / GC_WAVE;
+        const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
+        const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+        const long long per = std::min<long long>(GC_WAVE, std::max<long long>(1, (na + W - 1) / W));
+        for (long long i0 = wid * per; i0 < na; i0 += W * per) {
+            const long long i = i0 + lane;
+            const int v = (lane < per && i < na) ? L.heavy[i] : -1;
+            const int x = v >= 0 ? g.hid[v] : -1;
+            const int d = v >= 0 ? g.deg[v] : 0;
+            long long mex = -1;
+            if (x >= 0) {
+                const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
+                for (int t0 = 0; t0 < words && mex < 0; t0 += 8) {
+                    unsigned wd[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) wd[k] = t0 + k < words ? hb[t0 + k] : 0xFFFFFFFFu;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (mex < 0 && wd[k] != 0xFFFFFFFFu) mex = 32ll * (t0 + k) + __builtin_ctz(~wd[k]);
+                }
+                if (g.hub_w) {  // the hub JP's state: this round's conflict flag, cursors, mirror
+                    g.hkill[x] = 0u;
+                    g.hcur[x] = 0;
+                    g.hpc[x] = 0;
+                    if (g.hprep) g.hkcnt[x] = 0;
+                    g.hk[x] = gc_hk((unsigned)mex, GC_JP_UND);
+                }
+                gc_set_cand(g, v, mex);
+                lmax = mex > lmax ? mex : lmax;
+                if (kbound >= 0 && mex >= kbound && (!g.hub_repl || (v >= g.own_lo && v < g.own_hi))) lfail++;
+                lsum += (ull)d;
+                lnv++;
+            }
+        }
+    } else if (hub_waves) {  // a wave per hub (round 5)
         const int lane = gc_lane();
         const int w = threadIdx.x / GC_WAVE;
         for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < na;
@@ -1133,6 +1230,13 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         const int nl0 = v >= 0 ? g.nlow[v] : 0;
         const unsigned kv0 = v >= 0 ? (unsigned)k8[v] : 0xFFu;
         const long long rs0 = v >= 0 ? g.rp[v] : 0;
+#if GC_HOIST_HIN
+        // with the vertex's other words (one trip): its candidate past 61 and its hub-list
+        // bounds, so neither is a dependent trip of its own later (round 6)
+        const int cb0 = v >= 0 ? g.cand[v] : 0;
+        const long long hs0 = (v >= 0 && g.hub_w) ? g.hin_rp[v] : 0;
+        const long long he0 = (v >= 0 && g.hub_w) ? g.hin_rp[v + 1] : 0;
+#endif
         const bool skip = v < 0 || (skip_heavy && d > g.heavy_t);
         // resumable: entries before lcur[v] were seen decided-not-IN or off-candidate in an
         // earlier sweep of this round (states only move UND -> IN/OUT), so skip them
@@ -1144,7 +1248,11 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
         s_first[w][lane] = 0x7FFFFFFF;
         s_start[w][lane] = v >= 0 ? rs0 + lc : 0;
         s_c6[w][lane] = cv6;
+#if GC_HOIST_HIN
+        s_cv[w][lane] = cv6 == GC_K8_BIG ? cb0 : (int)cv6;
+#else
         s_cv[w][lane] = cv6 == GC_K8_BIG ? g.cand[v] : (int)cv6;
+#endif
         const int incl = gc_wave_incl_scan(dl);
         const int excl = incl - dl;
         const int total = __shfl(incl, GC_WAVE - 1, GC_WAVE);
@@ -1175,8 +1283,13 @@ __device__ __forceinline__ void gc_jp_sweep(GDev& g, const int* __restrict__ lis
             int dh = 0;
             long long hs = 0;
             if (nst == GC_JP_IN) {
+#if GC_HOIST_HIN
+                hs = hs0;
+                dh = (int)(he0 - hs0);
+#else
                 hs = g.hin_rp[v];
                 dh = (int)(g.hin_rp[v + 1] - hs);
+#endif
             }
             gc_wave_sync();
             s_start[w][lane] = hs;
@@ -1420,13 +1533,64 @@ __global__ void __launch_bounds__(NW * GC_WAVE) k_sweep_tail(GDev g, GLists L, i
 // colouring.  gc_stats.async_aborts counts such launches.
 // ------------------------------------------------------------------------------------
 
+#ifndef GC_KILL_DEFER
+#define GC_KILL_DEFER 0  // k_sweep_async: light winners' hub kill flags raised in batches (round 6;
+                         // measured slower: R-MAT-26 +5 ms, R-MAT-24 +-1, profiles/r06/q)
+#endif
+#define GC_KILL_BUF 256
 struct GcAsyncLds {  // one wave's rows
     unsigned flag[GC_WAVE];
     int first[GC_WAVE];
     long long start[GC_WAVE];
     unsigned c6[GC_WAVE];
     int cv[GC_WAVE];
+#if GC_KILL_DEFER
+    int winv[GC_KILL_BUF];  // the wave's light winners whose hub kill flags are not raised yet
+    int winc[GC_KILL_BUF];  //   and their colours
+    int nwin;               //   (wave-uniform count)
+#endif
 };
+
+// A light winner flags the hubs listing it that propose its colour (gc_hubs.hip): every
+// entry of buf[0, nb) / col[0, nb), the wave walking their hub lists as one flat range.
+__device__ void gc_async_kill_rows(GDev& g, const int* buf, const int* col, int nb, GcAsyncLds& s) {
+    const int lane = gc_lane();
+    for (int c0 = 0; c0 < nb; c0 += GC_WAVE) {
+        const int v = c0 + lane < nb ? buf[c0 + lane] : -1;
+        const int cv = c0 + lane < nb ? col[c0 + lane] : 0;
+        int dh = 0;
+        long long hs = 0;
+        if (v >= 0) {
+            hs = g.hin_rp[v];
+            dh = (int)(g.hin_rp[v + 1] - hs);
+        }
+        gc_wave_sync();
+        s.start[lane] = hs;
+        s.cv[lane] = cv;
+        const int hincl = gc_wave_incl_scan(dh);
+        const int hexcl = hincl - dh;
+        const int htotal = __shfl(hincl, GC_WAVE - 1, GC_WAVE);
+        gc_wave_sync();
+        gc_chunk_edges(
+            g.hin_col, s.start, hexcl, htotal, [&](int hx) { return g.hk[hx]; },  // candidate field: fixed
+            [&](int o, int hx, unsigned kh) {
+                if ((kh >> 2) != (unsigned)s.cv[o]) return;
+                if (!gc_ald32(g.hkill + hx)) gc_ast32(g.hkill + hx, 1u);
+            });
+        gc_wave_sync();
+    }
+}
+#if GC_KILL_DEFER
+// raise the kill flags of the buffered winners (the buffer is LDS: copied to registers first)
+__device__ __forceinline__ void gc_async_kill_flush(GDev& g, GcAsyncLds& s) {
+    const int nb = s.nwin;
+    if (nb == 0) return;
+    gc_async_kill_rows(g, s.winv, s.winc, nb, s);
+    gc_wave_sync();
+    if (gc_lane() == 0) s.nwin = 0;
+    gc_wave_sync();
+}
+#endif
 
 // One pass of a wave over its pending lights lst[0, np) (edge-balanced wave chunks, as
 // gc_jp_sweep); the still-undecided ones are compacted to the front of lst (a chunk is
@@ -1436,21 +1600,58 @@ struct GcAsyncLds {  // one wave's rows
 // cursor entry -- its first pending entry at the last scan -- is still undecided with its
 // candidate is kept without rescanning the rest of its range (an IN entry further on is seen
 // at the next full pass; the decisions are the same).
-__device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull& decided, int pass) {
+// GC_LIGHT_LDS (round 6): a wave whose slice holds at most GC_LL_CAP lights keeps their words
+// (vertex, cursor, low-row length, own byte, row start, candidate) in LDS after its first pass,
+// so a later pass starts at its row reads: one LDS read instead of the list entry and the
+// vertex's words, two dependent trips per 64-light chunk.
+#ifndef GC_LIGHT_LDS
+#define GC_LIGHT_LDS 1
+#endif
+#define GC_LL_CAP 256
+struct GcLightLds {
+    int v[GC_LL_CAP], lc[GC_LL_CAP], nl[GC_LL_CAP], cv[GC_LL_CAP];
+    unsigned kv[GC_LL_CAP];
+    long long rs[GC_LL_CAP];
+};
+// SRC = 1: the lights come from ll (else from lst and the vertex arrays); DST = 1: the
+// survivors are compacted into ll (else into lst)
+template <int SRC = 0, int DST = 0>
+__device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull& decided, int pass,
+                                   GcLightLds* ll = nullptr) {
     const int lane = gc_lane();
     const unsigned char* k8 = g.k8;
     const bool full_pass = g.a_watch <= 0 || pass % g.a_watch == 0;
     int nw = 0;
     for (int c0 = 0; c0 < np; c0 += GC_WAVE) {
         const int idx = c0 + lane;
-        int v = idx < np ? lst[idx] : -1;
+        int v, lc, nl, cvv;
+        unsigned kv, cv6;
+        long long rs;
+        if (SRC) {
+            const bool in = idx < np;
+            v = in ? ll->v[idx] : -1;
+            lc = in ? ll->lc[idx] : 0;
+            nl = in ? ll->nl[idx] : 0;
+            kv = in ? ll->kv[idx] : 0xFFu;
+            rs = in ? ll->rs[idx] : 0;
+            cvv = in ? ll->cv[idx] : 0;
+            cv6 = in ? gc_k8_cand(kv) : 0x100u;
+        } else {
+        v = idx < np ? lst[idx] : -1;
         if (v >= g.n) v = -1;  // never expected (a list entry out of range): skipped, not read through
-        const int lc = v >= 0 ? g.lcur[v] : 0;
-        const int nl = v >= 0 ? g.nlow[v] : 0;
-        const unsigned kv = v >= 0 ? (unsigned)k8[v] : 0xFFu;  // own byte: only this wave changes it
-        const long long rs = v >= 0 ? g.rp[v] : 0;
-        const unsigned cv6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
-        const int cvv = (v >= 0 && cv6 == GC_K8_BIG) ? g.cand[v] : (int)cv6;
+        lc = v >= 0 ? g.lcur[v] : 0;
+        nl = v >= 0 ? g.nlow[v] : 0;
+        kv = v >= 0 ? (unsigned)k8[v] : 0xFFu;  // own byte: only this wave changes it
+        rs = v >= 0 ? g.rp[v] : 0;
+#if GC_HOIST_HIN
+        const int cb0 = v >= 0 ? g.cand[v] : 0;
+        cv6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        cvv = (v >= 0 && cv6 == GC_K8_BIG) ? cb0 : (int)cv6;
+#else
+        cv6 = v >= 0 ? gc_k8_cand(kv) : 0x100u;
+        cvv = (v >= 0 && cv6 == GC_K8_BIG) ? g.cand[v] : (int)cv6;
+#endif
+        }
         bool held = false;
         if (!full_pass && v >= 0 && lc < nl) {
             const int u0 = g.col[rs + lc];
@@ -1476,18 +1677,60 @@ __device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull
         gc_wave_sync();
         unsigned nst = GC_JP_UND;
         bool pend = false;
+        int nlc = lc;
         if (v >= 0) {
             const unsigned f = s.flag[lane];
             if (f & 1u) nst = GC_JP_OUT;
             else if (f & 2u) pend = true;
             else nst = GC_JP_IN;
-            if (pend) g.lcur[v] = lc + s.first[lane];
-            else gc_ast8(g.k8 + v, (kv & ~3u) | nst);
+            if (pend) {
+                nlc = lc + s.first[lane];
+                g.lcur[v] = nlc;  // (host sweeps resume from it after a give-up)
+            } else {
+                gc_ast8(g.k8 + v, (kv & ~3u) | nst);
+            }
         }
         const ull pm = __ballot(pend);
-        if (pend) lst[nw + __popcll(pm & gc_lanemask_lt())] = v;
+        if (pend) {
+            const int k = nw + __popcll(pm & gc_lanemask_lt());  // <= idx: survivors only move down
+            if (DST) {
+                ll->v[k] = v;
+                ll->lc[k] = nlc;
+                ll->nl[k] = nl;
+                ll->kv[k] = kv;
+                ll->rs[k] = rs;
+                ll->cv[k] = cvv;
+            } else {
+                lst[k] = v;
+            }
+        }
         nw += __popcll(pm);
         decided += (ull)__popcll(__ballot(v >= 0 && !pend));
+#if GC_KILL_DEFER
+        // the wave's winners are buffered; their kill flags are raised in one flat walk when the
+        // buffer fills and before the wave publishes its decided lights (only the hub phase
+        // reads them, and it starts after every light's publication): a pass no longer waits
+        // for each chunk's three dependent kill trips
+        if (g.hub_w) {
+            const bool iw = v >= 0 && nst == GC_JP_IN;
+            const ull wmk = __ballot(iw);
+            const int nwk = __popcll(wmk);
+            if (nwk) {
+                const int mycv = s.cv[lane];  // (a flush rewrites s.cv)
+                if (s.nwin + nwk > GC_KILL_BUF) gc_async_kill_flush(g, s);
+                const int b = s.nwin;
+                gc_wave_sync();
+                if (iw) {
+                    const int k = b + __popcll(wmk & gc_lanemask_lt());
+                    s.winv[k] = v;
+                    s.winc[k] = mycv;
+                }
+                gc_wave_sync();
+                if (lane == 0) s.nwin = b + nwk;
+                gc_wave_sync();
+            }
+        }
+#else
         if (g.hub_w) {  // a light winner flags the hubs listing it that propose its colour
             int dh = 0;
             long long hs = 0;
@@ -1508,6 +1751,7 @@ __device__ int gc_async_light_pass(GDev& g, int* lst, int np, GcAsyncLds& s, ull
                     if (!gc_ald32(g.hkill + hx)) gc_ast32(g.hkill + hx, 1u);
                 });
         }
+#endif
         gc_wave_sync();
     }
     return nw;
@@ -1689,6 +1933,169 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 }
 
 
+// The hub phase of a wave whose slice holds at most 64 hubs (every small round: the slices
+// are GC_HUB_NG hubs), with each hub's words kept in ITS lane's registers across passes
+// (round 6; GC_HUB_REG, the default).  gc_async_hub_pass reloads a hub's words -- the list
+// entry, then k8 / cand / hid, then hkill / hlow_rp / hpc / hcur / hlen -- in every pass:
+// three dependent trips before each pass's row scan, ~12 passes a round.  Here they are
+// loaded once, and a hub whose scan stopped at an undecided same-candidate entry (the
+// blocker, its cursor) WATCHES that one entry: a later pass gathers the blockers' hub words
+// for all of the wave's pending hubs in one trip, and only a hub whose blocker has decided
+// resumes its scan (from the blocker, re-read, as gc_async_hub_pass resumes from the cursor).
+// The decisions are the resumable scan's (same cursor, same prefix, same flags); the cursor
+// and prefix words are stored as that pass stores them, so host sweeps after a give-up
+// resume from them.  Returns the hubs still pending when the wave stops (spilled by it).
+#ifndef GC_HUB_REG
+#define GC_HUB_REG 0  // measured: R-MAT-24 -0.5..-1 ms, R-MAT-26 -1.5 ms against the reloading pass (profiles/r06/q)
+#endif
+#ifndef GC_HUB_WATCH
+#define GC_HUB_WATCH 1
+#endif
+__device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, int par, ull t0, long long budget,
+                                 int* spill, ull* spill_cnt, ull* hpass_out, int* s_own) {
+    constexpr int GS = GC_WAVE / GC_HUB_NG;
+    const int lane = gc_lane();
+    const int grp = lane / GS, li = lane % GS;
+    const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
+    // this lane's hub (lane j = entry j of the slice)
+    const int v = lane < nh0 ? src[lane] : -1;
+    const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte
+    const int cb = v >= 0 ? g.cand[v] : 0;
+    const int x = v >= 0 ? g.hid[v] : -1;  // every heavy proposer is a hub while the hub JP is on
+    const int cv = gc_k8_cand(kv) == GC_K8_BIG ? cb : (int)gc_k8_cand(kv);
+    bool kill = false;
+    long long base = 0;
+    int full = 0, pos = 0, hstart = 0;
+    bool first = false;
+    if (x >= 0) {
+        kill = gc_ald32(g.hkill + x) != 0u;  // final in the hub phase
+        base = g.hlow_rp[x];
+        full = (int)(g.hlow_rp[x + 1] - base);
+        const int cursor = g.hpc[x];
+        first = g.hcur[x] == 0;
+        hstart = g.hlen[x];
+        pos = first ? hstart : cursor;
+    }
+    int ublk = -1;            // the watched blocker (hub index) once a scan stopped at one
+    bool pend = x >= 0;       // undecided (entries that are no hub are dropped, as in gc_async_hub_pass)
+    ull hpass = 0;
+    int idle = 0;
+    for (;;) {
+        ++hpass;
+        // the watched blockers of every pending hub in one trip: still undecided with the
+        // hub's candidate -> the hub stays blocked without reading its row
+        bool scan = pend;
+        if (GC_HUB_WATCH && pend && !kill && ublk >= 0) {
+            const unsigned kb = gc_ald32(g.hk + ublk);
+            if (kb != GC_HK_COLOURED && gc_jp_flag_h(g, ublk, kb, 0u, cv) == 2u) scan = false;
+        }
+        const ull sm = __ballot(scan);
+        const int rk = __popcll(sm & gc_lanemask_lt());  // this lane's rank among the scanning hubs
+        const int ns = __popcll(sm);
+        int decided = 0;
+        gc_wave_sync();
+        if (scan) s_own[rk] = lane;  // rank -> owner lane (LDS row of this wave)
+        gc_wave_sync();
+        for (int j0 = 0; j0 < ns; j0 += GC_HUB_NG) {
+            // group grp takes the scanning hub of rank j0 + grp (its owner lane ol)
+            const int want = j0 + grp;
+            const bool has = want < ns;
+            const int ol = has ? s_own[want] : 0;
+            const int hv = __shfl(v, ol, GC_WAVE);
+            const int hcv = __shfl(cv, ol, GC_WAVE);
+            const int hkill = __shfl((int)kill, ol, GC_WAVE);
+            const long long hbase = __shfl(base, ol, GC_WAVE);
+            const int hfull = __shfl(full, ol, GC_WAVE);
+            const int hpos = __shfl(pos, ol, GC_WAVE);
+            const int hfirst = __shfl((int)first, ol, GC_WAVE);
+            (void)hv;
+            const bool act = has && !hkill;  // group-uniform
+            int p = hpos;
+            bool out = false, prefix = act && hfirst;
+            int block = -1, nstart = hfull, ub = -1;
+            const int* __restrict__ row = g.hlow_col + hbase;
+            for (;;) {
+                const bool run = act && !out && block < 0 && p < hfull;
+                if (!__ballot(run)) break;
+                int u[GC_HUB_UNR];
+#pragma unroll
+                for (int k = 0; k < GC_HUB_UNR; ++k) {
+                    const int e = p + k * GS + li;
+                    u[k] = (run && e < hfull) ? row[e] : -1;
+                }
+                unsigned ku[GC_HUB_UNR];
+#pragma unroll
+                for (int k = 0; k < GC_HUB_UNR; ++k) ku[k] = u[k] >= 0 ? gc_ald32(g.hk + u[k]) : GC_HK_COLOURED;
+#pragma unroll
+                for (int k = 0; k < GC_HUB_UNR; ++k) {
+                    const unsigned fl = ku[k] != GC_HK_COLOURED ? gc_jp_flag_h(g, u[k], ku[k], 0u, hcv) : 0u;
+                    if (__ballot(fl == 1u) & gmask) out = true;
+                    const ull mb = __ballot(fl == 2u) & gmask;
+                    const int bl = mb ? __ffsll((long long)mb) - 1 : lane;
+                    const int bu = __shfl(u[k], bl, GC_WAVE);  // every lane takes part
+                    if (mb && block < 0) {
+                        block = p + k * GS + (bl - grp * GS);
+                        ub = bu;
+                    }
+                    const ull ml = __ballot(u[k] >= 0 && ku[k] != GC_HK_COLOURED) & gmask;
+                    if (prefix && ml) {  // first non-coloured entry: the end of the coloured prefix
+                        nstart = p + k * GS + __builtin_ctzll(ml >> (grp * GS));
+                        prefix = false;
+                    }
+                }
+                if (run) p += GC_HUB_UNR * GS;
+            }
+            const unsigned f = hkill ? 1u : (out ? 1u : (block >= 0 ? 2u : 0u));
+            // back to the owner lanes: lane r of rank j0 + q reads group q's leader
+            const bool mine = scan && rk >= j0 && rk < j0 + GC_HUB_NG;
+            const int src_l = mine ? (rk - j0) * GS : lane;
+            const unsigned rf = (unsigned)__shfl((int)f, src_l, GC_WAVE);
+            const int rblock = __shfl(block, src_l, GC_WAVE);
+            const int rub = __shfl(ub, src_l, GC_WAVE);
+            const int rns = __shfl(nstart, src_l, GC_WAVE);
+            const int ract = __shfl((int)act, src_l, GC_WAVE);
+            if (mine) {
+                if (ract) {
+                    if (first) {
+                        g.hcur[x] = 1;
+                        if (rns > hstart) g.hlen[x] = rns;
+                        first = false;
+                    }
+                    if (rf == 2u) {
+                        g.hpc[x] = rblock;
+                        pos = rblock;
+                        ublk = rub;
+                    }
+                }
+                if (rf != 2u) {
+                    const unsigned st = (rf & 1u) ? GC_JP_OUT : GC_JP_IN;
+                    gc_ast8(g.k8 + v, (kv & ~3u) | st);
+                    gc_ast32(g.hk + x, gc_hk((unsigned)cv, st));
+                    pend = false;
+                    decided = 1;
+                }
+            }
+        }
+        if (!__ballot(pend)) break;
+        if (gc_async_stop(c, par, t0, budget)) {
+            const ull pm = __ballot(pend);
+            ull b = 0;
+            if (lane == 0) b = atomicAdd(spill_cnt, (ull)__popcll(pm));
+            b = __shfl(b, 0, GC_WAVE);
+            if (pend) spill[b + __popcll(pm & gc_lanemask_lt())] = v;
+            *hpass_out = hpass;
+            return __popcll(pm);
+        }
+        if (!__ballot(decided)) {
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+        } else {
+            idle = 0;
+        }
+    }
+    *hpass_out = hpass;
+    return 0;
+}
+
 // The launch after sweep S (k_resolve = 0, or the last host sweep): reads slot S % 3,
 // spills to slot (S + 1) % 3 (cleared by sweep S), clears slot (S + 2) % 3 and sets
 // tail_last = S + 1, the slot the commit checks -- exactly what a tail that ran one more
@@ -1752,18 +2159,53 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         int* lst = L.undL[in] + la;
         ull decided = 0;
         int idle = 0, lpass = 0;
+#if GC_KILL_DEFER
+        if (gc_lane() == 0) s_w[w].nwin = 0;
+        gc_wave_sync();
+#endif
+#if GC_LIGHT_LDS
+        __shared__ GcLightLds s_ll[GC_WAVES_PER_BLOCK];
+        const bool lds = np <= GC_LL_CAP;
+#else
+        const bool lds = false;
+        (void)lds;
+#endif
         while (np > 0) {
             const int before = np;
+#if GC_LIGHT_LDS
+            if (lds) np = lpass == 0 ? gc_async_light_pass<0, 1>(g, lst, np, s_w[w], decided, ++lpass, &s_ll[w])
+                                     : gc_async_light_pass<1, 1>(g, lst, np, s_w[w], decided, ++lpass, &s_ll[w]);
+            else
+#endif
             np = gc_async_light_pass(g, lst, np, s_w[w], decided, ++lpass);
             if (np == 0) break;
             if ((stop = gc_async_stop(c, par, t0, budget))) break;
             if (np == before) {
+#if GC_KILL_DEFER
+                // waiting on other waves: raise the buffered winners' kill flags meanwhile
+                if (g.hub_w && s_w[w].nwin > 0) {
+                    gc_async_kill_flush(g, s_w[w]);
+                    continue;
+                }
+#endif
                 if (++idle > 2) __builtin_amdgcn_s_sleep(2);
             } else {
                 idle = 0;
             }
         }
-        if (stop) gc_async_spill(lst, np, L.undL[out], &c->und_cnt[out]);
+        if (stop) {
+#if GC_LIGHT_LDS
+            if (lds && lpass > 0) {  // the survivors are in LDS
+                gc_wave_sync();
+                for (int i = gc_lane(); i < np; i += GC_WAVE) lst[i] = s_ll[w].v[i];
+                gc_wave_sync();
+            }
+#endif
+            gc_async_spill(lst, np, L.undL[out], &c->und_cnt[out]);
+        }
+#if GC_KILL_DEFER
+        if (g.hub_w) gc_async_kill_flush(g, s_w[w]);  // before the publication below
+#endif
 #ifdef GC_A_PROF
         if (aprof && lpass > 0) {
             atomicMax(aprof + 0, wall_clock64() - t0);
@@ -1814,6 +2256,19 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         gc_async_spill(src, nh0, L.undH[out], &c->undh_cnt[out]);
         return;
     }
+    if (GC_HUB_REG && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
+        ull hp = 0;
+        gc_async_hubs_reg(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp, s_w[w].first);
+#ifdef GC_A_PROF
+        if (aprof) {
+            atomicMax(aprof + 2, wall_clock64() - t0);
+            atomicMax(aprof + 4, hp);
+            atomicAdd(aprof + 10, hp);
+            atomicMax(aprof + 11, (ull)nh0);
+        }
+#endif
+        return;
+    }
     int* hl = L.undH[z] + ha;
     for (int i = gc_lane(); i < nh0; i += GC_WAVE) hl[i] = src[i];
     gc_wave_sync();
@@ -1861,6 +2316,17 @@ __device__ __forceinline__ void gc_dbg(DevCtl* c, long long code, long long a, l
     }
 }
 
+// big-round push (k_commit / k_commit_big, mark mode): in-neighbour x of a winner joins the
+// next frontier.  GC_MARK_CHECK (round 6): only when its claim bit is clear -- coloured or
+// already-frontier vertices (most of a big round's in-neighbours) need no mark, and a read of
+// the 1/8-byte-per-vertex claim bitmap is cheaper than a random partial-line byte store
+#ifndef GC_MARK_CHECK
+#define GC_MARK_CHECK 1
+#endif
+__device__ __forceinline__ void gc_mark(const GDev& g, int x) {
+    if (GC_MARK_CHECK && ((g.inF[x >> 5] >> (x & 31)) & 1u)) return;
+    g.mark[x] = 1;
+}
 __device__ __forceinline__ bool gc_claim(unsigned* inF, int x) {
     const unsigned bit = 1u << (x & 31);
     if (inF[x >> 5] & bit) return false;
@@ -1875,6 +2341,9 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
 #endif
 #ifndef GC_PREFETCH_ROW
 #define GC_PREFETCH_ROW 1
+#endif
+#ifndef GC_COMMIT_HUB_LANES
+#define GC_COMMIT_HUB_LANES 1  // k_commit: a run of heavy entries per wave, one per lane (round 6)
 #endif
 
 
@@ -2130,14 +2599,53 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             int x = 0;
             if (e < te) {
                 x = g.tcol[e];
-                if (mark) g.mark[x] = 1;
+                if (mark) gc_mark(g, x);
                 else claim = gc_claim(g.inF, x);
             }
             push(claim, x);
         }
     };
-    // hubs on: a wave per hub (in-rows past bigrow are deferred to k_commit_big)
-    if (g.hub_w) {
+    // hubs on: each wave takes a run of up to 64 consecutive heavy entries, one per lane, so a
+    // whole run's list and state words are loaded in one trip each (round 6, GC_COMMIT_HUB_LANES:
+    // a wave per hub walked ~60 hubs one after another in a big round -- two dependent trips
+    // each, ~120 trips per wave); its winners' rows are then walked by the whole wave, one
+    // winner at a time (in-rows past bigrow are deferred to k_commit_big)
+    if (g.hub_w && GC_COMMIT_HUB_LANES) {
+        const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
+        const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
+        const long long per = std::min<long long>(GC_WAVE, std::max<long long>(1, (hcnt + W - 1) / W));
+        for (long long i0 = wid * per; i0 < hcnt; i0 += W * per) {
+            const long long i = i0 + lane;
+            const int v = (lane < per && i < hcnt) ? hlist[i] : -1;
+            const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;
+            const unsigned js = v >= 0 ? gc_k8_state(kv) : (unsigned)GC_JP_UND;
+            const bool win = js == GC_JP_IN;
+            int cc = 0;
+            bool walk = false;
+            if (win) {
+                const int cb = g.cand[v];
+                const long long ts = g.trp[v], te = g.trp[v + 1];
+                const long long hn = g.hin_rp[v + 1] - g.hin_rp[v];
+                cc = gc_k8_cand(kv) == GC_K8_BIG ? cb : (int)gc_k8_cand(kv);
+                const long long tl = te - ts;
+                walk = tl + hn <= g.bigrow;
+                gc_commit_colour(g, v, cc);
+                if (want_cround) g.cround[v] = round;
+                lmaxc = cc > lmaxc ? cc : lmaxc;
+                lacc++;
+                lsum += (ull)tl;
+            }
+            gc_wave_append(win && !walk, v, L.bigw, &c->bigw_cnt);  // the whole grid walks it
+            push(js == GC_JP_OUT && !big, v);                       // losers stay
+            for (ull wm = __ballot(walk); wm; wm &= wm - 1) {
+                const int l = __ffsll((long long)wm) - 1;
+                const int wv = __shfl(v, l, GC_WAVE);
+                const int wc = __shfl(cc, l, GC_WAVE);
+                gc_hub_mark_row(g, wv, wc, lane, GC_WAVE);  // gc_hubs.hip
+                if (mark || !big) walk_claims(g.trp[wv], g.trp[wv + 1], lane, GC_WAVE);
+            }
+        }
+    } else if (g.hub_w) {  // a wave per hub (round 5)
         for (long long i = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; i < hcnt;
              i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
             const int v = hlist[i];
@@ -2214,6 +2722,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         // one memory trip instead of two); fused: no heavy vertex, so no degree needed
         const int d = (v >= 0 && !FUSE) ? g.deg[v] : 0;
         const unsigned kv0 = v >= 0 ? (unsigned)g.k8[v] : 0u;
+#if GC_HOIST_HIN
+        const int cb0 = v >= 0 ? g.cand[v] : 0;
+        const long long hs0 = (v >= 0 && g.hbits_w) ? g.hin_rp[v] : 0;
+        const long long he0 = (v >= 0 && g.hbits_w) ? g.hin_rp[v + 1] : 0;
+#endif
 #if GC_PREFETCH_ROW
         const long long ts0 = v >= 0 ? g.trp[v] : 0, te0 = v >= 0 ? g.trp[v + 1] : 0;
 #else
@@ -2227,7 +2740,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         int din = 0, cc = 0;
         long long tstart = 0;
         if (acc) {
+#if GC_HOIST_HIN
+            cc = gc_k8_cand(kv) == GC_K8_BIG ? cb0 : (int)gc_k8_cand(kv);
+#else
             cc = gc_k8_cand(kv) == GC_K8_BIG ? g.cand[v] : (int)gc_k8_cand(kv);
+#endif
             if (FUSE) gc_commit_colour_keep(g, v, cc);
             else gc_commit_colour(g, v, cc);
             if (want_cround) g.cround[v] = round;
@@ -2269,7 +2786,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
             for (int k = 0; k < GC_CSLOTS; ++k) {
                 claim[k] = false;
                 if (ok[k]) {
-                    if (mark) g.mark[x[k]] = 1;
+                    if (mark) gc_mark(g, x[k]);
                     else if (FUSE && g.claim_direct) claim[k] = gc_claim_direct(g.inF, x[k]);
                     else claim[k] = gc_claim(g.inF, x[k]);
                 }
@@ -2280,8 +2797,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         if (g.hbits_w) {  // push the winners' colours into the hubs that list them (gc_hubs.hip)
             int dh = 0;
             if (acc) {
+#if GC_HOIST_HIN
+                tstart = hs0;
+                dh = (int)(he0 - hs0);
+#else
                 tstart = g.hin_rp[v];
                 dh = (int)(g.hin_rp[v + 1] - tstart);
+#endif
             }
             gc_wave_sync();
             s_start[w][lane] = tstart;
@@ -2399,7 +2921,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
                     gc_hub_mark(g, g.hin_col[s_hs[k] + off], s_cc[k]);
                 } else {
                     xv = g.tcol[s_ts[k] + (off - s_hl[k])];
-                    if (mark) g.mark[xv] = 1;
+                    if (mark) gc_mark(g, xv);
                     else claim = gc_claim(g.inF, xv);
                 }
             }

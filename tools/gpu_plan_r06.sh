@@ -74,6 +74,36 @@ case ${1:-} in
                  "file:tests/test_gpu_fullsize.py:engine_against_multicore~or~north_star_rmat26") ;;
   l) exec_steps=("abl:rmat24:3:2:base=-,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so,ng2=variants/ng2/libgcolor.so,ng8u4=variants/ng8u4/libgcolor.so"
                  "abl:rmat26:2:2:base=-,ng8=variants/ng8/libgcolor.so,ng16=variants/ng16/libgcolor.so,ng8u4=variants/ng8u4/libgcolor.so") ;;
+  # o: the hub phase's words in registers with a watched blocker (GC_HUB_REG), heavy runs a lane
+  #    each in k_commit / k_propose_block, the async lights' kill flags in batches: parity, then
+  #    A/B against all four off (variants/old) and each of the two async changes off
+  o) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_core.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,old=variants/old/libgcolor.so,noreg=variants/noreg/libgcolor.so,nodefer=variants/nodefer/libgcolor.so,nohint=variants/nohint/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,old=variants/old/libgcolor.so") ;;
+  # p: session o's build with the hub phase's owner lanes from LDS and the kill flags raised while
+  #    a wave waits: parity, then A/B on R-MAT-24 and R-MAT-26
+  p) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,old=variants/old/libgcolor.so,noreg=variants/noreg/libgcolor.so,nodefer=variants/nodefer/libgcolor.so,nohoist=variants/nohoist/libgcolor.so"
+                 "abl:rmat26:2:2:base=-,old=variants/old/libgcolor.so,noreg=variants/noreg/libgcolor.so,nodefer=variants/nodefer/libgcolor.so") ;;
+  # q: + the async lights' words in LDS (GC_LIGHT_LDS) and check-before-mark (GC_MARK_CHECK): the
+  #    parity files, then A/B against all off (variants/old) and each change off
+  q) V="old=variants/old/libgcolor.so,noreg=variants/noreg/libgcolor.so,nodefer=variants/nodefer/libgcolor.so"
+     V="$V,nohoist=variants/nohoist/libgcolor.so,nolds=variants/nolds/libgcolor.so,nomark=variants/nomark/libgcolor.so"
+     exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_variant_b.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,$V"
+                 "abl:rmat26:2:1:base=-,$V") ;;
+  # r: the defaults q chose (registers and batched kills off, hoist off); A/B of the hub phase in
+  #    registers with / without the watched blocker, the heavy runs a lane each off, the hint off,
+  #    the lights' LDS words off; then the per-round cost of the new default build
+  r) V="reg=variants/reg/libgcolor.so,regnw=variants/regnw/libgcolor.so,nolanes=variants/nolanes/libgcolor.so"
+     V="$V,nohint=variants/nohint/libgcolor.so,nolds=variants/nolds/libgcolor.so"
+     exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_core.py"
+                 "abl:rmat24:3:2:base=-,$V"
+                 "abl:rmat26:2:1:base=-,$V"
+                 rounds:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
