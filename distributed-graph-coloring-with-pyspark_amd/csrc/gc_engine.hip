@@ -425,7 +425,7 @@ struct Run {
         if (tail && async_grid > 0) {  // the rest of the JP chain: one asynchronous launch
             kt.begin(GC_K_SWEEP);
             if (core_ready && core_f >= core_min_f) gcl_hub_core(d, L, nsweeps, async_par, s);  // decides the hubs when it can
-            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s);
+            gcl_sweep_async(d, L, nsweeps, async_par, async_budget, async_grid, s, resort_hint ? 1 : 0);
             async_par ^= 1;
             kt.end();
         } else if (tail && loop_grid > 0) {  // the middle of the JP chain: one resident-grid launch

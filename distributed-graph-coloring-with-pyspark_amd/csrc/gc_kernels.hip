@@ -1780,11 +1780,12 @@ __device__ ull gc_aprof[GC_A_PROF_ROUNDS][GC_A_PROF_K];
 #ifndef GC_HUB_PREFETCH
 #define GC_HUB_PREFETCH 1
 #endif
+template <int NG = GC_HUB_NG>
 __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
-    constexpr int GS = GC_WAVE / GC_HUB_NG;
+    constexpr int GS = GC_WAVE / NG;
     const int lane = gc_lane();
     const int grp = lane / GS, li = lane % GS;
-    const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
+    const ull gmask = GS >= GC_WAVE ? ~0ull : ((1ull << (GS % GC_WAVE)) - 1ull) << (grp * GS);
     int nw = 0;
 #if GC_HUB_PREFETCH
     for (int b0 = 0; b0 < nh; b0 += GC_WAVE) {
@@ -1804,7 +1805,7 @@ __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
         phc0 = g.hcur[px];
         phs = g.hlen[px];
     }
-    for (int j0 = 0; j0 < bn; j0 += GC_HUB_NG) {
+    for (int j0 = 0; j0 < bn; j0 += NG) {
         const int j = j0 + grp;
         const bool has = j < bn;
         const int jj = has ? j : 0;  // every lane takes part in every shuffle
@@ -1822,7 +1823,7 @@ __device__ int gc_async_hub_pass(GDev& g, int* hl, int nh) {
         const int hc0 = __shfl(phc0, jj, GC_WAVE);
         const int hstart = __shfl(phs, jj, GC_WAVE);
 #else
-    for (int j0 = 0; j0 < nh; j0 += GC_HUB_NG) {
+    for (int j0 = 0; j0 < nh; j0 += NG) {
         const int j = j0 + grp;
         const int v = j < nh ? hl[j] : -1;
         const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte
@@ -1945,11 +1946,14 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 // The decisions are the resumable scan's (same cursor, same prefix, same flags); the cursor
 // and prefix words are stored as that pass stores them, so host sweeps after a give-up
 // resume from them.  Returns the hubs still pending when the wave stops (spilled by it).
+#ifndef GC_HUB_WIDE
+#define GC_HUB_WIDE 1
+#endif
 #ifndef GC_HUB_REG
-#define GC_HUB_REG 0  // measured: R-MAT-24 -0.5..-1 ms, R-MAT-26 -1.5 ms against the reloading pass (profiles/r06/q)
+#define GC_HUB_REG 1  // R-MAT-24 146.2 -> 143.1 ms, R-MAT-26 383.4 -> 379.3 without the watch (profiles/r06/r)
 #endif
 #ifndef GC_HUB_WATCH
-#define GC_HUB_WATCH 1
+#define GC_HUB_WATCH 0  // the watched blocker: slower (a blocker that decided costs a trip more; profiles/r06/r)
 #endif
 __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, int par, ull t0, long long budget,
                                  int* spill, ull* spill_cnt, ull* hpass_out, int* s_own) {
@@ -2103,7 +2107,8 @@ __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, in
 // here); `budget` is in wall-clock ticks.  (Round 3's variant that also made the round's
 // first sweep, in place of k_resolve, measured R-MAT-24 172.7 -> 190.4 ms in round 4,
 // profiles/r04/c: removed.)
-__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget) {
+__global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int S, int par, long long budget,
+                                                          int lds_lights) {
     DevCtl* c = g.ctl;
     if (budget < 0) {  // residency probe (gcl_sweep_async_resident)
         gc_residency_probe(c);
@@ -2164,9 +2169,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         gc_wave_sync();
 #endif
 #if GC_LIGHT_LDS
-        __shared__ GcLightLds s_ll[GC_WAVES_PER_BLOCK];
-        const bool lds = np <= GC_LL_CAP;
+        extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+        GcLightLds* s_ll = reinterpret_cast<GcLightLds*>(s_dyn);
+        const bool lds = lds_lights && np <= GC_LL_CAP;
 #else
+        (void)lds_lights;
         const bool lds = false;
         (void)lds;
 #endif
@@ -2225,7 +2232,12 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     if (ch == 0) return;
     // hubs: the wave's slice (GC_HUB_NG at least), copied to slot z (the source lists stay
     // intact: the commit walks L.heavy) and compacted there
-    const long long per = std::max<long long>(GC_HUB_NG, (ch + W - 1) / W);
+    // GC_HUB_WIDE (round 6): while the hubs fit one per wave (every small round), each wave
+    // takes ONE hub and scans its row with all 64 lanes (512 entries a step): a round's first
+    // evaluation walks ~280 entries past the coloured prefix (coloured hubs interleave with
+    // the uncoloured ones in rank order), 4-5 steps for a 16-lane group, one for a wave
+    const bool wide = GC_HUB_WIDE && ch <= W;
+    const long long per = wide ? 1ll : std::max<long long>(GC_HUB_NG, (ch + W - 1) / W);
     const long long ha = wid * per;
     if (ha >= ch) return;
     const int nh0 = (int)(std::min(ch, ha + per) - ha);
@@ -2256,7 +2268,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         gc_async_spill(src, nh0, L.undH[out], &c->undh_cnt[out]);
         return;
     }
-    if (GC_HUB_REG && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
+    if (GC_HUB_REG && !wide && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
         ull hp = 0;
         gc_async_hubs_reg(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp, s_w[w].first);
 #ifdef GC_A_PROF
@@ -2281,7 +2293,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
 #ifdef GC_A_PROF
         ++hpass;
 #endif
-        nh = gc_async_hub_pass(g, hl, nh);
+        nh = wide ? gc_async_hub_pass<1>(g, hl, nh) : gc_async_hub_pass<GC_HUB_NG>(g, hl, nh);
         if (nh == 0) break;
         if ((stop = gc_async_stop(c, par, t0, budget))) break;
         if (nh == before) {
@@ -3869,8 +3881,12 @@ void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s) {
     else if (g.tail_nw == 8) GC_LAUNCH(k_sweep_tail<8>, dim3(1), dim3(8 * GC_WAVE), 0, s, g, L, S);
     else GC_LAUNCH(k_sweep_tail<4>, dim3(1), dim3(4 * GC_WAVE), 0, s, g, L, S);
 }
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s) {
-    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, S, par, budget);
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
+                     int lds_lights) {
+    // the lights' LDS rows (GC_LIGHT_LDS) as dynamic LDS, only where the host asks for them
+    // (big rounds): 28 KB more per workgroup slowed the small rounds' launches (profiles/r06/r)
+    const size_t dyn = (GC_LIGHT_LDS && lds_lights) ? sizeof(GcLightLds) * GC_WAVES_PER_BLOCK : 0;
+    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), dyn, s, g, L, S, par, budget, dyn ? 1 : 0);
 }
 int gc_resident_blocks_per_cu(const void* fn, int block) {
     int occ = 0;
@@ -3930,7 +3946,7 @@ int gc_measure_resident(const void* key, gc_graph_ctl_view v, int query, void (*
 }
 static void launch_sweep_async_probe(const GDev& g, int grid, hipStream_t s) {
     GLists L{};
-    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, 0, 0, -1ll);
+    GC_LAUNCH(k_sweep_async, dim3(grid), dim3(GC_BLOCK), 0, s, g, L, 0, 0, -1ll, 0);
 }
 int gcl_sweep_async_resident(const GDev& g, hipStream_t s) {
     return gc_measure_resident((const void*)k_sweep_async, gc_graph_ctl_view{&g, s}, gcl_sweep_async_blocks_per_cu(),

@@ -128,7 +128,8 @@ void gcl_sweep(const GDev& g, const GLists& L, int i, hipStream_t s);
 void gcl_sweep_tail(const GDev& g, const GLists& L, int S, hipStream_t s);  // one-workgroup tail sweeps
 void gcl_sweep_loop(const GDev& g, const GLists& L, int S, int grid, hipStream_t s);  // resident-grid sweep chain
 // asynchronous JP after sweep S on a resident grid (budget in wall-clock ticks; par alternates per launch)
-void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s);
+void gcl_sweep_async(const GDev& g, const GLists& L, int S, int par, long long budget, int grid, hipStream_t s,
+                     int lds_lights = 0);
 int gcl_sweep_async_blocks_per_cu();
 // Workgroups of `block` threads of kernel `fn` that are RESIDENT on a CU at once: the
 // runtime's occupancy answer, bounded by what the kernel's own VGPR count and static LDS allow

@@ -104,6 +104,16 @@ case ${1:-} in
                  "abl:rmat24:3:2:base=-,$V"
                  "abl:rmat26:2:1:base=-,$V"
                  rounds:rmat24) ;;
+  # s: one hub per wave with all 64 lanes while the hubs fit (GC_HUB_WIDE), the hub words in
+  #    registers without the watch (GC_HUB_REG) above that, the lights' LDS rows only in big rounds:
+  #    parity, A/B against each off and against round 5's kernels (variants/r5), per-round cost
+  s) V="nowide=variants/nowide/libgcolor.so,noreg=variants/noreg/libgcolor.so,nolds=variants/nolds/libgcolor.so"
+     V="$V,r5=variants/r5/libgcolor.so"
+     exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_core.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,$V"
+                 "abl:rmat26:2:1:base=-,$V"
+                 rounds:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
