@@ -82,12 +82,26 @@ __host__ __device__ __forceinline__ void gc_st(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Word t of hub x's forbidden-colour bitmap.  GC_HB_WMAJOR (round 6, the default): words are
+// stored word-major -- word t of every hub together -- so the words a round touches (its newest
+// colours' word: the pushes of the round's winners, the hubs' proposals) are a few hundred KB
+// that stay in L2, not one 64-B line per hub out of a 512-B-per-hub array (97 MB on R-MAT-24).
+#ifndef GC_HB_WMAJOR
+#define GC_HB_WMAJOR 1
+#endif
+__device__ __forceinline__ unsigned* gc_hbw(const GDev& g, long long x, long long t) {
+#if GC_HB_WMAJOR
+    return g.hbits + t * g.hb_stride + x;
+#else
+    return g.hbits + x * g.hbits_w + t;
+#endif
+}
 // hubs (gc_hubs.hip): set colour cc in hub x's forbidden-colour bitmap (colours past the
 // bitmap are not tracked: such a hub scans its row when its mex could lie beyond it)
 __device__ __forceinline__ void gc_hub_mark(const GDev& g, int x, int cc) {
     if (g.hseen && !g.hseen[x]) g.hseen[x] = 1;  // shards: the hub now belongs to a frontier
     if (cc >= 32 * g.hbits_w) return;
-    unsigned* p = g.hbits + (long long)x * g.hbits_w + (cc >> 5);
+    unsigned* p = gc_hbw(g, x, cc >> 5);
     const unsigned bit = 1u << (cc & 31);
     if (!(*p & bit)) atomicOr(p, bit);
 }

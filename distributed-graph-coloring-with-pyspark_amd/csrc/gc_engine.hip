@@ -141,6 +141,7 @@ GDev gc_view(const gc_graph* g) {
     d.hin_rp = nullptr;
     d.hin_col = nullptr;
     d.hbits = nullptr;
+    d.hb_stride = 0;
     d.hkill = nullptr;
     d.hlow_rp = nullptr;
     d.hlow_col = nullptr;

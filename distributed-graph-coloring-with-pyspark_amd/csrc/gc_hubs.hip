@@ -439,6 +439,7 @@ int gc_hubs_prepare(gc_graph* g, GDev& d) {
     d.hin_rp = g->hin_rp;
     d.hin_col = g->hin_col;
     d.hbits = g->hbits;
+    d.hb_stride = g->nhub;
     d.hkill = g->hkill;
     d.hlow_rp = g->hlow_rp;
     d.hlow_col = g->hlow_col;

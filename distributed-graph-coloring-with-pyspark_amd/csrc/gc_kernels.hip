@@ -336,9 +336,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
                 const long long hint = c6 == GC_K8_NONE ? 0ll : (c6 == GC_K8_BIG ? (long long)cbv : (long long)c6);
                 hw0 = (int)(hint >> 5);
                 if (hw0 < 0 || hw0 >= hwords) hw0 = 0;
-                const unsigned* hb = g.hbits + (long long)hx * g.hbits_w;
-                hwa = hb[hw0];
-                if (hw0 + 1 < hwords) hwb = hb[hw0 + 1];
+                hwa = *gc_hbw(g, hx, hw0);
+                if (hw0 + 1 < hwords) hwb = *gc_hbw(g, hx, hw0 + 1);
             }
         }
         const int incl = gc_wave_incl_scan(de);
@@ -389,9 +388,8 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
             } else if (hwb != 0xFFFFFFFFu) {
                 mex = 32ll * (hw0 + 1) + __builtin_ctz(~hwb);
             } else {
-                const unsigned* hb = g.hbits + (long long)hx * g.hbits_w;
                 for (int t = hw0 + 2; t < hwords && mex < 0; ++t) {
-                    const unsigned wd = hb[t];
+                    const unsigned wd = *gc_hbw(g, hx, t);
                     if (wd != 0xFFFFFFFFu) mex = 32ll * t + __builtin_ctz(~wd);
                 }
             }
@@ -413,21 +411,21 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
             long long hmex = -1;  // this lane's hub's mex
             for (ull hm = hm0; hm;) {
                 int hl[GC_PH_B];
-                const unsigned* hb[GC_PH_B];
+                int hbx[GC_PH_B];
                 long long mx[GC_PH_B];
 #pragma unroll
                 for (int k = 0; k < GC_PH_B; ++k) {
                     hl[k] = hm ? __ffsll((long long)hm) - 1 : -1;  // wave-uniform
                     hm &= hm - 1;
                     const int xk = __shfl(xl, hl[k] < 0 ? 0 : hl[k], GC_WAVE);
-                    hb[k] = g.hbits + (long long)(hl[k] < 0 ? 0 : xk) * g.hbits_w;
+                    hbx[k] = hl[k] < 0 ? 0 : xk;
                     mx[k] = hl[k] < 0 ? 0 : -1;
                 }
                 for (int t0 = 0; t0 < hwords; t0 += GC_WAVE) {  // a zero bit lies in range
                     const int t = t0 + lane;
                     unsigned wd[GC_PH_B];
 #pragma unroll
-                    for (int k = 0; k < GC_PH_B; ++k) wd[k] = (mx[k] < 0 && t < hwords) ? hb[k][t] : 0xFFFFFFFFu;
+                    for (int k = 0; k < GC_PH_B; ++k) wd[k] = (mx[k] < 0 && t < hwords) ? *gc_hbw(g, hbx[k], t) : 0xFFFFFFFFu;
                     bool done = true;
 #pragma unroll
                     for (int k = 0; k < GC_PH_B; ++k) {
@@ -532,11 +530,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
             const int d = v >= 0 ? g.deg[v] : 0;
             long long mex = -1;
             if (x >= 0) {
-                const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
                 for (int t0 = 0; t0 < words && mex < 0; t0 += 8) {
                     unsigned wd[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) wd[k] = t0 + k < words ? hb[t0 + k] : 0xFFFFFFFFu;
+                    for (int k = 0; k < 8; ++k) wd[k] = t0 + k < words ? *gc_hbw(g, x, t0 + k) : 0xFFFFFFFFu;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         if (mex < 0 && wd[k] != 0xFFFFFFFFu) mex = 32ll * (t0 + k) + __builtin_ctz(~wd[k]);
@@ -562,11 +559,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
              i += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
             const int v = L.heavy[i];
             const int x = g.hid[v];
-            const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
             long long mex = -1;
             for (int t0 = 0; t0 < words && mex < 0; t0 += GC_WAVE) {  // a zero bit lies in range
                 const int t = t0 + lane;
-                const unsigned wd = t < words ? hb[t] : 0xFFFFFFFFu;
+                const unsigned wd = t < words ? *gc_hbw(g, x, t) : 0xFFFFFFFFu;
                 const ull m = __ballot(wd != 0xFFFFFFFFu);
                 if (m) {
                     const int l = __ffsll((long long)m) - 1;
@@ -610,11 +606,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose_block(GDev g, GLists L) {
             }
             __syncthreads();
             if (maxc + 2 <= 32ll * g.hbits_w) {  // mex <= maxcolor + 1: a zero bit lies in range
-                const unsigned* hb = g.hbits + (long long)x * g.hbits_w;
                 for (int t = threadIdx.x; t < words; t += blockDim.x)
-                    if (~hb[t]) atomicMin(&s_first, t);
+                    if (~*gc_hbw(g, x, t)) atomicMin(&s_first, t);
                 __syncthreads();
-                mex = 32ll * s_first + __builtin_ctz(~hb[s_first]);
+                mex = 32ll * s_first + __builtin_ctz(~*gc_hbw(g, x, s_first));
             }
             __syncthreads();
         }

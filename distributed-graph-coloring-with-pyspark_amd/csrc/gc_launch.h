@@ -83,6 +83,8 @@ struct GDev {
     const long long* hin_rp;  // for every u: the hubs (indices) whose rows list u
     const int* hin_col;
     unsigned* hbits;          // hub x: bit c set <=> a listed neighbour is coloured c (c < 32*hub_w)
+    long long hb_stride;      //   hubs of the bitmap array: word t of hub x is hbits[t * hb_stride + x]
+                              //   (word-major, GC_HB_WMAJOR; gc_hbw)
     unsigned* hkill;          // hub x, this round: a lower-rank light neighbour it lists won its candidate
     const long long* hlow_rp; // hub x: the lower-rank HUBS its row lists (vertex ids)
     const int* hlow_col;

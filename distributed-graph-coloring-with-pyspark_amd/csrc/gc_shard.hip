@@ -58,6 +58,7 @@ static GDev shard_view(gc_shard* sh) {
     if (sh->hbits && p && p->nhub == sh->nhub && p->hub_w == sh->hub_w) {
         d.hbits_w = sh->hub_w;
         d.hbits = sh->hbits;
+        d.hb_stride = sh->nhub;
         d.hid = p->hid;
         d.hin_rp = p->hin_rp;
         d.hin_col = p->hin_col;

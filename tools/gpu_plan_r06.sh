@@ -114,6 +114,14 @@ case ${1:-} in
                  "abl:rmat24:3:2:base=-,$V"
                  "abl:rmat26:2:1:base=-,$V"
                  rounds:rmat24) ;;
+  # t: the hub bitmaps word-major (GC_HB_WMAJOR): parity (A, B, priorities, shards), A/B, round cost
+  t) V="nowm=variants/nowm/libgcolor.so"
+     exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_variant_b.py"
+                 "file:tests/test_gpu_priority.py" "file:tests/test_shard_gpu.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:3:base=-,$V"
+                 "abl:rmat26:2:2:base=-,$V"
+                 rounds:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
