@@ -205,7 +205,7 @@ int gc_alloc_run_state(gc_graph* g) {
     A(g->cand, n);
     A(g->lcur, n);
     A(g->bstat, (size_t)GC_STAT_SLOTS * 16);
-    A(g->accs, (size_t)GC_ACC_SLOTS);
+    A(g->accs, (size_t)GC_ACC_SLOTS + GC_TICK_WORDS);  // + k_commit_big's arrival tickets
     A(g->c8, n);
     A(g->c4, n / 8 + 2);
     A(g->k8, n);
@@ -385,6 +385,8 @@ struct Run {
             GC_HIP(hipMemsetAsync(g->ctl->async_abort, 0, sizeof(g->ctl->async_abort), s));
             async_par = 0;
         }
+        if (d.accs)  // k_commit_big's tickets: a launch cut short by a halt may have left arrivals
+            GC_HIP(hipMemsetAsync(d.accs + GC_ACC_SLOTS, 0, sizeof(ull) * GC_TICK_WORDS, s));
         if (debug) {
             const DevCtl& h = *g->hctl;
             fprintf(stderr, "[gc] halt=%d round=%lld U=%lld cur=%d fcnt=%llu/%llu und=%llu/%llu/%llu undh=%llu/%llu/%llu "
@@ -445,13 +447,16 @@ struct Run {
         // measured slower, R-MAT-24 172.7 -> 176.8 ms, profiles/r04/c: its workgroups then wait
         // for the arrival ticket instead of returning at once when no winner was deferred)
         const bool tclose = mode == GC_CM_ROUND && !big && (fuse || !d.big_rows) && ticket_close;
+        // graphs with big rows: k_commit_big's last workgroup closes the round (GC_CB_CLOSE, round 6;
+        // the tickets are counted per dispatch residue, gc_cb_ticket)
+        const bool bclose = mode == GC_CM_ROUND && !big && !fuse && d.big_rows && ticket_close && cb_close && d.accs;
         DevCtl* snap = mode == GC_CM_ROUND ? snap_ptr : nullptr;
         kt.begin(mode == GC_CM_INIT ? GC_K_INIT : GC_K_COMMIT);
-        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0, tclose ? snap : nullptr,
-                   tclose ? 1 : 0);
+        gcl_commit(d, L, mode, mode == GC_CM_ROUND && !tail ? -1 : nsweeps, s, big, fuse ? 1 : 0,
+                   (tclose || bclose) ? snap : nullptr, tclose ? 1 : (bclose ? 2 : 0));
         kt.end();
         if (mode == GC_CM_ROUND) snap_ptr = nullptr;
-        if (tclose) {
+        if (tclose || bclose) {
             kt.close();
             proposed = fuse;
             return;
@@ -517,6 +522,8 @@ struct Run {
     DevCtl* snap_ptr = nullptr;  // handed to the next round's k_close (or closing commit)
     // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
     const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
+    // GC_CB_CLOSE=0: graphs with big rows keep the k_close launch (A/B measurements)
+    const bool cb_close = !(getenv("GC_CB_CLOSE") && atoi(getenv("GC_CB_CLOSE")) == 0);
     int enqueue_batch(int B, int S, int slot) {
         if (core_pending) {  // between rounds: the colours it reads are a round start
             kt.begin(GC_K_OTHER);
@@ -829,7 +836,7 @@ static int color_impl(gc_graph* g, const gc_options* opt, int32_t* colors_out, i
         run.fuse_ok = !run.need_pblock() && run.d.hub_w == 0 && !(f && atoi(f) == 0);
     }
     run.d.accs = g->accs;
-    GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * GC_ACC_SLOTS, g->stream));
+    GC_HIP(hipMemsetAsync(g->accs, 0, sizeof(ull) * (GC_ACC_SLOTS + GC_TICK_WORDS), g->stream));
     cc.mark("set-up", g->stream);
     rc = run.go(colors_out, cround_out, rs);  // stats->rounds may exceed round_cap: the caller re-asks
     cc.mark("rounds", g->stream);

@@ -63,7 +63,8 @@ typedef unsigned long long ull;
 #endif
 #define GC_BLOCK_GRID 1024
 #define GC_STAT_SLOTS 256
-#define GC_ACC_SLOTS 256   // commit's winner count, summed by k_close  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
+#define GC_ACC_SLOTS 256
+#define GC_TICK_WORDS 72   // k_commit_big's arrival tickets after the winner slots: 8 residues x 8 words, top   // commit's winner count, summed by k_close  // per-class algorithmic-byte counters spread over slots (k_stat_reduce)
 // dynamic LDS words of the workgroup-per-vertex mex bitmap (128 Ki colours per window)
 #define GC_MEX_WORDS 4096
 

@@ -268,6 +268,12 @@ __device__ __forceinline__ void gc_set_cand(GDev& g, int v, long long mex) {
 #define GC_PH_B 4  // hub bitmaps read together by k_propose<1>
 #endif
 #define GC_INL_BITS (64 * GC_INL_WORDS)
+#ifndef GC_PROP_STAGE
+#define GC_PROP_STAGE 1  // k_propose: heavy-list appends staged per workgroup (round 6)
+#endif
+#ifndef GC_VPW_MIN_P
+#define GC_VPW_MIN_P 16  // k_propose<1> (small rounds): vertices per wave chunk at least (round 6)
+#endif
 #ifndef GC_PROP_HINT
 #define GC_PROP_HINT 1  // k_propose<1>: hub bitmaps read from the last proposal's word (round 6)
 #endif
@@ -286,13 +292,25 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
     __shared__ ull s_wide[INL ? GC_WAVES_PER_BLOCK : 1][INL ? GC_INL_WORDS : 1];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
+#if GC_PROP_STAGE
+    // the heavy list's appends staged in LDS, one atomic per workgroup at the end (round 6): a
+    // returning atomic per wave on the one counter cost ~11 ns each, serialised -- ~1500 waves
+    // with a hub in a 12k-vertex round, most of k_propose's 20 us
+    __shared__ int s_hstage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
+#endif
     const int lane = gc_lane();
     const int w = threadIdx.x / GC_WAVE;
     const int cur = c->cur;
     const int* __restrict__ list = L.F[cur];
     const long long cnt = (long long)c->fcnt[cur];
     const long long kbound = c->kbound;
-    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    // small rounds: at least GC_VPW_MIN_P vertices a wave chunk, so fewer waves and workgroups
+    // take part (each one's appends cost an atomic on a shared counter; round 6)
+    if (INL && vpw < GC_VPW_MIN_P) vpw = GC_VPW_MIN_P;
+#if GC_PROP_STAGE
+    GcStage hst{s_hstage[w], 0, g.list_cap, &c->loop_err, &c->halt};
+#endif
     const long long nch = gc_nchunks(cnt, vpw);
     long long lmax = -1;
     ull lfail = 0, lsum = 0, lnv = 0;
@@ -311,7 +329,11 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
         const int v = (lane < vpw && idx < cnt) ? list[idx] : -1;
         const int d = v >= 0 ? g.deg[v] : 0;
         const bool isheavy = d > g.heavy_t;
+#if GC_PROP_STAGE
+        gc_stage_push(hst, isheavy, v, L.heavy, &c->heavy_cnt);
+#else
         gc_wave_append(isheavy, v, L.heavy, &c->heavy_cnt);
+#endif
         if (g.hub_repl) {  // replicated hubs of other ranks: in this rank's lists, not in its F
             const ull xm = __ballot(isheavy && (v < g.own_lo || v >= g.own_hi));
             if (xm && gc_lane() == 0) atomicAdd(&c->xhub_cnt, (ull)__popcll(xm));
@@ -488,6 +510,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_propose(GDev g, GLists L) {
             gc_wave_sync();
         }
     }
+#if GC_PROP_STAGE
+    gc_stage_flush_block(hst, L.heavy, &c->heavy_cnt);
+#endif
     __syncthreads();
     gc_block_max(&c->maxmex, lmax, (long long*)scratch);
     gc_block_add(&c->failcnt, lfail, scratch);
@@ -1950,12 +1975,13 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 #ifndef GC_HUB_WATCH
 #define GC_HUB_WATCH 0  // the watched blocker: slower (a blocker that decided costs a trip more; profiles/r06/r)
 #endif
+template <int NG = GC_HUB_NG>
 __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, int par, ull t0, long long budget,
                                  int* spill, ull* spill_cnt, ull* hpass_out, int* s_own) {
-    constexpr int GS = GC_WAVE / GC_HUB_NG;
+    constexpr int GS = GC_WAVE / NG;
     const int lane = gc_lane();
     const int grp = lane / GS, li = lane % GS;
-    const ull gmask = ((1ull << GS) - 1ull) << (grp * GS);
+    const ull gmask = GS >= GC_WAVE ? ~0ull : ((1ull << (GS % GC_WAVE)) - 1ull) << (grp * GS);
     // this lane's hub (lane j = entry j of the slice)
     const int v = lane < nh0 ? src[lane] : -1;
     const unsigned kv = v >= 0 ? (unsigned)g.k8[v] : 0u;  // own byte
@@ -1995,7 +2021,7 @@ __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, in
         gc_wave_sync();
         if (scan) s_own[rk] = lane;  // rank -> owner lane (LDS row of this wave)
         gc_wave_sync();
-        for (int j0 = 0; j0 < ns; j0 += GC_HUB_NG) {
+        for (int j0 = 0; j0 < ns; j0 += NG) {
             // group grp takes the scanning hub of rank j0 + grp (its owner lane ol)
             const int want = j0 + grp;
             const bool has = want < ns;
@@ -2046,7 +2072,7 @@ __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, in
             }
             const unsigned f = hkill ? 1u : (out ? 1u : (block >= 0 ? 2u : 0u));
             // back to the owner lanes: lane r of rank j0 + q reads group q's leader
-            const bool mine = scan && rk >= j0 && rk < j0 + GC_HUB_NG;
+            const bool mine = scan && rk >= j0 && rk < j0 + NG;
             const int src_l = mine ? (rk - j0) * GS : lane;
             const unsigned rf = (unsigned)__shfl((int)f, src_l, GC_WAVE);
             const int rblock = __shfl(block, src_l, GC_WAVE);
@@ -2263,9 +2289,13 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
         gc_async_spill(src, nh0, L.undH[out], &c->undh_cnt[out]);
         return;
     }
-    if (GC_HUB_REG && !wide && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
+    if (GC_HUB_REG && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
         ull hp = 0;
-        gc_async_hubs_reg(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp, s_w[w].first);
+        if (wide)  // one hub, all 64 lanes on its row
+            gc_async_hubs_reg<1>(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp, s_w[w].first);
+        else
+            gc_async_hubs_reg<GC_HUB_NG>(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp,
+                                         s_w[w].first);
 #ifdef GC_A_PROF
         if (aprof) {
             atomicMax(aprof + 2, wall_clock64() - t0);
@@ -2351,6 +2381,15 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
 #endif
 #ifndef GC_COMMIT_HUB_LANES
 #define GC_COMMIT_HUB_LANES 1  // k_commit: a run of heavy entries per wave, one per lane (round 6)
+#endif
+#ifndef GC_CB_UNR
+#define GC_CB_UNR 4  // k_commit_big: entries a thread per step (round 6)
+#endif
+#ifndef GC_COMMIT_HUB_MIN
+#define GC_COMMIT_HUB_MIN 16
+#endif
+#ifndef GC_VPW_MIN_C
+#define GC_VPW_MIN_C 16
 #endif
 
 
@@ -2620,7 +2659,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     if (g.hub_w && GC_COMMIT_HUB_LANES) {
         const long long W = (long long)gridDim.x * GC_WAVES_PER_BLOCK;
         const long long wid = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w;
-        const long long per = std::min<long long>(GC_WAVE, std::max<long long>(1, (hcnt + W - 1) / W));
+        // (at least GC_COMMIT_HUB_MIN entries a run: fewer waves and workgroups hold losers, and
+        // each holding workgroup's flush is an atomic on the next frontier's counter)
+        const long long per = std::min<long long>(GC_WAVE, std::max<long long>(GC_COMMIT_HUB_MIN, (hcnt + W - 1) / W));
         for (long long i0 = wid * per; i0 < hcnt; i0 += W * per) {
             const long long i = i0 + lane;
             const int v = (lane < per && i < hcnt) ? hlist[i] : -1;
@@ -2712,8 +2753,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         if (s_acc && (mark || !big)) walk_claims(g.trp[v], g.trp[v + 1], threadIdx.x, blockDim.x);
         __syncthreads();
     }
-    // light vertices: wave chunks
-    const int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    // light vertices: wave chunks (at least GC_VPW_MIN_C vertices each, round 6: as above)
+    int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
+    if (vpw < GC_VPW_MIN_C) vpw = GC_VPW_MIN_C;
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
@@ -2862,11 +2904,46 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
 // 256 winners per tile (their row offsets prefix-summed in LDS, owner by binary search).
 // Walking the winners one after another cost ~5 dependent memory round trips per winner
 // on every workgroup: 1.8 ms for the ~400 hub winners of an R-MAT-26 round.
-__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big) {
+// tclose (round 6, GC_CB_CLOSE; the one-GPU engine's small rounds): the last workgroup closes the
+// round (k_close's work and the snapshot), found by arrival tickets counted per dispatch residue
+// (blockIdx % 8, ~1/8 of the workgroups on each of eight counters, then eight arrivals on a top
+// counter) -- round 4's single counter for 1024 workgroups cost more than the k_close it saved
+__device__ __forceinline__ bool gc_cb_ticket(ull* tick) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's counter atomics are performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned sh = blockIdx.x & 7u;
+        const ull nsh = (ull)((gridDim.x - sh + 7u) / 8u);  // workgroups of this residue
+        const ull ntop = gridDim.x < 8u ? (ull)gridDim.x : 8ull;
+        int last = 0;
+        if (atomicAdd(&tick[8 * sh], 1ull) + 1ull == nsh) {
+            gc_st(&tick[8 * sh], 0ull);  // every arrival of this residue is in
+            if (atomicAdd(&tick[64], 1ull) + 1ull == ntop) {
+                gc_st(&tick[64], 0ull);
+                last = 1;
+            }
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+__global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int mode, int allow_big, DevCtl* snap,
+                                                         int tclose) {
     DevCtl* c = g.ctl;
-    if (mode == GC_CM_ROUND && c->halt) return;
+    if (mode == GC_CM_ROUND && c->halt) {
+        if (tclose && snap && blockIdx.x == 0) gc_snap_copy(c, snap);
+        return;
+    }
     const long long nb = (long long)c->bigw_cnt;
-    if (nb == 0) return;
+    if (nb == 0) {
+        if (tclose && gc_cb_ticket(g.accs + GC_ACC_SLOTS)) {
+            gc_close_body(g, L, c, mode, 0, 0);
+            if (snap) gc_snap_copy(c, snap);
+        }
+        return;
+    }
     __shared__ int s_stage[GC_WAVES_PER_BLOCK][GC_STAGE_CAP];
     __shared__ long long s_off[GC_BLOCK + 1];  // exclusive prefix of the tile's per-winner work
     __shared__ long long s_hs[GC_BLOCK], s_ts[GC_BLOCK];
@@ -2914,6 +2991,65 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
         if (t == 0) s_off[0] = 0;
         __syncthreads();
         const long long total = s_off[tn];
+#if GC_CB_UNR > 1
+        // GC_CB_UNR entries a thread per step, their loads in flight together (round 6: one
+        // entry a step paid its dependent trips -- entry, claim word, atomic -- per entry)
+        for (long long f0 = (long long)blockIdx.x * blockDim.x * GC_CB_UNR; f0 < total; f0 += stride * GC_CB_UNR) {
+            int ent[GC_CB_UNR], kk[GC_CB_UNR];
+            bool hub[GC_CB_UNR], ok[GC_CB_UNR];
+#pragma unroll
+            for (int u = 0; u < GC_CB_UNR; ++u) {
+                const long long f = f0 + (long long)u * blockDim.x + t;
+                ok[u] = f < total;
+                int k = 0;  // max k < tn with s_off[k] <= f
+                if (ok[u]) {
+#pragma unroll
+                    for (int step = GC_BLOCK / 2; step > 0; step >>= 1)
+                        if (k + step < tn && s_off[k + step] <= f) k += step;
+                }
+                kk[u] = k;
+                const long long off = ok[u] ? f - s_off[k] : 0;
+                hub[u] = ok[u] && off < s_hl[k];
+                ent[u] = !ok[u] ? 0 : (hub[u] ? g.hin_col[s_hs[k] + off] : g.tcol[s_ts[k] + (off - s_hl[k])]);
+            }
+            // the check words first (claim word, or the hub's bitmap word), then the writes
+            unsigned* wp[GC_CB_UNR];
+            unsigned bit[GC_CB_UNR], wd[GC_CB_UNR];
+#pragma unroll
+            for (int u = 0; u < GC_CB_UNR; ++u) {
+                wp[u] = nullptr;
+                bit[u] = 0u;
+                if (ok[u]) {
+                    if (hub[u]) {
+                        const int cc = s_cc[kk[u]];
+                        if (cc < 32 * g.hbits_w) {
+                            wp[u] = gc_hbw(g, ent[u], cc >> 5);
+                            bit[u] = 1u << (cc & 31);
+                        }
+                    } else {
+                        wp[u] = g.inF + (ent[u] >> 5);
+                        bit[u] = 1u << (ent[u] & 31);
+                    }
+                }
+                wd[u] = wp[u] ? *wp[u] : 0xFFFFFFFFu;
+            }
+            bool claim[GC_CB_UNR];
+#pragma unroll
+            for (int u = 0; u < GC_CB_UNR; ++u) {
+                claim[u] = false;
+                if (!ok[u]) continue;
+                if (hub[u]) {
+                    if (g.hseen && !g.hseen[ent[u]]) g.hseen[ent[u]] = 1;  // (gc_hub_mark)
+                    if (wp[u] && !(wd[u] & bit[u])) atomicOr(wp[u], bit[u]);
+                } else if (!(wd[u] & bit[u])) {
+                    if (mark) g.mark[ent[u]] = 1;  // (gc_mark: its claim bit is clear)
+                    else claim[u] = !(atomicOr(wp[u], bit[u]) & bit[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < GC_CB_UNR; ++u) gc_stage_push(st, claim[u], ent[u], next, next_cnt);
+        }
+#else
         for (long long f0 = (long long)blockIdx.x * blockDim.x; f0 < total; f0 += stride) {
             const long long f = f0 + t;
             bool claim = false;
@@ -2934,9 +3070,14 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit_big(GDev g, GLists L, int m
             }
             gc_stage_push(st, claim, xv, next, next_cnt);
         }
+#endif
         __syncthreads();  // the tile's LDS is rewritten next
     }
     gc_stage_flush_block(st, next, next_cnt);
+    if (tclose && gc_cb_ticket(g.accs + GC_ACC_SLOTS)) {
+        gc_close_body(g, L, c, mode, 0, 0);
+        if (snap) gc_snap_copy(c, snap);
+    }
 }
 
 // Pull half of a big round (see gc_big_on): every dormant vertex -- unclaimed in inF, hence
@@ -3957,9 +4098,12 @@ void gcl_commit(const GDev& g, const GLists& L, int mode, int nsweeps, hipStream
         GC_LAUNCH(k_commit<1>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
         return;
     }
-    GC_LAUNCH(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, snap, tclose);
+    // tclose 2: k_commit_big's last workgroup closes the round (k_commit does not)
+    GC_LAUNCH(k_commit<0>, dim3(gc), dim3(GC_BLOCK), 0, s, g, L, mode, nsweeps, allow_big, tclose == 2 ? nullptr : snap,
+              tclose == 2 ? 0 : tclose);
     if (g.big_rows)  // otherwise no in-row can exceed GC_BIGROW
-        GC_LAUNCH(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big);
+        GC_LAUNCH(k_commit_big, dim3(kGridCB), dim3(GC_BLOCK), 0, s, g, L, mode, allow_big, tclose == 2 ? snap : nullptr,
+                  tclose == 2 ? 1 : 0);
 }
 void gcl_unc_compact(const GDev& g, int* list, ull* cnt, int* parent, ull* best, int grid, hipStream_t s) {
     GC_LAUNCH(k_unc_compact, dim3(grid), dim3(GC_BLOCK), 0, s, g, list, cnt, parent, best);

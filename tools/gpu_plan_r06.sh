@@ -122,6 +122,18 @@ case ${1:-} in
                  "abl:rmat24:3:3:base=-,$V"
                  "abl:rmat26:2:2:base=-,$V"
                  rounds:rmat24) ;;
+  # u: + k_propose's heavy appends staged per workgroup, minimum chunk sizes in small rounds, k_commit_big
+  #    four entries a thread, k_commit_big closing the round (GC_CB_CLOSE), the one-hub-per-wave slices
+  #    in registers: parity (A, B, priorities, shards, resume), A/B of each, round cost
+  u) V="nowm=variants/nowm/libgcolor.so,nostage=variants/nostage/libgcolor.so,vmin1=variants/vmin1/libgcolor.so"
+     V="$V,nocbu=variants/nocbu/libgcolor.so,noreg=variants/noreg/libgcolor.so"
+     exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_variant_b.py"
+                 "file:tests/test_gpu_priority.py" "file:tests/test_shard_gpu.py" "file:tests/test_gpu_resume.py"
+                 "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                 "abl:rmat24:3:2:base=-,$V"
+                 "ab:rmat24:3:base,nocbclose=GC_CB_CLOSE:0"
+                 "abl:rmat26:2:1:base=-,$V"
+                 rounds:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
