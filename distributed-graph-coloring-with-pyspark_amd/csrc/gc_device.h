@@ -82,12 +82,12 @@ __host__ __device__ __forceinline__ void gc_st(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Word t of hub x's forbidden-colour bitmap.  GC_HB_WMAJOR (round 6, the default): words are
-// stored word-major -- word t of every hub together -- so the words a round touches (its newest
-// colours' word: the pushes of the round's winners, the hubs' proposals) are a few hundred KB
-// that stay in L2, not one 64-B line per hub out of a 512-B-per-hub array (97 MB on R-MAT-24).
+// Word t of hub x's forbidden-colour bitmap.  GC_HB_WMAJOR=1 (round 6, measured and left off):
+// words stored word-major -- word t of every hub together -- so that the words a round touches
+// (its newest colours' word) are a few hundred KB; R-MAT-24 +5 ms, R-MAT-26 +1.3 ms against
+// the hub-major rows (profiles/r06/u): a big round's proposals read several words per hub.
 #ifndef GC_HB_WMAJOR
-#define GC_HB_WMAJOR 1
+#define GC_HB_WMAJOR 0
 #endif
 __device__ __forceinline__ unsigned* gc_hbw(const GDev& g, long long x, long long t) {
 #if GC_HB_WMAJOR

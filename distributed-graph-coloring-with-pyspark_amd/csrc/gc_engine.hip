@@ -522,8 +522,10 @@ struct Run {
     DevCtl* snap_ptr = nullptr;  // handed to the next round's k_close (or closing commit)
     // GC_TICKET_CLOSE=0: always a separate k_close launch (A/B measurements)
     const bool ticket_close = !(getenv("GC_TICKET_CLOSE") && atoi(getenv("GC_TICKET_CLOSE")) == 0);
-    // GC_CB_CLOSE=0: graphs with big rows keep the k_close launch (A/B measurements)
-    const bool cb_close = !(getenv("GC_CB_CLOSE") && atoi(getenv("GC_CB_CLOSE")) == 0);
+    // GC_CB_CLOSE=1: graphs with big rows close the round in k_commit_big's last workgroup instead
+    // of a k_close launch (round 6: neutral on R-MAT-24, 142.30 vs 142.26 ms, profiles/r06/u; off,
+    // so the per-round trace views keep finding one closing kernel per round)
+    const bool cb_close = getenv("GC_CB_CLOSE") && atoi(getenv("GC_CB_CLOSE")) > 0;
     int enqueue_batch(int B, int S, int slot) {
         if (core_pending) {  // between rounds: the colours it reads are a round start
             kt.begin(GC_K_OTHER);

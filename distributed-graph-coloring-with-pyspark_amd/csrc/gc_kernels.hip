@@ -2383,7 +2383,11 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
 #define GC_COMMIT_HUB_LANES 1  // k_commit: a run of heavy entries per wave, one per lane (round 6)
 #endif
 #ifndef GC_CB_UNR
-#define GC_CB_UNR 4  // k_commit_big: entries a thread per step (round 6)
+#define GC_CB_UNR 1  // k_commit_big: entries a thread per step (round 6: 4 measured slower, R-MAT-24 +2 ms,
+                     // R-MAT-26 +3.9 ms, profiles/r06/u)
+#endif
+#ifndef GC_COMMIT_FLAT
+#define GC_COMMIT_FLAT 1  // k_commit: a winner's in-row and hub list walked as one flat range (round 6)
 #endif
 #ifndef GC_COMMIT_HUB_MIN
 #define GC_COMMIT_HUB_MIN 16
@@ -2567,6 +2571,10 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     __shared__ long long s_pstart[FUSE ? GC_WAVES_PER_BLOCK : 1][GC_WAVE];
     __shared__ long long s_start[GC_WAVES_PER_BLOCK][GC_WAVE];
     __shared__ int s_cc[GC_WAVES_PER_BLOCK][GC_WAVE];
+#if GC_COMMIT_FLAT
+    __shared__ long long s_hs[FUSE ? 1 : GC_WAVES_PER_BLOCK][GC_WAVE];
+    __shared__ int s_din[FUSE ? 1 : GC_WAVES_PER_BLOCK][GC_WAVE];
+#endif
     __shared__ ull scratch[2 * GC_WAVES_PER_BLOCK];
     __shared__ int s_acc, s_accc, s_lose;
     const int lane = gc_lane();
@@ -2755,7 +2763,7 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
     }
     // light vertices: wave chunks (at least GC_VPW_MIN_C vertices each, round 6: as above)
     int vpw = gc_vpw(cnt, (long long)gridDim.x * GC_WAVES_PER_BLOCK);
-    if (vpw < GC_VPW_MIN_C) vpw = GC_VPW_MIN_C;
+    if (!FUSE && vpw < GC_VPW_MIN_C) vpw = GC_VPW_MIN_C;  // (the fused commit's graphs have no hub list)
     const long long nch = gc_nchunks(cnt, vpw);
     for (long long ch = (long long)blockIdx.x * GC_WAVES_PER_BLOCK + w; ch < nch;
          ch += (long long)gridDim.x * GC_WAVES_PER_BLOCK) {
@@ -2806,6 +2814,55 @@ __global__ void __launch_bounds__(GC_BLOCK) k_commit(GDev g, GLists L, int mode,
         }
         // losers stay in the frontier (they still have a coloured neighbour)
         push(js == GC_JP_OUT && !big, v);
+#if GC_COMMIT_FLAT
+        if (!FUSE && g.hbits_w) {
+            // the winners' in-rows (claims / marks) and hub lists (colour pushes) as ONE flat
+            // range of the wave (round 6): the two walks' loads in flight together instead of
+            // one walk after the other
+            long long hs = 0;
+            int dh = 0;
+            if (acc) {
+                hs = g.hin_rp[v];
+                dh = (int)(g.hin_rp[v + 1] - hs);
+            }
+            s_start[w][lane] = tstart;
+            s_hs[w][lane] = hs;
+            s_din[w][lane] = din;
+            s_cc[w][lane] = cc;
+            const int len = din + dh;
+            const int fincl = gc_wave_incl_scan(len);
+            const int fexcl = fincl - len;
+            const int ftotal = __shfl(fincl, GC_WAVE - 1, GC_WAVE);
+            gc_wave_sync();
+            for (int base = 0; base < ftotal; base += GC_CSLOTS * GC_WAVE) {
+                int x[GC_CSLOTS], hc[GC_CSLOTS];
+                bool ok[GC_CSLOTS], hub[GC_CSLOTS], claim[GC_CSLOTS];
+#pragma unroll
+                for (int k = 0; k < GC_CSLOTS; ++k) {
+                    const int e = base + k * GC_WAVE + lane;
+                    const int o = gc_owner(fexcl, e);
+                    const int off = e - __shfl(fexcl, o, GC_WAVE);
+                    ok[k] = e < ftotal;
+                    const int dno = s_din[w][o];
+                    hub[k] = ok[k] && off >= dno;
+                    hc[k] = s_cc[w][o];
+                    x[k] = !ok[k] ? 0 : (hub[k] ? g.hin_col[s_hs[w][o] + (off - dno)] : g.tcol[s_start[w][o] + off]);
+                }
+#pragma unroll
+                for (int k = 0; k < GC_CSLOTS; ++k) {
+                    claim[k] = false;
+                    if (!ok[k]) continue;
+                    if (hub[k]) gc_hub_mark(g, x[k], hc[k]);
+                    else if (mark) gc_mark(g, x[k]);
+                    else claim[k] = gc_claim(g.inF, x[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < GC_CSLOTS; ++k) push(claim[k], x[k]);
+            }
+            gc_wave_sync();
+            continue;
+        }
+#endif
         s_start[w][lane] = tstart;
         const int incl = gc_wave_incl_scan(din);
         const int excl = incl - din;

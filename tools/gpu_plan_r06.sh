@@ -134,6 +134,22 @@ case ${1:-} in
                  "ab:rmat24:3:base,nocbclose=GC_CB_CLOSE:0"
                  "abl:rmat26:2:1:base=-,$V"
                  rounds:rmat24) ;;
+  # v: the defaults u chose (hub-major bitmaps, k_commit_big one entry a step, k_close kept): parity, A/B
+  #    against round 5's kernels (variants/r5) on every bench workload, the word-major bitmaps again, round cost
+  v) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py"
+                 "abl:rmat24:3:2:base=-,wm=variants/wm/libgcolor.so,r5=variants/r5/libgcolor.so"
+                 "abl:rmat26:2:1:base=-,r5=variants/r5/libgcolor.so"
+                 "abl:uniform10M:5:1:base=-,r5=variants/r5/libgcolor.so"
+                 "abl:mesh512:3:1:base=-,r5=variants/r5/libgcolor.so"
+                 rounds:rmat24) ;;
+  # w: + a winner's in-row and hub list as one flat walk in k_commit (GC_COMMIT_FLAT), the minimum chunk
+  #    only for the unfused commit: parity, A/B, the other workloads against round 5's kernels, round cost
+  w) exec_steps=("file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py" "file:tests/test_gpu_priority.py"
+                 "abl:rmat24:3:2:base=-,noflat=variants/noflat/libgcolor.so,r5=variants/r5/libgcolor.so"
+                 "abl:rmat26:2:1:base=-,noflat=variants/noflat/libgcolor.so"
+                 "abl:uniform10M:5:2:base=-,r5=variants/r5/libgcolor.so"
+                 "abl:mesh512:3:2:base=-,r5=variants/r5/libgcolor.so"
+                 rounds:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
