@@ -2387,7 +2387,8 @@ __device__ __forceinline__ bool gc_claim_direct(unsigned* inF, int x) {
                      // R-MAT-26 +3.9 ms, profiles/r06/u)
 #endif
 #ifndef GC_COMMIT_FLAT
-#define GC_COMMIT_FLAT 1  // k_commit: a winner's in-row and hub list walked as one flat range (round 6)
+#define GC_COMMIT_FLAT 0  // k_commit: a winner's in-row and hub list walked as one flat range (round 6:
+                          // measured slower, R-MAT-24 +1 ms, R-MAT-26 +4.6 ms, profiles/r06/w)
 #endif
 #ifndef GC_COMMIT_HUB_MIN
 #define GC_COMMIT_HUB_MIN 16

@@ -150,6 +150,9 @@ case ${1:-} in
                  "abl:uniform10M:5:2:base=-,r5=variants/r5/libgcolor.so"
                  "abl:mesh512:3:2:base=-,r5=variants/r5/libgcolor.so"
                  rounds:rmat24) ;;
+  # x: the build w chose (no flat walk): every GPU test, smoke, the asynchronous kernels' workgroups per CU
+  x) exec_steps=(tests smoke "ab:rmat24:3:base,bpc3=GC_ASYNC_BPC:3,bpc4=GC_ASYNC_BPC:4"
+                 "ab:rmat26:2:base,bpc3=GC_ASYNC_BPC:3") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
