@@ -153,6 +153,9 @@ case ${1:-} in
   # x: the build w chose (no flat walk): every GPU test, smoke, the asynchronous kernels' workgroups per CU
   x) exec_steps=(tests smoke "ab:rmat24:3:base,bpc3=GC_ASYNC_BPC:3,bpc4=GC_ASYNC_BPC:4"
                  "ab:rmat26:2:base,bpc3=GC_ASYNC_BPC:3") ;;
+  # y / z: rocprofv3 summaries of the final build (bench line, kernel trace, FETCH_SIZE / WRITE_SIZE passes)
+  y) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B") ;;
+  z) exec_steps=(profile:rmat26 profile:rmat28) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
