@@ -155,7 +155,10 @@ case ${1:-} in
                  "ab:rmat26:2:base,bpc3=GC_ASYNC_BPC:3") ;;
   # y / z: rocprofv3 summaries of the final build (bench line, kernel trace, FETCH_SIZE / WRITE_SIZE passes)
   y) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B") ;;
-  z) exec_steps=(profile:rmat26 "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768,t1024=GC_HUB_T:1024" profile:rmat28) ;;
+  z) exec_steps=(profile:rmat26 "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768,t1024=GC_HUB_T:1024") ;;
+  z2) exec_steps=(profile:rmat28) ;;
+  # fin: the default bench line of the final build (the committed profiles/pmc summaries in use) and smoke
+  fin) exec_steps=(smoke bench:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
