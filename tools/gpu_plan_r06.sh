@@ -156,9 +156,13 @@ case ${1:-} in
   # y / z: rocprofv3 summaries of the final build (bench line, kernel trace, FETCH_SIZE / WRITE_SIZE passes)
   y) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B") ;;
   z) exec_steps=(profile:rmat26 "ab:rmat24:3:base,t384=GC_HUB_T:384,t768=GC_HUB_T:768,t1024=GC_HUB_T:1024") ;;
-  z2) exec_steps=(profile:rmat28) ;;
+  z2) exec_steps=("profile:rmat28:--no-cpu-baseline,--no-north-star,--no-variant-b") ;;  # (the CPU leg on R-MAT-28 prints nothing for > 3 min)
   # fin: the default bench line of the final build (the committed profiles/pmc summaries in use) and smoke
   fin) exec_steps=(smoke bench:rmat24) ;;
+  # ab2: minimum chunks for the round's first sweep (k_resolve) and 32 for propose / commit (variants built
+  #    from a scratch copy of the sources with -DGC_VPW_MIN_R / _P / _C)
+  ab2) V="vr16=variants/vr16/libgcolor.so,vm32=variants/vm32/libgcolor.so,vm32r16=variants/vm32r16/libgcolor.so"
+       exec_steps=("abl:rmat24:3:2:base=-,$V" "abl:rmat26:2:1:base=-,$V") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
