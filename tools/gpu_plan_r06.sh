@@ -163,6 +163,8 @@ case ${1:-} in
   #    from a scratch copy of the sources with -DGC_VPW_MIN_R / _P / _C)
   ab2) V="vr16=variants/vr16/libgcolor.so,vm32=variants/vm32/libgcolor.so,vm32r16=variants/vm32r16/libgcolor.so"
        exec_steps=("abl:rmat24:3:2:base=-,$V" "abl:rmat26:2:1:base=-,$V") ;;
+  z3) exec_steps=("profile:uniform10M:--no-cpu-baseline,--no-north-star,--no-variant-b"
+                  "profile:mesh512:--no-cpu-baseline,--no-north-star,--no-variant-b") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
