@@ -1966,6 +1966,9 @@ __device__ __forceinline__ void gc_async_spill(const int* src, int cnt, int* out
 // The decisions are the resumable scan's (same cursor, same prefix, same flags); the cursor
 // and prefix words are stored as that pass stores them, so host sweeps after a give-up
 // resume from them.  Returns the hubs still pending when the wave stops (spilled by it).
+#ifndef GC_HUB_WIN
+#define GC_HUB_WIN 1
+#endif
 #ifndef GC_HUB_WIDE
 #define GC_HUB_WIDE 1
 #endif
@@ -2119,6 +2122,101 @@ __device__ int gc_async_hubs_reg(GDev& g, const int* src, int nh0, DevCtl* c, in
     }
     *hpass_out = hpass;
     return 0;
+}
+
+// One hub per wave (GC_HUB_WIDE), its words in registers and its row window too (GC_HUB_WIN,
+// round 6): a scan that stopped at an undecided same-candidate entry keeps the 512 entries it
+// loaded (8 a lane), and the next pass re-gathers their hub words from the window's start --
+// the entries before the blocker were coloured, OUT or of another candidate, final within the
+// launch, so they read as not blocking again -- one dependent trip a pass instead of two
+// (the row entries, then their hub words).  The decisions and the stored cursor / prefix are
+// the resumable scan's.
+__device__ void gc_async_hub_win(GDev& g, const int* src, int nh0, DevCtl* c, int par, ull t0, long long budget,
+                                 int* spill, ull* spill_cnt, ull* hpass_out) {
+    constexpr int STEP = GC_HUB_UNR * GC_WAVE;
+    const int lane = gc_lane();
+    *hpass_out = 0;
+    if (nh0 <= 0) return;
+    const int v = src[0];
+    const unsigned kv = (unsigned)g.k8[v];  // own byte
+    const int cb = g.cand[v];
+    const int x = g.hid[v];
+    if (x < 0) return;  // no hub (cannot happen while the hub JP is on): dropped, as gc_async_hub_pass does
+    const int cv = gc_k8_cand(kv) == GC_K8_BIG ? cb : (int)gc_k8_cand(kv);
+    const bool kill = gc_ald32(g.hkill + x) != 0u;
+    const long long base = g.hlow_rp[x];
+    const int full = (int)(g.hlow_rp[x + 1] - base);
+    const int cursor = g.hpc[x];
+    bool first = g.hcur[x] == 0;
+    const int hstart = g.hlen[x];
+    const int* __restrict__ row = g.hlow_col + base;
+    int pos = first ? hstart : cursor;
+    int u[GC_HUB_UNR];
+    int wlo = -1;  // the window holds row[wlo + k * 64 + lane] in u[k] (or -1 past the row)
+    ull hpass = 0;
+    int idle = 0;
+    unsigned f = 1u;  // killed: OUT
+    if (!kill) {
+        for (;;) {
+            ++hpass;
+            bool out = false, prefix = first;
+            int block = -1, nstart = full;
+            int p = pos;
+            while (!out && block < 0 && p < full) {
+                if (wlo < 0 || p < wlo || p >= wlo + STEP) {  // a new window from p
+                    wlo = p;
+#pragma unroll
+                    for (int k = 0; k < GC_HUB_UNR; ++k) {
+                        const int e = wlo + k * GC_WAVE + lane;
+                        u[k] = e < full ? row[e] : -1;
+                    }
+                }
+                unsigned ku[GC_HUB_UNR];
+#pragma unroll
+                for (int k = 0; k < GC_HUB_UNR; ++k) {
+                    const int e = wlo + k * GC_WAVE + lane;
+                    ku[k] = (u[k] >= 0 && e >= p) ? gc_ald32(g.hk + u[k]) : GC_HK_COLOURED;
+                }
+#pragma unroll
+                for (int k = 0; k < GC_HUB_UNR; ++k) {
+                    const unsigned fl = ku[k] != GC_HK_COLOURED ? gc_jp_flag_h(g, u[k], ku[k], 0u, cv) : 0u;
+                    if (__ballot(fl == 1u)) out = true;
+                    const ull mb = __ballot(fl == 2u);
+                    if (mb && block < 0) block = wlo + k * GC_WAVE + __builtin_ctzll(mb);
+                    const ull ml = __ballot(u[k] >= 0 && ku[k] != GC_HK_COLOURED);
+                    if (prefix && ml) {  // first non-coloured entry: the end of the coloured prefix
+                        nstart = wlo + k * GC_WAVE + __builtin_ctzll(ml);
+                        prefix = false;
+                    }
+                }
+                if (!out && block < 0) p = wlo + STEP;
+            }
+            if (lane == 0 && first) {
+                g.hcur[x] = 1;
+                if (nstart > hstart) g.hlen[x] = nstart;
+            }
+            first = false;
+            f = out ? 1u : (block >= 0 ? 2u : 0u);
+            if (f != 2u) break;
+            if (lane == 0) g.hpc[x] = block;
+            pos = block;
+            if (gc_async_stop(c, par, t0, budget)) {
+                ull b = 0;
+                if (lane == 0) b = atomicAdd(spill_cnt, 1ull);
+                b = __shfl(b, 0, GC_WAVE);
+                if (lane == 0) spill[b] = v;
+                *hpass_out = hpass;
+                return;
+            }
+            if (++idle > 2) __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    if (lane == 0) {
+        const unsigned st = (f & 1u) ? GC_JP_OUT : GC_JP_IN;
+        gc_ast8(g.k8 + v, (kv & ~3u) | st);
+        gc_ast32(g.hk + x, gc_hk((unsigned)cv, st));
+    }
+    *hpass_out = hpass;
 }
 
 // The launch after sweep S (k_resolve = 0, or the last host sweep): reads slot S % 3,
@@ -2291,7 +2389,9 @@ __global__ void __launch_bounds__(GC_BLOCK) k_sweep_async(GDev g, GLists L, int 
     }
     if (GC_HUB_REG && nh0 <= GC_WAVE) {  // the slice's words in registers (gc_async_hubs_reg)
         ull hp = 0;
-        if (wide)  // one hub, all 64 lanes on its row
+        if (wide && GC_HUB_WIN)  // one hub, all 64 lanes on its row, the row window kept
+            gc_async_hub_win(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp);
+        else if (wide)  // one hub, all 64 lanes on its row
             gc_async_hubs_reg<1>(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp, s_w[w].first);
         else
             gc_async_hubs_reg<GC_HUB_NG>(g, src, nh0, c, par, t0, budget, L.undH[out], &c->undh_cnt[out], &hp,

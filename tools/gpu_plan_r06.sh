@@ -165,6 +165,15 @@ case ${1:-} in
        exec_steps=("abl:rmat24:3:2:base=-,$V" "abl:rmat26:2:1:base=-,$V") ;;
   z3) exec_steps=("profile:uniform10M:--no-cpu-baseline,--no-north-star,--no-variant-b"
                   "profile:mesh512:--no-cpu-baseline,--no-north-star,--no-variant-b") ;;
+  # win: one hub per wave with its row window kept across passes (a scratch-copy build, variants/win):
+  #    parity with that build, then A/B against the final build
+  win) exec_steps=(env:GC_LIB_PATH=variants/win/libgcolor.so "file:tests/test_gpu_hubs.py" "file:tests/test_gpu_parity.py"
+                   "file:tests/test_gpu_core.py" "file:tests/test_gpu_fullsize.py:c3_rmat24_against_single_thread_oracle~or~c3_rmat24_hubs_match"
+                   env:GC_LIB_PATH= "abl:rmat24:3:2:base=-,win=variants/win/libgcolor.so"
+                   "abl:rmat26:2:1:base=-,win=variants/win/libgcolor.so") ;;
+  # fin2a / fin2b: the final build (with GC_HUB_WIN) profiled again, its default bench line
+  fin2a) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B") ;;
+  fin2b) exec_steps=(profile:rmat26 smoke bench:rmat24) ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
