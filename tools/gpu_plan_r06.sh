@@ -174,6 +174,9 @@ case ${1:-} in
   # fin2a / fin2b: the final build (with GC_HUB_WIN) profiled again, its default bench line
   fin2a) exec_steps=(profile:rmat24 "profile:rmat24:--variant,B") ;;
   fin2b) exec_steps=(profile:rmat26 smoke bench:rmat24) ;;
+  fin3) exec_steps=(tests smoke) ;;
+  fin4) exec_steps=("profile:rmat28:--no-cpu-baseline,--no-north-star,--no-variant-b"
+                    "profile:uniform10M:--no-cpu-baseline,--no-north-star,--no-variant-b") ;;
   *) echo "usage: $0 a|..." >&2; exit 2 ;;
 esac
 bash tools/gpu_session.sh "r06$1" "${exec_steps[@]}"
